@@ -1,0 +1,260 @@
+// Batch normalisation + (leaky) ReLU over the active sites of a sparse tensor.
+//
+// Semantics follow SCN's BatchNormalization with leakiness (SURVEY.md §8(a)
+// a10; scn.BatchNormReLU / BatchNormLeakyReLU at models/SparseConvNet.py:69,
+// 86,103,116,...): train mode normalises with the batch mean and BIASED
+// variance over the V rows, eps inside the sqrt, and updates
+//   running_mean = momentum*running_mean + (1-momentum)*mean
+//   running_var  = momentum*running_var  + (1-momentum)*var*V/(V-1)
+// eval mode uses the running statistics.  y = max(z, 0) + leak*min(z, 0) with
+// z = ((x - mean_hi) - mean_lo)*scale + shift, scale = invstd*weight,
+// shift = bias.  The fp64 mean is carried as an fp32 hi/lo pair and
+// subtracted before scaling: folding it into the shift (or rounding it to
+// fp32) moves z by ulp(mean)*invstd, which for low-variance channels far from
+// zero is many ulps of z and flips ReLU decisions.
+//
+// Per-channel statistics live in one float array stats[5][C]:
+//   [0] mean_hi  [1] mean_lo  [2] invstd  [3] scale  [4] shift
+//
+// Reductions accumulate in fp64 per block and are combined in block order,
+// so results are deterministic and the 65 stacked BN layers of the headline
+// UNet do not drift from an fp64 reference.
+#include "msp_common.h"
+
+namespace msp {
+
+constexpr int kT = 256;
+constexpr int64_t kMaxParts = 1024;
+
+__host__ __device__ inline int64_t bn_parts(int64_t V) {
+  int64_t p = (V + 255) / 256;
+  return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
+}
+
+struct BnStats {
+  const float *mh, *ml, *is, *sc, *sh;
+  __host__ __device__ BnStats(const float* st, int C)
+      : mh(st), ml(st + C), is(st + 2 * C), sc(st + 3 * C), sh(st + 4 * C) {}
+  __device__ float centred(float x, int c) const { return (x - mh[c]) - ml[c]; }
+  __device__ float z(float x, int c) const { return centred(x, c) * sc[c] + sh[c]; }
+};
+
+// MODE 0: (sum x, sum x^2).  MODE 1: (sum dz, sum dz*xhat).
+template <int MODE>
+__global__ __launch_bounds__(kT) void bn_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                       int64_t V, int C, const float* __restrict__ stats,
+                                                       float leak, double* __restrict__ partial) {
+  const int64_t P = gridDim.x;
+  const int64_t per = (V + P - 1) / P;
+  const int64_t v0 = blockIdx.x * per, v1 = min(V, v0 + per);
+  const int t = threadIdx.x;
+  double* out0 = partial + (int64_t)blockIdx.x * 2 * C;
+  double* out1 = out0 + C;
+  const BnStats st(stats, C);
+  auto term = [&](int64_t v, int c, double& s0, double& s1) {
+    const float xv = x[v * C + c];
+    if (MODE == 0) {
+      s0 += xv;
+      s1 += (double)xv * xv;
+    } else {
+      const float g = dy[v * C + c];
+      const float dz = st.z(xv, c) > 0.f ? g : g * leak;
+      s0 += dz;
+      s1 += (double)dz * ((double)st.centred(xv, c) * st.is[c]);
+    }
+  };
+  if (C <= kT) {
+    __shared__ double red0[kT], red1[kT];
+    const int R = kT / C;
+    const int ro = t / C, c = t % C;
+    double s0 = 0.0, s1 = 0.0;
+    if (ro < R)
+      for (int64_t v = v0 + ro; v < v1; v += R) term(v, c, s0, s1);
+    red0[t] = s0;
+    red1[t] = s1;
+    __syncthreads();
+    if (t < C) {
+      double a = 0.0, b = 0.0;
+      for (int k = 0; k < R; ++k) {
+        a += red0[k * C + t];
+        b += red1[k * C + t];
+      }
+      out0[t] = a;
+      out1[t] = b;
+    }
+  } else {
+    for (int c = t; c < C; c += kT) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int64_t v = v0; v < v1; ++v) term(v, c, s0, s1);
+      out0[c] = s0;
+      out1[c] = s1;
+    }
+  }
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ partial, int64_t P, int C, int64_t V, double eps,
+                                   double momentum, int train, float* __restrict__ rmean,
+                                   float* __restrict__ rvar, const float* __restrict__ weight,
+                                   const float* __restrict__ bias, float* __restrict__ stats) {
+  for (int c = threadIdx.x + blockIdx.x * blockDim.x; c < C; c += blockDim.x * gridDim.x) {
+    double mu, var;
+    if (train) {
+      double s = 0.0, ss = 0.0;
+      for (int64_t p = 0; p < P; ++p) {
+        s += partial[p * 2 * C + c];
+        ss += partial[p * 2 * C + C + c];
+      }
+      mu = V > 0 ? s / (double)V : 0.0;
+      var = V > 0 ? ss / (double)V - mu * mu : 0.0;
+      if (var < 0.0) var = 0.0;
+      const double unb = V > 1 ? var * (double)V / (double)(V - 1) : var;
+      rmean[c] = (float)(momentum * rmean[c] + (1.0 - momentum) * mu);
+      rvar[c] = (float)(momentum * rvar[c] + (1.0 - momentum) * unb);
+    } else {
+      mu = rmean[c];
+      var = rvar[c];
+    }
+    const double is = 1.0 / sqrt(var + eps);
+    const double w = weight ? weight[c] : 1.0, b = bias ? bias[c] : 0.0;
+    const float hi = (float)mu;
+    stats[c] = hi;
+    stats[C + c] = (float)(mu - (double)hi);
+    stats[2 * C + c] = (float)is;
+    stats[3 * C + c] = (float)(w * is);
+    stats[4 * C + c] = (float)b;
+  }
+}
+
+__global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ x, int64_t n, int C,
+                                                      const float* __restrict__ stats, float leak,
+                                                      float* __restrict__ y) {
+  const int64_t stride = (int64_t)gridDim.x * kT;
+  const BnStats st(stats, C);
+  if ((C & 3) == 0) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n4; i += stride) {
+      const float4 v = reinterpret_cast<const float4*>(x)[i];
+      const int c = (int)((i * 4) % C);
+      float4 o;
+      o.x = st.z(v.x, c);
+      o.y = st.z(v.y, c + 1);
+      o.z = st.z(v.z, c + 2);
+      o.w = st.z(v.w, c + 3);
+      o.x = o.x > 0.f ? o.x : o.x * leak;
+      o.y = o.y > 0.f ? o.y : o.y * leak;
+      o.z = o.z > 0.f ? o.z : o.z * leak;
+      o.w = o.w > 0.f ? o.w : o.w * leak;
+      reinterpret_cast<float4*>(y)[i] = o;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
+      const float z = st.z(x[i], (int)(i % C));
+      y[i] = z > 0.f ? z : z * leak;
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ partial, int64_t P, int C,
+                                       float* __restrict__ dweight, float* __restrict__ dbias,
+                                       double* __restrict__ sums) {
+  for (int c = threadIdx.x + blockIdx.x * blockDim.x; c < C; c += blockDim.x * gridDim.x) {
+    double a = 0.0, b = 0.0;
+    for (int64_t p = 0; p < P; ++p) {
+      a += partial[p * 2 * C + c];
+      b += partial[p * 2 * C + C + c];
+    }
+    sums[c] = a;      // sum dz
+    sums[C + c] = b;  // sum dz * xhat
+    if (dbias) dbias[c] = (float)a;
+    if (dweight) dweight[c] = (float)b;
+  }
+}
+
+__global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ dy, int64_t n, int C,
+                                                          int64_t V, const double* __restrict__ sums,
+                                                          const float* __restrict__ stats,
+                                                          const float* __restrict__ weight, float leak, int train,
+                                                          float* __restrict__ dx) {
+  const int64_t stride = (int64_t)gridDim.x * kT;
+  const double invV = V > 0 ? 1.0 / (double)V : 0.0;
+  const BnStats st(stats, C);
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % C);
+    const float xv = x[i];
+    const float g = dy[i];
+    const float dz = st.z(xv, c) > 0.f ? g : g * leak;
+    const float w = weight ? weight[c] : 1.f;
+    if (train) {
+      const float xh = st.centred(xv, c) * st.is[c];
+      const float mdz = (float)(sums[c] * invV), mdzx = (float)(sums[C + c] * invV);
+      dx[i] = w * st.is[c] * (dz - mdz - xh * mdzx);
+    } else {
+      dx[i] = w * st.is[c] * dz;
+    }
+  }
+}
+
+inline unsigned ew_grid(int64_t n) {
+  int64_t g = (n + kT - 1) / kT;
+  if (g > 4096) g = 4096;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+}  // namespace msp
+
+using namespace msp;
+
+extern "C" {
+
+int64_t msp_bn_partials(int64_t V, int C) {
+  (void)C;
+  return bn_parts(V);
+}
+
+int msp_bn_stats(const float* x, int64_t V, int C, double* partial, msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_stats: bad shape");
+  bn_reduce_kernel<0><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
+                                                                           partial);
+  return check_launch("msp_bn_stats");
+}
+
+int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double momentum, int train,
+                    float* running_mean, float* running_var, const float* weight, const float* bias, float* stats,
+                    msp_stream_t stream) {
+  MSP_REQUIRE(C > 0, "msp_bn_finalize: bad C");
+  bn_finalize_kernel<<<(unsigned)ceil_div(C, 256), 256, 0, as_stream(stream)>>>(
+      partial, bn_parts(V), C, V, eps, momentum, train, running_mean, running_var, weight, bias, stats);
+  return check_launch("msp_bn_finalize");
+}
+
+int msp_bn_apply(const float* x, int64_t V, int C, const float* stats, float leak, float* y, msp_stream_t stream) {
+  const int64_t n = V * C;
+  if (n == 0) return MSP_OK;
+  bn_apply_kernel<<<ew_grid(n / 4 + 1), kT, 0, as_stream(stream)>>>(x, n, C, stats, leak, y);
+  return check_launch("msp_bn_apply");
+}
+
+int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const float* stats, float leak,
+                     double* partial, msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_bwd_stats: bad shape");
+  bn_reduce_kernel<1><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
+  return check_launch("msp_bn_bwd_stats");
+}
+
+int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,
+                     const float* weight, float leak, int train, float* dx, float* dweight, float* dbias,
+                     msp_stream_t stream) {
+  hipStream_t s = as_stream(stream);
+  // The combined per-channel sums go to the extra 2*C doubles at the tail of
+  // the partial buffer (it holds (P + 1) * 2 * C doubles, see the header).
+  double* sums = const_cast<double*>(partial) + bn_parts(V) * 2 * C;
+  bn_bwd_finalize_kernel<<<(unsigned)ceil_div(C, 256), 256, 0, s>>>(partial, bn_parts(V), C, dweight, dbias,
+                                                                    sums);
+  const int64_t n = V * C;
+  if (n > 0)
+    bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, dx);
+  return check_launch("msp_bn_bwd_apply");
+}
+
+}  // extern "C"

@@ -1,0 +1,430 @@
+// Metadata on the device: voxel keys, dedup, hash grid, submanifold neighbour
+// maps, strided child maps and the two rulebook forms the convolutions use.
+//
+// What this replaces: SparseConvNet builds the same structures on the HOST
+// (per-sample hash maps + OpenMP) inside `scn.InputLayer` and lazily in the
+// first convolution of each spatial size, then copies the rules to the device
+// per call.  Here everything stays in HBM.
+#include "msp_common.h"
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+namespace msp {
+
+constexpr int kThreads = 256;
+
+// ---------------------------------------------------------------- keys
+__global__ __launch_bounds__(kThreads) void point_keys_kernel(const int64_t* __restrict__ coords, int64_t n,
+                                                              int64_t stride, int log2s, int64_t size,
+                                                              uint64_t* __restrict__ keys,
+                                                              int32_t* __restrict__ vals,
+                                                              int64_t* __restrict__ stats) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  bool bad = false;
+  int64_t b = 0;
+  if (i < n) {
+    const int64_t* c = coords + i * stride;
+    const int64_t x = c[0], y = c[1], z = c[2];
+    b = c[3];
+    bad = x < 0 || y < 0 || z < 0 || x >= size || y >= size || z >= size || b < 0;
+    keys[i] = bad ? kEmptyKey : make_key(b, x, y, z, log2s);
+    vals[i] = (int32_t)i;
+  }
+  // one atomic per wave
+  const unsigned long long badm = ballot64(bad);
+  int64_t bmax = (i < n && !bad) ? b : 0;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) bmax = max(bmax, (int64_t)__shfl_xor(bmax, d, 64));
+  if ((threadIdx.x & 63) == 0) {
+    if (badm) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)__popcll(badm));
+    atomicMax((unsigned long long*)&stats[1], (unsigned long long)bmax);
+  }
+}
+
+// ---------------------------------------------------------------- segment
+constexpr int kSegItems = 8;
+constexpr int kSegTile = kThreads * kSegItems;
+
+__device__ inline bool seg_flag(const uint64_t* k, int64_t i, int shift) {
+  return i == 0 || (k[i] >> shift) != (k[i - 1] >> shift);
+}
+
+__global__ __launch_bounds__(kThreads) void seg_count_kernel(const uint64_t* __restrict__ k, int64_t n,
+                                                             int shift, int64_t* __restrict__ block_sums) {
+  const int64_t base = (int64_t)blockIdx.x * kSegTile + (int64_t)threadIdx.x * kSegItems;
+  int64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kSegItems; ++j) {
+    const int64_t i = base + j;
+    if (i < n) c += seg_flag(k, i, shift);
+  }
+  int64_t tot;
+  block_excl_scan<kThreads>(c, &tot);
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kThreads) void seg_apply_kernel(
+    const uint64_t* __restrict__ k, int64_t n, int shift, const int64_t* __restrict__ block_off,
+    const int32_t* __restrict__ perm, int32_t* __restrict__ seg_of, int32_t* __restrict__ p2v,
+    uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start) {
+  const int64_t base = (int64_t)blockIdx.x * kSegTile + (int64_t)threadIdx.x * kSegItems;
+  bool f[kSegItems];
+  int64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kSegItems; ++j) {
+    const int64_t i = base + j;
+    f[j] = (i < n) && seg_flag(k, i, shift);
+    c += f[j];
+  }
+  int64_t tot;
+  int64_t g = block_excl_scan<kThreads>(c, &tot) + block_off[blockIdx.x] - 1;  // group of the previous row
+#pragma unroll
+  for (int j = 0; j < kSegItems; ++j) {
+    const int64_t i = base + j;
+    if (i >= n) break;
+    if (f[j]) {
+      ++g;
+      uniq[g] = k[i] >> shift;
+      seg_start[g] = (int32_t)i;
+    }
+    seg_of[i] = (int32_t)g;
+    if (p2v) p2v[perm[i]] = (int32_t)g;
+    if (i == n - 1) seg_start[g + 1] = (int32_t)n;
+  }
+}
+
+// ---------------------------------------------------------------- hash grid
+__global__ __launch_bounds__(kThreads) void hash_build_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                              uint64_t* __restrict__ tkeys,
+                                                              int32_t* __restrict__ tvals, uint64_t mask) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t key = keys[i];
+  uint64_t h = hash_key(key) & mask;
+  for (;;) {
+    const unsigned long long prev =
+        atomicCAS((unsigned long long*)&tkeys[h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+    if (prev == kEmptyKey) {
+      tvals[h] = (int32_t)i;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                            int log2s, int64_t size, int f,
+                                                            const uint64_t* __restrict__ tkeys,
+                                                            const int32_t* __restrict__ tvals, uint64_t mask,
+                                                            int32_t* __restrict__ nbr) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  int64_t b, x, y, z;
+  split_key(keys[i], log2s, b, x, y, z);
+  const int h = f / 2;
+  int o = 0;
+  for (int dx = -h; dx <= h; ++dx) {
+    const int64_t xx = x + dx;
+    for (int dy = -h; dy <= h; ++dy) {
+      const int64_t yy = y + dy;
+      for (int dz = -h; dz <= h; ++dz, ++o) {
+        const int64_t zz = z + dz;
+        int32_t v = -1;
+        if (dx == 0 && dy == 0 && dz == 0) {
+          v = (int32_t)i;
+        } else if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size) {
+          v = hash_find(tkeys, tvals, mask, make_key(b, xx, yy, zz, log2s));
+        }
+        nbr[(int64_t)o * n + i] = v;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void down_map_kernel(const uint64_t* __restrict__ keys, int64_t n_fine,
+                                                            const int32_t* __restrict__ parent, int log2s,
+                                                            int ls, int32_t* __restrict__ down,
+                                                            int64_t n_coarse) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n_fine) return;
+  int64_t b, x, y, z;
+  split_key(keys[i], log2s, b, x, y, z);
+  const int64_t m = (1 << ls) - 1;
+  const int o = (int)((((x & m) << ls) + (y & m)) << ls) + (int)(z & m);
+  down[(int64_t)o * n_coarse + parent[i]] = (int32_t)i;
+}
+
+// ---------------------------------------------------------------- pair lists
+// Stable per-offset compaction of an offset-major map.  One block handles
+// kSegTile consecutive rows of one offset.
+__global__ __launch_bounds__(kThreads) void pair_count_kernel(const int32_t* __restrict__ map, int64_t n,
+                                                              int64_t nrb, int64_t* __restrict__ counts) {
+  const int o = blockIdx.y;
+  const int64_t base = (int64_t)blockIdx.x * kSegTile + (int64_t)threadIdx.x * kSegItems;
+  const int32_t* row = map + (int64_t)o * n;
+  int64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kSegItems; ++j) {
+    const int64_t i = base + j;
+    if (i < n) c += row[i] >= 0;
+  }
+  int64_t tot;
+  block_excl_scan<kThreads>(c, &tot);
+  if (threadIdx.x == 0) counts[(int64_t)o * nrb + blockIdx.x] = tot;
+}
+
+__global__ void pair_starts_kernel(const int64_t* __restrict__ offs, int K, int64_t nrb, const int64_t* total,
+                                   int64_t* __restrict__ off_start) {
+  const int o = threadIdx.x + blockIdx.x * blockDim.x;
+  if (o < K) off_start[o] = offs[(int64_t)o * nrb];
+  if (o == K) off_start[K] = *total;
+}
+
+__global__ __launch_bounds__(kThreads) void pair_fill_kernel(const int32_t* __restrict__ map, int64_t n,
+                                                             int64_t nrb, const int64_t* __restrict__ offs,
+                                                             int32_t* __restrict__ pin,
+                                                             int32_t* __restrict__ pout) {
+  const int o = blockIdx.y;
+  const int64_t base = (int64_t)blockIdx.x * kSegTile + (int64_t)threadIdx.x * kSegItems;
+  const int32_t* row = map + (int64_t)o * n;
+  int32_t v[kSegItems];
+  int64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kSegItems; ++j) {
+    const int64_t i = base + j;
+    v[j] = (i < n) ? row[i] : -1;
+    c += v[j] >= 0;
+  }
+  int64_t tot;
+  int64_t p = block_excl_scan<kThreads>(c, &tot) + offs[(int64_t)o * nrb + blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < kSegItems; ++j) {
+    if (v[j] >= 0) {
+      pin[p] = v[j];
+      pout[p] = (int32_t)(base + j);
+      ++p;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- tile rulebook
+// One wave per 64-row output tile.  For each filter offset the wave ballots
+// which of its rows have that neighbour, and the present rows are compacted
+// (mbcnt prefix) into 16-row chunks that share the offset.
+constexpr int kTile = MSP_TILE_ROWS;
+constexpr int kChunk = MSP_CHUNK;
+static_assert(kTile == 64, "one wave per tile");
+
+__global__ __launch_bounds__(kThreads) void tile_count_kernel(const int32_t* __restrict__ map, int K, int64_t n,
+                                                              int64_t n_tiles, int64_t* __restrict__ cnt) {
+  const int64_t t = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (t >= n_tiles) return;
+  const int64_t r = t * kTile + (threadIdx.x & 63);
+  int64_t nch = 0;
+  for (int o = 0; o < K; ++o) {
+    const bool p = r < n && map[(int64_t)o * n + r] >= 0;
+    const int pc = __popcll(ballot64(p));
+    nch += (pc + kChunk - 1) / kChunk;
+  }
+  if ((threadIdx.x & 63) == 0) cnt[t] = nch;
+}
+
+__global__ __launch_bounds__(kThreads) void tile_fill_kernel(const int32_t* __restrict__ map, int K, int64_t n,
+                                                             int64_t n_tiles,
+                                                             const int64_t* __restrict__ tile_start,
+                                                             uint8_t* __restrict__ chunk_off,
+                                                             int32_t* __restrict__ chunk_src,
+                                                             uint8_t* __restrict__ chunk_row) {
+  const int64_t t = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (t >= n_tiles) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = t * kTile + lane;
+  int64_t c = tile_start[t];
+  for (int o = 0; o < K; ++o) {
+    const int32_t v = (r < n) ? map[(int64_t)o * n + r] : -1;
+    const unsigned long long m = ballot64(v >= 0);
+    const int pc = __popcll(m);
+    if (pc == 0) continue;
+    const int nch = (pc + kChunk - 1) / kChunk;
+    if (v >= 0) {
+      const int pos = mbcnt64(m);
+      const int64_t e = (c + pos / kChunk) * kChunk + (pos % kChunk);
+      chunk_src[e] = v;
+      chunk_row[e] = (uint8_t)lane;
+    }
+    if (lane >= pc && lane < nch * kChunk) {  // padding slots of the last chunk
+      const int64_t e = (c + lane / kChunk) * kChunk + (lane % kChunk);
+      chunk_src[e] = -1;
+      chunk_row[e] = (uint8_t)kTile;
+    }
+    if (lane < nch) chunk_off[c + lane] = (uint8_t)o;
+    c += nch;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void decode_kernel(const uint64_t* __restrict__ keys, int64_t n, int log2s,
+                                                          int64_t* __restrict__ coords) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  int64_t b, x, y, z;
+  split_key(keys[i], log2s, b, x, y, z);
+  coords[4 * i + 0] = x;
+  coords[4 * i + 1] = y;
+  coords[4 * i + 2] = z;
+  coords[4 * i + 3] = b;
+}
+
+inline unsigned grid1(int64_t n) { return (unsigned)ceil_div(n > 0 ? n : 1, kThreads); }
+
+}  // namespace msp
+
+using namespace msp;
+
+extern "C" {
+
+int msp_point_keys(const int64_t* coords, int64_t n, int64_t row_stride, int log2_size, int64_t spatial_size,
+                   uint64_t* keys, int32_t* vals, int64_t* stats, msp_stream_t stream) {
+  MSP_REQUIRE(n >= 0 && row_stride >= 4, "msp_point_keys: bad n/row_stride");
+  MSP_REQUIRE(log2_size >= 1 && log2_size <= 20 && (1ll << log2_size) >= spatial_size,
+              "msp_point_keys: log2_size %d does not cover spatial_size %lld", log2_size,
+              (long long)spatial_size);
+  MSP_REQUIRE(n < (1ll << 31), "msp_point_keys: too many points");
+  if (n == 0) return MSP_OK;
+  point_keys_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(coords, n, row_stride, log2_size,
+                                                                   spatial_size, keys, vals, stats);
+  return check_launch("msp_point_keys");
+}
+
+size_t msp_sort_workspace_size(int64_t n, int end_bit) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs((void*)nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                            (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0u, (unsigned)end_bit);
+  return bytes;
+}
+
+int msp_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* vals_in, int32_t* vals_out,
+                   int64_t n, int end_bit, void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(end_bit > 0 && end_bit <= 64, "msp_sort_pairs: bad end_bit %d", end_bit);
+  if (n == 0) return MSP_OK;
+  size_t need = msp_sort_workspace_size(n, end_bit);
+  MSP_REQUIRE(ws_bytes >= need, "msp_sort_pairs: workspace too small (%zu < %zu)", ws_bytes, need);
+  MSP_HIP(rocprim::radix_sort_pairs(ws, need, keys_in, keys_out, vals_in, vals_out, (size_t)n, 0u,
+                                    (unsigned)end_bit, as_stream(stream)),
+          "msp_sort_pairs");
+  return MSP_OK;
+}
+
+int msp_segment(const uint64_t* sorted_keys, int64_t n, int shift, const int32_t* perm, int32_t* seg_of,
+                int32_t* p2v, uint64_t* uniq_keys, int32_t* seg_start, int64_t* n_uniq, void* ws,
+                size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(n >= 0 && shift >= 0 && shift < 64, "msp_segment: bad args");
+  MSP_REQUIRE((p2v == nullptr) == (perm == nullptr), "msp_segment: perm and p2v go together");
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {
+    MSP_HIP(hipMemsetAsync(n_uniq, 0, sizeof(int64_t), s), "msp_segment");
+    MSP_HIP(hipMemsetAsync(seg_start, 0, sizeof(int32_t), s), "msp_segment");
+    return MSP_OK;
+  }
+  const int64_t nb = ceil_div(n, kSegTile);
+  MSP_REQUIRE(ws_bytes >= (size_t)(nb + 1) * sizeof(int64_t), "msp_segment: workspace too small");
+  int64_t* sums = reinterpret_cast<int64_t*>(ws);
+  seg_count_kernel<<<nb, kThreads, 0, s>>>(sorted_keys, n, shift, sums);
+  int rc = scan_small_inplace(sums, nb, n_uniq, s);
+  if (rc) return rc;
+  seg_apply_kernel<<<nb, kThreads, 0, s>>>(sorted_keys, n, shift, sums, perm, seg_of, p2v, uniq_keys,
+                                           seg_start);
+  return check_launch("msp_segment");
+}
+
+int64_t msp_hash_capacity(int64_t n) {
+  int64_t cap = 1024;
+  while (cap < 2 * n) cap <<= 1;
+  return cap;
+}
+
+int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* tkeys, int32_t* tvals, int64_t cap,
+                   msp_stream_t stream) {
+  MSP_REQUIRE(cap >= 2 * n && (cap & (cap - 1)) == 0, "msp_hash_build: capacity must be a power of 2 >= 2n");
+  if (n == 0) return MSP_OK;
+  hash_build_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, tkeys, tvals, (uint64_t)(cap - 1));
+  return check_launch("msp_hash_build");
+}
+
+int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
+                 const uint64_t* tkeys, const int32_t* tvals, int64_t cap, int32_t* nbr, msp_stream_t stream) {
+  MSP_REQUIRE(filter_size >= 1 && (filter_size & 1) == 1 && filter_size <= 5,
+              "msp_subm_map: filter_size must be odd and <= 5 (got %d)", filter_size);
+  MSP_REQUIRE((cap & (cap - 1)) == 0, "msp_subm_map: bad capacity");
+  if (n == 0) return MSP_OK;
+  subm_map_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, log2_size, spatial_size, filter_size,
+                                                                tkeys, tvals, (uint64_t)(cap - 1), nbr);
+  return check_launch("msp_subm_map");
+}
+
+int msp_down_map(const uint64_t* fine_keys, int64_t n_fine, const int32_t* parent_of, int log2_size_fine,
+                 int log2_stride, int32_t* down, int64_t n_coarse, msp_stream_t stream) {
+  MSP_REQUIRE(log2_stride >= 1 && log2_stride <= 2, "msp_down_map: stride must be 2 or 4");
+  const int K = 1 << (3 * log2_stride);
+  hipStream_t s = as_stream(stream);
+  MSP_HIP(hipMemsetAsync(down, 0xFF, (size_t)K * n_coarse * sizeof(int32_t), s), "msp_down_map");
+  if (n_fine == 0) return MSP_OK;
+  down_map_kernel<<<grid1(n_fine), kThreads, 0, s>>>(fine_keys, n_fine, parent_of, log2_size_fine,
+                                                     log2_stride, down, n_coarse);
+  return check_launch("msp_down_map");
+}
+
+int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32_t* pair_out, int64_t cap,
+                   int64_t* off_start, void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && K <= 65535 && n >= 0, "msp_pair_lists: bad K/n");
+  hipStream_t s = as_stream(stream);
+  const int64_t nrb = ceil_div(n > 0 ? n : 1, kSegTile);
+  const int64_t m = (int64_t)K * nrb;
+  // workspace: counts[m] | offs[m] | total | scan ws
+  const size_t need = (size_t)(2 * m + 1) * sizeof(int64_t) + scan_ws_bytes(m);
+  MSP_REQUIRE(ws_bytes >= need, "msp_pair_lists: workspace too small (%zu < %zu)", ws_bytes, need);
+  int64_t* counts = reinterpret_cast<int64_t*>(ws);
+  int64_t* offs = counts + m;
+  int64_t* total = offs + m;
+  void* sws = total + 1;
+  dim3 grid((unsigned)nrb, (unsigned)K);
+  pair_count_kernel<<<grid, kThreads, 0, s>>>(map, n, nrb, counts);
+  int rc = scan_exclusive_i64(counts, offs, m, total, sws, scan_ws_bytes(m), s);
+  if (rc) return rc;
+  pair_starts_kernel<<<(unsigned)ceil_div(K + 1, 256), 256, 0, s>>>(offs, K, nrb, total, off_start);
+  if (cap > 0) {
+    pair_fill_kernel<<<grid, kThreads, 0, s>>>(map, n, nrb, offs, pair_in, pair_out);
+  }
+  return check_launch("msp_pair_lists");
+}
+
+int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int64_t* tile_start, uint8_t* chunk_off,
+                      int32_t* chunk_src, uint8_t* chunk_row, int64_t chunk_cap, void* ws, size_t ws_bytes,
+                      msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && K <= 255 && n >= 0, "msp_tile_rulebook: K must be in [1,255]");
+  hipStream_t s = as_stream(stream);
+  const int64_t n_tiles = ceil_div(n, kTile);
+  const size_t need = (size_t)(n_tiles + 1) * sizeof(int64_t) + scan_ws_bytes(n_tiles);
+  MSP_REQUIRE(ws_bytes >= need, "msp_tile_rulebook: workspace too small (%zu < %zu)", ws_bytes, need);
+  if (n_tiles == 0) {
+    MSP_HIP(hipMemsetAsync(tile_start, 0, sizeof(int64_t), s), "msp_tile_rulebook");
+    return MSP_OK;
+  }
+  int64_t* cnt = reinterpret_cast<int64_t*>(ws);
+  void* sws = cnt + n_tiles + 1;
+  const unsigned g = (unsigned)ceil_div(n_tiles, kThreads / 64);
+  tile_count_kernel<<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt);
+  int rc = scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
+  if (rc) return rc;
+  if (chunk_cap > 0) {
+    tile_fill_kernel<<<g, kThreads, 0, s>>>(map, K, n, n_tiles, tile_start, chunk_off, chunk_src, chunk_row);
+  }
+  return check_launch("msp_tile_rulebook");
+}
+
+int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coords, msp_stream_t stream) {
+  if (n == 0) return MSP_OK;
+  decode_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, log2_size, coords);
+  return check_launch("msp_decode_keys");
+}
+
+}  // extern "C"

@@ -1,0 +1,114 @@
+"""ctypes binding of libmi3dsparse.so (the C ABI in include/mi3dsparse.h).
+
+The library is the only compute path: there is no CPU or eager-PyTorch
+fallback.  If the .so is missing, or a tensor handed to it is not a HIP
+device tensor, the call raises instead of silently running elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_int64, c_size_t, c_void_p
+
+import torch
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("MI3DSPARSE_LIB", os.path.join(PKG_ROOT, "lib", "libmi3dsparse.so"))
+
+P, I, I64, F, D, SZ = c_void_p, c_int, c_int64, c_float, c_double, c_size_t
+
+# name -> (restype, argtypes); mirrors include/mi3dsparse.h one to one
+PROTOTYPES = {
+    "msp_abi_version": (I, []),
+    "msp_last_error": (ctypes.c_char_p, []),
+    "msp_point_keys": (I, [P, I64, I64, I, I64, P, P, P, P]),
+    "msp_sort_workspace_size": (SZ, [I64, I]),
+    "msp_sort_pairs": (I, [P, P, P, P, I64, I, P, SZ, P]),
+    "msp_scan_workspace_size": (SZ, [I64]),
+    "msp_segment": (I, [P, I64, I, P, P, P, P, P, P, P, SZ, P]),
+    "msp_hash_capacity": (I64, [I64]),
+    "msp_hash_build": (I, [P, I64, P, P, I64, P]),
+    "msp_subm_map": (I, [P, I64, I, I64, I, P, P, I64, P, P]),
+    "msp_down_map": (I, [P, I64, P, I, I, P, I64, P]),
+    "msp_pair_lists": (I, [P, I, I64, P, P, I64, P, P, SZ, P]),
+    "msp_tile_rulebook": (I, [P, I, I64, P, P, P, P, I64, P, SZ, P]),
+    "msp_decode_keys": (I, [P, I64, I, P, P]),
+    "msp_conv_tile": (I, [P, I, P, I, I, I, P, P, P, P, I64, P, P]),
+    "msp_conv_pairs": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
+    "msp_conv_wgrad": (I, [P, I, P, I, P, P, P, P, I, I64, I64, P, P, P]),
+    "msp_bn_partials": (I64, [I64, I]),
+    "msp_bn_stats": (I, [P, I64, I, P, P]),
+    "msp_bn_finalize": (I, [P, I64, I, D, D, I, P, P, P, P, P, P]),
+    "msp_bn_apply": (I, [P, I64, I, P, F, P, P]),
+    "msp_bn_bwd_stats": (I, [P, P, I64, I, P, F, P, P]),
+    "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
+    "msp_input_avg_fwd": (I, [P, I, P, P, I64, P, P]),
+    "msp_input_avg_bwd": (I, [P, I, P, P, I64, P, P]),
+    "msp_output_fwd": (I, [P, I, P, I64, P, P]),
+    "msp_output_bwd": (I, [P, I, P, P, I64, P, P]),
+    "msp_unpool_fwd": (I, [P, I, P, I64, P, P]),
+    "msp_unpool_bwd": (I, [P, I, P, I64, P, P]),
+    "msp_maxpool_fwd": (I, [P, I, P, I64, P, P, P]),
+    "msp_maxpool_bwd": (I, [P, I, P, I64, P, P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load the library once; raise if it is absent (no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.isfile(LIB_PATH):
+            raise RuntimeError(
+                f"mi3dsparse: {LIB_PATH} not found - build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                " (there is no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("mi3dsparse kernels need HIP device tensors (got a CPU tensor); there is no CPU path")
+    return t.data_ptr()
+
+
+def stream(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name, *args):
+    """Invoke an int-returning entry point; raise RuntimeError on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.msp_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def query(name, *args):
+    """Invoke a size/capacity query that returns a value."""
+    return getattr(load(), name)(*args)
+
+
+# --------------------------------------------------------------- GPU event hooks
+# bench.py installs a recorder here to time the dominant kernel live (HIP
+# events on the launch stream) and to sum its algorithmic FLOPs.
+_recorder = None
+
+
+def set_recorder(rec):
+    global _recorder
+    _recorder = rec
+
+
+def recorder():
+    return _recorder

@@ -1,0 +1,265 @@
+"""Per-forward sparse metadata, built on the device.
+
+SCN keeps one `Metadata` per InputLayer call: a hash grid per spatial size and
+rulebooks cached per (operation, spatial size), built on the host
+(SURVEY.md §3.1, §8(a) a4/a5/a7).  This class keeps the same caching contract
+-- one `Level` per spatial size, one submanifold rulebook per filter size, one
+strided map per stride -- but every structure lives in HBM and is produced by
+the kernels of libmi3dsparse:
+
+  Level            sorted Morton keys of the active sites (V rows)
+  SubmRules        offset-major neighbour map nbr[K][V], the output-tile
+                   rulebook for msp_conv_tile and per-offset pair lists
+                   for the weight gradient
+  DownRules        parent of every fine site, child runs per coarse site,
+                   child map down[K][Vc] + its tile rulebook and pair lists
+
+The only device->host reads are the counts that size the next allocation
+(V per level, rulebook chunk totals, per-offset list starts).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from ._lib import I64, call, ptr, query
+
+TILE_ROWS = 64  # MSP_TILE_ROWS
+CHUNK = 16      # MSP_CHUNK
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 8), dtype=torch.uint8, device=device)
+
+
+def _log2_ceil(n: int) -> int:
+    return max(1, int(math.ceil(math.log2(max(2, int(n))))))
+
+
+def tile_rulebook(m, K, n, device, s):
+    """Output-tile rulebook of an offset-major map m[K][n] (two passes:
+    count, then fill; one host read of the chunk total)."""
+    n_tiles = (n + TILE_ROWS - 1) // TILE_ROWS
+    tile_start = torch.empty(n_tiles + 1, dtype=torch.int64, device=device)
+    ws = _ws((n_tiles + 1) * 8 + query("msp_scan_workspace_size", I64(n_tiles)), device)
+    call("msp_tile_rulebook", ptr(m), K, n, ptr(tile_start), None, None, None, 0, ptr(ws), ws.numel(), s)
+    n_chunks = int(tile_start[-1].item()) if n_tiles else 0
+    chunk_off = torch.empty(max(n_chunks, 1), dtype=torch.uint8, device=device)
+    chunk_src = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int32, device=device)
+    chunk_row = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.uint8, device=device)
+    if n_chunks:
+        call("msp_tile_rulebook", ptr(m), K, n, ptr(tile_start), ptr(chunk_off), ptr(chunk_src), ptr(chunk_row),
+             n_chunks, ptr(ws), ws.numel(), s)
+    return dict(tile_start=tile_start, chunk_off=chunk_off, chunk_src=chunk_src, chunk_row=chunk_row,
+                n_chunks=n_chunks)
+
+
+class PairLists:
+    """Per-offset (in, out) pair lists of an offset-major map, plus the chunk
+    and block partitions used by msp_conv_pairs / msp_conv_wgrad."""
+
+    def __init__(self, m, K, n, device, s):
+        nrb = max(1, (n + 2047) // 2048)
+        mm = K * nrb
+        ws = _ws((2 * mm + 1) * 8 + query("msp_scan_workspace_size", I64(mm)), device)
+        self.off_start = torch.empty(K + 1, dtype=torch.int64, device=device)
+        call("msp_pair_lists", ptr(m), K, n, None, None, 0, ptr(self.off_start), ptr(ws), ws.numel(), s)
+        starts = self.off_start.tolist()
+        self.total = int(starts[-1])
+        self.counts = [starts[o + 1] - starts[o] for o in range(K)]
+        self.pair_in = torch.empty(max(self.total, 1), dtype=torch.int32, device=device)
+        self.pair_out = torch.empty(max(self.total, 1), dtype=torch.int32, device=device)
+        if self.total:
+            call("msp_pair_lists", ptr(m), K, n, ptr(self.pair_in), ptr(self.pair_out), self.total,
+                 ptr(self.off_start), ptr(ws), ws.numel(), s)
+        self.K = K
+        # 16-pair chunks per offset (msp_conv_pairs)
+        cs = [0]
+        for c in self.counts:
+            cs.append(cs[-1] + (c + CHUNK - 1) // CHUNK)
+        self.n_chunks = cs[-1]
+        self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(device, non_blocking=True)
+        # weight-gradient blocks: about 2048 blocks in total
+        ppb = max(256, -(-self.total // 2048))
+        self.pairs_per_block = ((ppb + CHUNK - 1) // CHUNK) * CHUNK
+        bs = [0]
+        for c in self.counts:
+            bs.append(bs[-1] + (c + self.pairs_per_block - 1) // self.pairs_per_block)
+        self.n_blocks = bs[-1]
+        self.block_start = torch.tensor(bs, dtype=torch.int64).to(device, non_blocking=True)
+
+
+class SubmRules:
+    def __init__(self, level, filter_size):
+        dev, s = level.device, _lib.stream(level.device)
+        K = filter_size ** 3
+        self.K, self.filter_size = K, filter_size
+        V = level.n
+        tkeys, tvals, cap = level.hash()
+        self.nbr = torch.empty((K, max(V, 1)), dtype=torch.int32, device=dev)
+        if V:
+            call("msp_subm_map", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(tkeys), ptr(tvals),
+                 cap, ptr(self.nbr), s)
+        self.tiles = tile_rulebook(self.nbr, K, V, dev, s)
+        self.pairs = PairLists(self.nbr, K, V, dev, s)
+        self.n_rules = self.pairs.total  # = SCN rulebook size (centre included)
+
+
+class DownRules:
+    """Strided (size == stride) relation between a fine and a coarse level."""
+
+    def __init__(self, fine, coarse, parent_of, child_start, log2_stride):
+        dev, s = fine.device, _lib.stream(fine.device)
+        K = 8 ** log2_stride
+        self.K = K
+        self.parent_of = parent_of
+        self.child_start = child_start
+        self.down = torch.empty((K, max(coarse.n, 1)), dtype=torch.int32, device=dev)
+        call("msp_down_map", ptr(fine.keys), fine.n, ptr(parent_of), fine.log2, log2_stride, ptr(self.down),
+             coarse.n, s)
+        self.tiles = tile_rulebook(self.down, K, coarse.n, dev, s)
+        # pair_in = fine row, pair_out = coarse row, grouped by child offset
+        self.pairs = PairLists(self.down, K, coarse.n, dev, s)
+
+
+class Level:
+    def __init__(self, size, log2, keys, n, device):
+        self.size, self.log2, self.keys, self.n, self.device = int(size), int(log2), keys, int(n), device
+        self._hash = None
+        self.subm = {}
+        self.down = {}  # stride -> (coarse size, DownRules)
+
+    def hash(self):
+        if self._hash is None:
+            cap = int(query("msp_hash_capacity", I64(self.n)))
+            tkeys = torch.full((cap,), -1, dtype=torch.int64, device=self.device)
+            tvals = torch.empty(cap, dtype=torch.int32, device=self.device)
+            if self.n:
+                call("msp_hash_build", ptr(self.keys), self.n, ptr(tkeys), ptr(tvals), cap,
+                     _lib.stream(self.device))
+            self._hash = (tkeys, tvals, cap)
+        return self._hash
+
+    def subm_rules(self, filter_size):
+        r = self.subm.get(filter_size)
+        if r is None:
+            r = self.subm[filter_size] = SubmRules(self, filter_size)
+        return r
+
+
+class InputRules:
+    """Point <-> voxel relation of InputLayer/OutputLayer."""
+
+    def __init__(self, n_points, perm, p2v, vstart, batch_size):
+        self.n_points, self.perm, self.p2v, self.vstart, self.batch_size = n_points, perm, p2v, vstart, batch_size
+
+
+class Metadata:
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.levels = {}
+        self.input = None
+
+    # ------------------------------------------------------------ level 0
+    def build_input(self, coords, spatial_size):
+        dev = self.device
+        s = _lib.stream(dev)
+        size = int(spatial_size)
+        log2 = _log2_ceil(size)
+        coords = coords.to(dev, torch.int64).contiguous()
+        if coords.dim() != 2 or coords.size(1) != 4:
+            raise ValueError(f"InputLayer expects coords (N, 4) [x, y, z, batch], got {tuple(coords.shape)}")
+        n = coords.size(0)
+        keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        vals = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        stats = torch.zeros(2, dtype=torch.int64, device=dev)
+        if n:
+            call("msp_point_keys", ptr(coords), n, 4, log2, size, ptr(keys), ptr(vals), ptr(stats), s)
+        n_bad, max_b = stats.tolist()
+        if n_bad:
+            raise ValueError(f"InputLayer: {n_bad} points outside [0, {size})^3 or with a negative batch index")
+        end_bit = min(64, 3 * log2 + max(1, int(max_b).bit_length()))
+        if 3 * log2 + int(max_b).bit_length() > 63:
+            raise ValueError("InputLayer: batch index too large for 64-bit keys")
+        skeys = torch.empty_like(keys)
+        perm = torch.empty_like(vals)
+        if n:
+            wsb = int(query("msp_sort_workspace_size", I64(n), end_bit))
+            ws = _ws(wsb, dev)
+            call("msp_sort_pairs", ptr(keys), ptr(skeys), ptr(vals), ptr(perm), n, end_bit, ptr(ws), ws.numel(), s)
+        seg_of = torch.empty_like(vals)
+        p2v = torch.empty_like(vals)
+        uniq = torch.empty_like(keys)
+        vstart = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        nu = torch.zeros(1, dtype=torch.int64, device=dev)
+        ws = _ws(((n + 2047) // 2048 + 1) * 8, dev)
+        call("msp_segment", ptr(skeys), n, 0, ptr(perm), ptr(seg_of), ptr(p2v), ptr(uniq), ptr(vstart), ptr(nu),
+             ptr(ws), ws.numel(), s)
+        V = int(nu.item())
+        lvl = Level(size, log2, uniq[:max(V, 1)], V, dev)
+        self.levels[size] = lvl
+        self.input = InputRules(n, perm[:n], p2v[:n], vstart[:V + 1], int(max_b) + 1 if n else 0)
+        return lvl
+
+    def level(self, size):
+        lvl = self.levels.get(int(size))
+        if lvl is None:
+            raise RuntimeError(f"no active sites at spatial size {size} in this metadata")
+        return lvl
+
+    # ------------------------------------------------------------ coarsening
+    def downsample(self, size, stride):
+        """Return (coarse Level, DownRules) for a size==stride convolution or
+        pooling from spatial size `size`."""
+        fine = self.level(size)
+        stride = int(stride)
+        if stride & (stride - 1) or stride not in (2, 4):
+            raise NotImplementedError(f"strided ops support filter_size == stride in {{2, 4}}, got {stride}")
+        if fine.size % stride:
+            raise ValueError(f"spatial size {fine.size} is not divisible by stride {stride}")
+        hit = fine.down.get(stride)
+        if hit is not None:
+            return self.levels[hit[0]], hit[1]
+        k = stride.bit_length() - 1
+        if fine.log2 < k:
+            raise ValueError("spatial size too small for this stride")
+        dev = self.device
+        s = _lib.stream(dev)
+        n = fine.n
+        parent = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        uniq = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        cstart = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        nu = torch.zeros(1, dtype=torch.int64, device=dev)
+        ws = _ws(((n + 2047) // 2048 + 1) * 8, dev)
+        call("msp_segment", ptr(fine.keys), n, 3 * k, None, ptr(parent), None, ptr(uniq), ptr(cstart), ptr(nu),
+             ptr(ws), ws.numel(), s)
+        Vc = int(nu.item())
+        csize = fine.size // stride
+        coarse = self.levels.get(csize)
+        if coarse is None:
+            coarse = Level(csize, fine.log2 - k, uniq[:max(Vc, 1)], Vc, dev)
+            self.levels[csize] = coarse
+        elif coarse.n != Vc:
+            raise RuntimeError("inconsistent coarse level")
+        rules = DownRules(fine, coarse, parent[:max(n, 1)], cstart[:Vc + 1], k)
+        fine.down[stride] = (csize, rules)
+        return coarse, rules
+
+    def upsample_rules(self, coarse_size, stride):
+        """DownRules linking the existing fine level (coarse_size*stride) to
+        `coarse_size` (Deconvolution / UnPooling)."""
+        fine_size = int(coarse_size) * int(stride)
+        fine = self.levels.get(fine_size)
+        if fine is None or int(stride) not in fine.down:
+            raise RuntimeError(f"no strided relation {fine_size} -> {coarse_size}: a Deconvolution/UnPooling needs "
+                               "the matching Convolution/MaxPooling earlier in the same forward")
+        return fine, fine.down[int(stride)][1]
+
+    def locations(self, size):
+        lvl = self.level(size)
+        out = torch.empty((max(lvl.n, 1), 4), dtype=torch.int64, device=self.device)
+        if lvl.n:
+            call("msp_decode_keys", ptr(lvl.keys), lvl.n, lvl.log2, ptr(out), _lib.stream(self.device))
+        return out[:lvl.n]

@@ -1,0 +1,311 @@
+"""`scn.*` layer classes with SparseConvNet's constructor signatures.
+
+Constructor arguments, parameter names/shapes and initialisation follow the
+SCN 0.2 API that the reference calls (SURVEY.md §8(b) Layer 1; call sites
+models/SparseConvNet.py:60-229, Function_test.py:35-86):
+
+  weight of (Submanifold)Convolution/Deconvolution: (filter_volume, groups,
+      nIn/groups, nOut/groups) ~ N(0, sqrt(2 / (nIn * filter_volume)))
+  NetworkInNetwork weight: (nIn, nOut) ~ N(0, sqrt(2 / nIn))
+  BatchNormalization: weight=1, bias=0, running_mean=0, running_var=1,
+      eps=1e-4, momentum=0.9 (SCN convention: running = m*running + (1-m)*batch)
+
+Containers index their children '0', '1', ... like nn.Sequential so that
+state_dict keys follow the module tree.
+"""
+from __future__ import annotations
+
+import math
+import sys
+
+import torch
+from torch import nn
+
+from . import ops
+from .metadata import Metadata
+from .sparseConvNetTensor import SparseConvNetTensor
+
+
+def _pkg():
+    return sys.modules[__package__]
+
+
+def _count(macs, out_features):
+    pkg = _pkg()
+    pkg.forward_pass_multiplyAdd_count += int(macs)
+    pkg.forward_pass_hidden_states += int(out_features.nelement())
+
+
+def _cube(v, dimension, what):
+    vals = v.tolist() if torch.is_tensor(v) else (list(v) if isinstance(v, (list, tuple)) else [v] * dimension)
+    vals = [int(a) for a in vals]
+    if len(vals) != dimension or any(a != vals[0] for a in vals):
+        raise NotImplementedError(f"{what}: only cubic sizes are supported, got {vals}")
+    return vals[0]
+
+
+def _check_dim(dimension):
+    if dimension != 3:
+        raise NotImplementedError(f"mi3dsparse implements dimension=3 (got {dimension})")
+
+
+class InputLayer(nn.Module):
+    """[coords (N,4) int, features (N,C)] -> SparseConvNetTensor.
+
+    mode (Function_test.py:37-43): 0/2 first occurrence, 1 last occurrence,
+    3 sum, 4 average of the points that share a voxel."""
+
+    def __init__(self, dimension, spatial_size, mode=3):
+        super().__init__()
+        _check_dim(dimension)
+        self.dimension = dimension
+        self.spatial_size = torch.LongTensor([_cube(spatial_size, dimension, "InputLayer")] * dimension)
+        self.mode = int(mode)
+        if self.mode not in (0, 1, 2, 3, 4):
+            raise ValueError(f"InputLayer mode must be in 0..4, got {mode}")
+
+    def forward(self, input):
+        coords, feats = input[0], input[1]
+        ops._check_feats(feats)
+        if coords.size(1) == self.dimension:  # no batch column: one sample
+            coords = torch.cat([coords.long(), torch.zeros_like(coords[:, :1]).long()], 1)
+        if coords.size(0) != feats.size(0):
+            raise ValueError(f"InputLayer: {coords.size(0)} coordinates but {feats.size(0)} feature rows")
+        meta = Metadata(feats.device)
+        size = int(self.spatial_size[0])
+        lvl = meta.build_input(coords.long(), size)
+        rules = meta.input
+        if self.mode in (3, 4):
+            out = ops.InputLayerFunction.apply(feats, rules, lvl.n, self.mode)
+        else:
+            vs = rules.vstart.long()
+            pick = vs[1:] - 1 if self.mode == 1 else vs[:-1]
+            out = feats.index_select(0, rules.perm.long().index_select(0, pick))
+        return SparseConvNetTensor(out, meta, self.spatial_size)
+
+
+class OutputLayer(nn.Module):
+    """SparseConvNetTensor -> per-point features in the original point order."""
+
+    def __init__(self, dimension):
+        super().__init__()
+        self.dimension = dimension
+
+    def forward(self, input):
+        return ops.OutputLayerFunction.apply(input.features, input.metadata.input)
+
+
+class _ConvBase(nn.Module):
+    def __init__(self, dimension, nIn, nOut, filter_size, bias, groups, std_fan_in=True):
+        super().__init__()
+        _check_dim(dimension)
+        if groups != 1:
+            raise NotImplementedError("mi3dsparse convolutions implement groups=1")
+        self.dimension, self.nIn, self.nOut, self.groups = dimension, nIn, nOut, groups
+        self.filter_size = torch.LongTensor([_cube(filter_size, dimension, type(self).__name__)] * dimension)
+        self.filter_volume = int(self.filter_size.prod().item())
+        std = math.sqrt(2.0 / nIn / self.filter_volume)
+        self.weight = nn.Parameter(torch.empty(self.filter_volume, groups, nIn // groups, nOut // groups).normal_(0, std))
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(nOut))
+        else:
+            self.bias = None
+
+    def _bias(self, f):
+        return f if self.bias is None else f + self.bias
+
+
+class SubmanifoldConvolution(_ConvBase):
+    def __init__(self, dimension, nIn, nOut, filter_size, bias, groups=1):
+        super().__init__(dimension, nIn, nOut, filter_size, bias, groups)
+        if int(self.filter_size[0]) % 2 != 1:
+            raise ValueError("SubmanifoldConvolution needs an odd filter_size")
+
+    def forward(self, input):
+        size = input.size_int
+        rules = input.metadata.level(size).subm_rules(int(self.filter_size[0]))
+        f = ops.SubmanifoldConvFunction.apply(input.features, self.weight, rules)
+        f = self._bias(f)
+        _count(rules.n_rules * self.nIn * self.nOut, f)
+        return SparseConvNetTensor(f, input.metadata, input.spatial_size)
+
+
+class Convolution(_ConvBase):
+    def __init__(self, dimension, nIn, nOut, filter_size, filter_stride, bias, groups=1):
+        super().__init__(dimension, nIn, nOut, filter_size, bias, groups)
+        self.filter_stride = torch.LongTensor([_cube(filter_stride, dimension, "Convolution")] * dimension)
+        if int(self.filter_stride[0]) != int(self.filter_size[0]):
+            raise NotImplementedError("Convolution: mi3dsparse implements filter_size == filter_stride")
+
+    def forward(self, input):
+        stride = int(self.filter_stride[0])
+        coarse, rules = input.metadata.downsample(input.size_int, stride)
+        f = ops.ConvolutionFunction.apply(input.features, self.weight, rules, coarse.n)
+        f = self._bias(f)
+        _count(input.features.size(0) * self.nIn * self.nOut, f)
+        size = (input.spatial_size - self.filter_size) // self.filter_stride + 1
+        return SparseConvNetTensor(f, input.metadata, size)
+
+
+class Deconvolution(_ConvBase):
+    def __init__(self, dimension, nIn, nOut, filter_size, filter_stride, bias, groups=1):
+        super().__init__(dimension, nIn, nOut, filter_size, bias, groups)
+        self.filter_stride = torch.LongTensor([_cube(filter_stride, dimension, "Deconvolution")] * dimension)
+        if int(self.filter_stride[0]) != int(self.filter_size[0]):
+            raise NotImplementedError("Deconvolution: mi3dsparse implements filter_size == filter_stride")
+
+    def forward(self, input):
+        stride = int(self.filter_stride[0])
+        fine, rules = input.metadata.upsample_rules(input.size_int, stride)
+        f = ops.DeconvolutionFunction.apply(input.features, self.weight, rules, fine.n)
+        f = self._bias(f)
+        _count(fine.n * self.nIn * self.nOut, f)
+        size = (input.spatial_size - 1) * self.filter_stride + self.filter_size
+        return SparseConvNetTensor(f, input.metadata, size)
+
+
+class NetworkInNetwork(nn.Module):
+    """Per-site dense linear map (a plain GEMM, rocBLAS/hipBLASLt via torch)."""
+
+    def __init__(self, nIn, nOut, bias=False):
+        super().__init__()
+        self.nIn, self.nOut = nIn, nOut
+        self.weight = nn.Parameter(torch.empty(nIn, nOut).normal_(0, math.sqrt(2.0 / nIn)))
+        self.bias = nn.Parameter(torch.zeros(nOut)) if bias else None
+
+    def forward(self, input):
+        ops._check_feats(input.features)
+        f = input.features @ self.weight
+        if self.bias is not None:
+            f = f + self.bias
+        _count(input.features.size(0) * self.nIn * self.nOut, f)
+        return SparseConvNetTensor(f, input.metadata, input.spatial_size)
+
+
+class UnPooling(nn.Module):
+    def __init__(self, dimension, pool_size, pool_stride, nFeaturesToDrop=0):
+        super().__init__()
+        _check_dim(dimension)
+        self.dimension = dimension
+        self.pool_size = torch.LongTensor([_cube(pool_size, dimension, "UnPooling")] * dimension)
+        self.pool_stride = torch.LongTensor([_cube(pool_stride, dimension, "UnPooling")] * dimension)
+        if int(self.pool_size[0]) != int(self.pool_stride[0]) or nFeaturesToDrop:
+            raise NotImplementedError("UnPooling: pool_size == pool_stride and nFeaturesToDrop == 0 only")
+
+    def forward(self, input):
+        stride = int(self.pool_stride[0])
+        fine, rules = input.metadata.upsample_rules(input.size_int, stride)
+        f = ops.UnPoolingFunction.apply(input.features, rules, fine.n)
+        size = (input.spatial_size - 1) * self.pool_stride + self.pool_size
+        return SparseConvNetTensor(f, input.metadata, size)
+
+
+class MaxPooling(nn.Module):
+    def __init__(self, dimension, pool_size, pool_stride, nFeaturesToDrop=0):
+        super().__init__()
+        _check_dim(dimension)
+        self.dimension = dimension
+        self.pool_size = torch.LongTensor([_cube(pool_size, dimension, "MaxPooling")] * dimension)
+        self.pool_stride = torch.LongTensor([_cube(pool_stride, dimension, "MaxPooling")] * dimension)
+        if int(self.pool_size[0]) != int(self.pool_stride[0]) or nFeaturesToDrop:
+            raise NotImplementedError("MaxPooling: pool_size == pool_stride and nFeaturesToDrop == 0 only")
+
+    def forward(self, input):
+        stride = int(self.pool_stride[0])
+        coarse, rules = input.metadata.downsample(input.size_int, stride)
+        f = ops.MaxPoolingFunction.apply(input.features, rules, coarse.n)
+        size = (input.spatial_size - self.pool_size) // self.pool_stride + 1
+        return SparseConvNetTensor(f, input.metadata, size)
+
+
+class BatchNormalization(nn.Module):
+    def __init__(self, nPlanes, eps=1e-4, momentum=0.9, affine=True, leakiness=1):
+        super().__init__()
+        self.nPlanes, self.eps, self.momentum, self.affine, self.leakiness = nPlanes, eps, momentum, affine, leakiness
+        self.register_buffer("running_mean", torch.zeros(nPlanes))
+        self.register_buffer("running_var", torch.ones(nPlanes))
+        if affine:
+            self.weight = nn.Parameter(torch.ones(nPlanes))
+            self.bias = nn.Parameter(torch.zeros(nPlanes))
+        else:
+            self.weight = self.bias = None
+
+    def forward(self, input):
+        if input.features.size(1) != self.nPlanes:
+            raise ValueError(f"BatchNormalization({self.nPlanes}) got {input.features.size(1)} channels")
+        f = ops.BatchNormFunction.apply(input.features, self.weight, self.bias, self.running_mean, self.running_var,
+                                        self.eps, self.momentum, float(self.leakiness), self.training)
+        return SparseConvNetTensor(f, input.metadata, input.spatial_size)
+
+    def extra_repr(self):
+        return f"{self.nPlanes}, eps={self.eps}, momentum={self.momentum}, leakiness={self.leakiness}"
+
+
+class BatchNormReLU(BatchNormalization):
+    def __init__(self, nPlanes, eps=1e-4, momentum=0.9):
+        super().__init__(nPlanes, eps, momentum, True, 0)
+
+
+class BatchNormLeakyReLU(BatchNormalization):
+    def __init__(self, nPlanes, eps=1e-4, momentum=0.9, leakiness=0.333):
+        super().__init__(nPlanes, eps, momentum, True, leakiness)
+
+
+# ------------------------------------------------------------------ containers
+class Sequential(nn.Sequential):
+    def add(self, module):
+        self._modules[str(len(self._modules))] = module
+        return self
+
+
+class ConcatTable(nn.Module):
+    def __init__(self, *args):
+        super().__init__()
+        for i, m in enumerate(args):
+            self._modules[str(i)] = m
+
+    def add(self, module):
+        self._modules[str(len(self._modules))] = module
+        return self
+
+    def forward(self, input):
+        return [m(input) for m in self._modules.values()]
+
+
+class AddTable(nn.Module):
+    def forward(self, input):
+        f = input[0].features
+        for t in input[1:]:
+            f = f + t.features
+        return SparseConvNetTensor(f, input[0].metadata, input[0].spatial_size)
+
+
+class JoinTable(nn.Module):
+    def forward(self, input):
+        return SparseConvNetTensor(torch.cat([t.features for t in input], 1), input[0].metadata,
+                                   input[0].spatial_size)
+
+
+class Identity(nn.Module):
+    def forward(self, input):
+        return input
+
+
+class SparseToDense(nn.Module):
+    """(B, nPlanes, S, S, S) dense tensor of a sparse tensor (format
+    conversion only; Function_test.py:45-53, models/projector/components.py:78-80)."""
+
+    def __init__(self, dimension, nPlanes):
+        super().__init__()
+        _check_dim(dimension)
+        self.dimension, self.nPlanes = dimension, nPlanes
+
+    def forward(self, input):
+        S = input.size_int
+        loc = input.get_spatial_locations()
+        B = input.batch_size()
+        f = input.features
+        flat = f.new_zeros((B * S * S * S, self.nPlanes))
+        idx = ((loc[:, 3] * S + loc[:, 0]) * S + loc[:, 1]) * S + loc[:, 2]
+        flat = flat.index_add(0, idx, f)
+        return flat.view(B, S, S, S, self.nPlanes).permute(0, 4, 1, 2, 3).contiguous()

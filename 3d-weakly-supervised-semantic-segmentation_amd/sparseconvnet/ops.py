@@ -1,0 +1,332 @@
+"""autograd Functions over libmi3dsparse.
+
+Each Function owns the saved tensors of its backward (features, weights,
+rulebooks); every forward and backward pass is one or more C-ABI calls on the
+current HIP stream.  Channel counts that are not multiples of 16 (the 3-channel
+colour input of the first SubmanifoldConvolution, models/SparseConvNet.py:62)
+are zero-padded to the MFMA chunk width here and sliced back.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import call, ptr
+
+_EMPTY = {}
+
+
+def _stream(t):
+    return _lib.stream(t.device)
+
+
+def _pad16(c):
+    return (c + 15) // 16 * 16
+
+
+def _pad_cols(x, c):
+    return x if x.size(1) == c else F.pad(x, (0, c - x.size(1)))
+
+
+def _check_feats(x):
+    if not x.is_cuda:
+        raise RuntimeError("sparseconvnet (mi3dsparse): features must be on a HIP device; there is no CPU path")
+    if x.dtype != torch.float32:
+        raise TypeError(f"sparseconvnet (mi3dsparse): features must be float32, got {x.dtype}")
+
+
+def _pad_weight(w, cin_p, cout_p):
+    K, cin, cout = w.shape
+    if cin == cin_p and cout == cout_p:
+        return w.contiguous()
+    return F.pad(w, (0, cout_p - cout, 0, cin_p - cin))
+
+
+def _record(kind, flops, fn):
+    """Run fn(); when bench.py installed a recorder, bracket it with HIP
+    events on the current stream and account its algorithmic FLOPs."""
+    rec = _lib.recorder()
+    if rec is None:
+        return fn()
+    return rec.run(kind, flops, fn)
+
+
+# ------------------------------------------------------------------ convolution helpers
+def conv_tile(x, wt, K, flip, c_out, tiles, n_rows, kind="conv_tile", flops=0):
+    out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
+    if n_rows:
+        _record(kind, flops, lambda: call(
+            "msp_conv_tile", ptr(x), x.size(1), ptr(wt), K, int(flip), c_out, ptr(tiles["tile_start"]),
+            ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), n_rows, ptr(out),
+            _stream(x)))
+    return out[:n_rows]
+
+
+def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out):
+    out = torch.empty((max(n_out, 1), c_out), dtype=torch.float32, device=x.device)
+    if pairs.n_chunks:
+        call("msp_conv_pairs", ptr(x), x.size(1), ptr(wt), K, c_out, ptr(pin), ptr(pout), ptr(pairs.off_start),
+             ptr(pairs.chunk_start), pairs.n_chunks, ptr(out), _stream(x))
+    return out[:n_out]
+
+
+def conv_wgrad(x, dy, pairs, pin, pout, K):
+    c_in, c_out = x.size(1), dy.size(1)
+    dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
+    slab = torch.empty((max(pairs.n_blocks, 1), c_in, c_out), dtype=torch.float32, device=x.device)
+    call("msp_conv_wgrad", ptr(x), c_in, ptr(dy), c_out, ptr(pin), ptr(pout), ptr(pairs.off_start),
+         ptr(pairs.block_start), K, pairs.pairs_per_block, pairs.n_blocks, ptr(slab), ptr(dw), _stream(x))
+    return dw
+
+
+# ------------------------------------------------------------------ submanifold
+class SubmanifoldConvFunction(torch.autograd.Function):
+    """out[i] = sum_o W[o]^T x[nbr(i, o)] over the active set."""
+
+    @staticmethod
+    def forward(ctx, x, weight, rules):
+        _check_feats(x)
+        K, _, cin, cout = weight.shape
+        cin_p, cout_p = _pad16(cin), _pad16(cout)
+        xp = _pad_cols(x.contiguous(), cin_p)
+        wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
+        wt = wp.transpose(1, 2).contiguous()  # [K][cout][cin]
+        V = x.size(0)
+        out = conv_tile(xp, wt, K, 0, cout_p, rules.tiles, V, "subm_fwd",
+                        2.0 * rules.n_rules * cin * cout)
+        ctx.save_for_backward(xp, wp)
+        ctx.rules, ctx.dims = rules, (cin, cout)
+        return out if cout_p == cout else out[:, :cout].contiguous()
+
+    @staticmethod
+    def backward(ctx, gout):
+        xp, wp = ctx.saved_tensors
+        rules, (cin, cout) = ctx.rules, ctx.dims
+        K, cin_p, cout_p = wp.shape
+        g = _pad_cols(gout.contiguous(), cout_p)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dxp = conv_tile(g, wp, K, 1, cin_p, rules.tiles, xp.size(0), "subm_bwd_data",
+                            2.0 * rules.n_rules * cin * cout)
+            dx = dxp if cin_p == cin else dxp[:, :cin]
+        if ctx.needs_input_grad[1]:
+            p = rules.pairs
+            dwp = conv_wgrad(xp, g, p, p.pair_in, p.pair_out, K)
+            dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
+        return dx, dw, None
+
+
+# ------------------------------------------------------------------ strided convolution
+class ConvolutionFunction(torch.autograd.Function):
+    """Strided conv, filter_size == stride: out[p] = sum_o W[o]^T x[child(p, o)] (§8(a) a7)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, rules, n_coarse):
+        _check_feats(x)
+        K, _, cin, cout = weight.shape
+        cin_p, cout_p = _pad16(cin), _pad16(cout)
+        xp = _pad_cols(x.contiguous(), cin_p)
+        wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
+        wt = wp.transpose(1, 2).contiguous()
+        out = conv_tile(xp, wt, K, 0, cout_p, rules.tiles, n_coarse, "conv_fwd", 2.0 * x.size(0) * cin * cout)
+        ctx.save_for_backward(xp, wp)
+        ctx.rules, ctx.dims = rules, (cin, cout)
+        return out if cout_p == cout else out[:, :cout].contiguous()
+
+    @staticmethod
+    def backward(ctx, gout):
+        xp, wp = ctx.saved_tensors
+        rules, (cin, cout) = ctx.rules, ctx.dims
+        K, cin_p, cout_p = wp.shape
+        g = _pad_cols(gout.contiguous(), cout_p)
+        p = rules.pairs
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            # dx[fine] = W[o] g[parent]: src = coarse (pair_out), dst = fine (pair_in)
+            dxp = conv_pairs(g, wp, K, cin_p, p, p.pair_out, p.pair_in, xp.size(0))
+            dx = dxp if cin_p == cin else dxp[:, :cin]
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad(xp, g, p, p.pair_in, p.pair_out, K)[:, :cin, :cout].reshape(K, 1, cin, cout)
+        return dx, dw, None, None
+
+
+class DeconvolutionFunction(torch.autograd.Function):
+    """Transpose of ConvolutionFunction on the same rules (§8(a) a8):
+    out[fine] = W[o]^T x[parent(fine)]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, rules, n_fine):
+        _check_feats(x)
+        K, _, cin, cout = weight.shape
+        cin_p, cout_p = _pad16(cin), _pad16(cout)
+        xp = _pad_cols(x.contiguous(), cin_p)
+        wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
+        wt = wp.transpose(1, 2).contiguous()
+        p = rules.pairs
+        out = conv_pairs(xp, wt, K, cout_p, p, p.pair_out, p.pair_in, n_fine)
+        ctx.save_for_backward(xp, wp)
+        ctx.rules, ctx.dims = rules, (cin, cout)
+        return out if cout_p == cout else out[:, :cout].contiguous()
+
+    @staticmethod
+    def backward(ctx, gout):
+        xp, wp = ctx.saved_tensors
+        rules, (cin, cout) = ctx.rules, ctx.dims
+        K, cin_p, cout_p = wp.shape
+        g = _pad_cols(gout.contiguous(), cout_p)
+        p = rules.pairs
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dxp = conv_tile(g, wp, K, 0, cin_p, rules.tiles, xp.size(0), "deconv_bwd_data",
+                            2.0 * g.size(0) * cin * cout)
+            dx = dxp if cin_p == cin else dxp[:, :cin]
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad(xp, g, p, p.pair_out, p.pair_in, K)[:, :cin, :cout].reshape(K, 1, cin, cout)
+        return dx, dw, None, None
+
+
+# ------------------------------------------------------------------ batch norm
+class BatchNormFunction(torch.autograd.Function):
+    """BatchNormalization + (leaky) ReLU; stats[5][C] as in include/mi3dsparse.h."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train):
+        _check_feats(x)
+        x = x.contiguous()
+        V, C = x.shape
+        s = _stream(x)
+        P = int(_lib.query("msp_bn_partials", _lib.I64(V), C))
+        stats = torch.empty((5, C), dtype=torch.float32, device=x.device)
+        partial = torch.empty((P + 1) * 2 * C, dtype=torch.float64, device=x.device)
+        if train:
+            call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
+        call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
+             ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
+        y = torch.empty_like(x)
+        call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
+        ctx.save_for_backward(x, weight, stats)
+        ctx.cfg = (float(leak), int(train), weight is not None, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, stats = ctx.saved_tensors
+        leak, train, has_w, has_b = ctx.cfg
+        gy = gy.contiguous()
+        V, C = x.shape
+        s = _stream(x)
+        P = int(_lib.query("msp_bn_partials", _lib.I64(V), C))
+        partial = torch.empty((P + 1) * 2 * C, dtype=torch.float64, device=x.device)
+        call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
+        dx = torch.empty_like(x)
+        dw = torch.empty(C, dtype=torch.float32, device=x.device)
+        db = torch.empty(C, dtype=torch.float32, device=x.device)
+        call("msp_bn_bwd_apply", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats), ptr(weight) if has_w else None,
+             leak, train, ptr(dx), ptr(dw), ptr(db), s)
+        return dx, (dw if has_w else None), (db if has_b else None), None, None, None, None, None, None
+
+
+# ------------------------------------------------------------------ input / output / pooling
+class InputLayerFunction(torch.autograd.Function):
+    """mode 3 (sum) / 4 (mean) point -> voxel reduction (§8(a) a4)."""
+
+    @staticmethod
+    def forward(ctx, feats, rules, n_vox, mode):
+        _check_feats(feats)
+        feats = feats.contiguous()
+        C = feats.size(1)
+        s = _stream(feats)
+        out = torch.empty((max(n_vox, 1), C), dtype=torch.float32, device=feats.device)
+        if n_vox:
+            if mode == 4:
+                call("msp_input_avg_fwd", ptr(feats), C, ptr(rules.perm), ptr(rules.vstart), n_vox, ptr(out), s)
+            else:
+                call("msp_output_bwd", ptr(feats), C, ptr(rules.perm), ptr(rules.vstart), n_vox, ptr(out), s)
+        ctx.rules, ctx.mode, ctx.n = rules, mode, feats.size(0)
+        return out[:n_vox]
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        rules = ctx.rules
+        C = g.size(1)
+        df = torch.empty((max(ctx.n, 1), C), dtype=torch.float32, device=g.device)
+        if ctx.n:
+            if ctx.mode == 4:
+                call("msp_input_avg_bwd", ptr(g), C, ptr(rules.p2v), ptr(rules.vstart), ctx.n, ptr(df), _stream(g))
+            else:
+                call("msp_output_fwd", ptr(g), C, ptr(rules.p2v), ctx.n, ptr(df), _stream(g))
+        return df[:ctx.n], None, None, None
+
+
+class OutputLayerFunction(torch.autograd.Function):
+    """voxel -> point gather through the InputLayer map (§8(a) a14)."""
+
+    @staticmethod
+    def forward(ctx, x, rules):
+        _check_feats(x)
+        x = x.contiguous()
+        C = x.size(1)
+        out = torch.empty((max(rules.n_points, 1), C), dtype=torch.float32, device=x.device)
+        if rules.n_points:
+            call("msp_output_fwd", ptr(x), C, ptr(rules.p2v), rules.n_points, ptr(out), _stream(x))
+        ctx.rules, ctx.V = rules, x.size(0)
+        return out[:rules.n_points]
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        rules = ctx.rules
+        C = g.size(1)
+        din = torch.empty((max(ctx.V, 1), C), dtype=torch.float32, device=g.device)
+        if ctx.V:
+            call("msp_output_bwd", ptr(g), C, ptr(rules.perm), ptr(rules.vstart), ctx.V, ptr(din), _stream(g))
+        return din[:ctx.V], None
+
+
+class UnPoolingFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rules, n_fine):
+        _check_feats(x)
+        x = x.contiguous()
+        C = x.size(1)
+        out = torch.empty((max(n_fine, 1), C), dtype=torch.float32, device=x.device)
+        if n_fine:
+            call("msp_unpool_fwd", ptr(x), C, ptr(rules.parent_of), n_fine, ptr(out), _stream(x))
+        ctx.rules, ctx.Vc = rules, x.size(0)
+        return out[:n_fine]
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        C = g.size(1)
+        din = torch.empty((max(ctx.Vc, 1), C), dtype=torch.float32, device=g.device)
+        if ctx.Vc:
+            call("msp_unpool_bwd", ptr(g), C, ptr(ctx.rules.child_start), ctx.Vc, ptr(din), _stream(g))
+        return din[:ctx.Vc], None, None
+
+
+class MaxPoolingFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rules, n_coarse):
+        _check_feats(x)
+        x = x.contiguous()
+        C = x.size(1)
+        out = torch.empty((max(n_coarse, 1), C), dtype=torch.float32, device=x.device)
+        arg = torch.empty((max(n_coarse, 1), C), dtype=torch.int32, device=x.device)
+        if n_coarse:
+            call("msp_maxpool_fwd", ptr(x), C, ptr(rules.child_start), n_coarse, ptr(out), ptr(arg), _stream(x))
+        ctx.save_for_backward(arg)
+        ctx.Vf, ctx.Vc = x.size(0), n_coarse
+        return out[:n_coarse]
+
+    @staticmethod
+    def backward(ctx, g):
+        (arg,) = ctx.saved_tensors
+        g = g.contiguous()
+        C = g.size(1)
+        din = torch.zeros((max(ctx.Vf, 1), C), dtype=torch.float32, device=g.device)
+        if ctx.Vc:
+            call("msp_maxpool_bwd", ptr(g), C, ptr(arg), ctx.Vc, ptr(din), _stream(g))
+        return din[:ctx.Vf], None, None

@@ -1,0 +1,11 @@
+"""Host-side mirror of the reference's model layer for the encoder hot path:
+registry (`utils/registry.py`), encoder plugin surface
+(`models/SparseConvNet.py`), task heads and losses
+(`models/MultiLabelContrastive.py`, `utils/loss.py`), the synthetic batch
+producer (`dataset/data.py` transforms) and the data-parallel driver."""
+from .edict import EasyDict
+from .registry import LOSS_REGISTRY, MODEL_REGISTRY, Registry
+from . import encoders, heads  # noqa: F401  (registers the classes)
+from .encoders import SparseConvBase_, segment_mean
+
+__all__ = ["EasyDict", "Registry", "MODEL_REGISTRY", "LOSS_REGISTRY", "SparseConvBase_", "segment_mean"]

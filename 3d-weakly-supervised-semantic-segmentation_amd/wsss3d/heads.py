@@ -1,0 +1,104 @@
+"""Task heads and losses around the encoder (`models/MultiLabelContrastive.py:7-101`,
+`utils/loss.py:5-33`).
+
+The training call is `model((x, text), istrain=True)` (train.py:69) and the
+eval call `model(x)` -> per-point logits (N, 20) (train.py:106).  The
+TextTransformer branch of MultiLabelContrastive is out of scope for this
+round: a text model must be supplied by the caller.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .encoders import segment_mean
+from .registry import LOSS_REGISTRY, MODEL_REGISTRY
+from .synthetic import NUM_CLASSES
+
+
+def _encoder(pc_config):
+    cls, meta = MODEL_REGISTRY.get(pc_config.name)
+    width = meta.get("embed_length", lambda m: m)(pc_config.m)
+    return cls(**pc_config), width
+
+
+@MODEL_REGISTRY.register()
+class MultiLabel(nn.Module):
+    """Scene-level multilabel classification (models/MultiLabelContrastive.py:50-70)."""
+
+    def __init__(self, pc_config):
+        super().__init__()
+        self.pc_encoder, width = _encoder(pc_config)
+        self.linear = nn.Linear(width, NUM_CLASSES)
+
+    def forward(self, x, istrain=False):
+        if istrain:
+            x = x[0]
+        logits = self.linear(self.pc_encoder(x, istrain))
+        return (logits, None) if istrain else logits
+
+
+@MODEL_REGISTRY.register()
+class FullySupervised(nn.Module):
+    """Per-point logits + per-scene mean logits (models/MultiLabelContrastive.py:72-101)."""
+
+    def __init__(self, pc_config):
+        super().__init__()
+        self.pc_encoder, width = _encoder(pc_config)
+        self.linear = nn.Linear(width, NUM_CLASSES)
+
+    def forward(self, x, istrain=False):
+        if istrain:
+            pc_input = x[0]
+            logits = self.linear(self.pc_encoder(pc_input))
+            return segment_mean(logits, pc_input.batch_offsets), logits
+        return self.linear(self.pc_encoder(x))
+
+
+@MODEL_REGISTRY.register()
+class MultiLabelContrastive(nn.Module):
+    """Point + text heads (models/MultiLabelContrastive.py:7-47).  The text
+    encoder class is looked up in the registry; none is registered by this
+    package yet."""
+
+    def __init__(self, pc_config, text_config):
+        super().__init__()
+        self.pc_encoder, width = _encoder(pc_config)
+        text_cls, _ = MODEL_REGISTRY.get(text_config.name)
+        self.text_encoder = text_cls(**text_config)
+        self.text_linear = nn.Linear(text_config.width, width)
+        self.linear = nn.Linear(width, NUM_CLASSES)
+
+    def forward(self, x, istrain=False):
+        if not istrain:
+            return self.linear(self.pc_encoder(x))
+        pc_input, (text, has_text) = x
+        if has_text.size(0) > 0:
+            bt, nt, length = text.size()
+            tf = self.text_encoder(text.view(-1, length), as_dict=True)["x"].view(bt, nt, -1)
+            text_feats = self.text_linear(tf)
+        else:
+            text_feats = -1
+        global_feats = segment_mean(self.pc_encoder(pc_input), pc_input.batch_offsets)
+        return self.linear(global_feats), (global_feats, text_feats, has_text)
+
+
+@LOSS_REGISTRY.register()
+def TextContrastive(pc: torch.Tensor, text: torch.Tensor, has_text):
+    """utils/loss.py:5-18"""
+    if has_text.size(0) == 0:
+        return 0
+    sim = text @ pc.T  # B', num_text, B
+    labels = has_text[:, None].expand(-1, sim.size(1))
+    return F.cross_entropy(sim.transpose(1, 2), labels)
+
+
+@LOSS_REGISTRY.register()
+def Classification(logits: torch.Tensor, labels: torch.Tensor):
+    """utils/loss.py:20-33: scene level (B, C) multilabel soft margin, point
+    level (N,) cross entropy ignoring -100."""
+    if labels.ndim == 2:
+        return F.multilabel_soft_margin_loss(logits, labels)
+    keep = labels != -100
+    return F.cross_entropy(logits[keep], labels[keep])

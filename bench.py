@@ -1,0 +1,261 @@
+"""Headline benchmark: active-voxels/sec of one SparseConvUNet training step.
+
+Workload (BASELINE.json configs[2], the metric's config): SparseConvUNet m=32,
+block_reps=2, residual blocks, scale 50 (2 cm voxels), 8 synthetic
+ScanNet-shaped scenes per GPU, MultiLabel head + multilabel soft-margin loss.
+A step = zero_grad -> forward (metadata built on the device from raw coords)
+-> loss -> backward -> Adam step, on batches already resident in HBM.
+value = sum over ranks of level-0 active voxels per step x steps / max-over-
+ranks wall time.  N>1: one process per GPU (torchrun), each rank its own
+scenes (weak scaling), DDP gradient all-reduce over RCCL.
+
+Also reported: roofline of the dominant kernel (msp_conv_tile, fp32 MFMA)
+timed live with HIP events on its launch stream during the timed steps, and
+the CPU oracle path (fp32, torch threads) on a bounded sample on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "3d-weakly-supervised-semantic-segmentation_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (f32 MFMA = f32 vector peak)
+HBM_PEAK_GBS = 8000.0
+
+
+class KernelRecorder:
+    """Brackets every msp_conv_tile launch with torch.cuda.Events on the
+    current stream (the stream the kernel is launched on) and accumulates the
+    algorithmic FLOPs (2 * rules * c_in * c_out) per launch."""
+
+    def __init__(self):
+        self.events = []
+        self.active = False
+
+    def run(self, kind, flops, fn):
+        if not self.active:
+            return fn()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn()
+        e.record()
+        self.events.append((kind, flops, s, e))
+        return r
+
+    def summary(self):
+        torch.cuda.synchronize()
+        tot_f, tot_ms, n = 0.0, 0.0, 0
+        per = {}
+        for kind, f, s, e in self.events:
+            ms = s.elapsed_time(e)
+            tot_f += f
+            tot_ms += ms
+            n += 1
+            k = per.setdefault(kind, [0, 0.0, 0.0])
+            k[0] += 1
+            k[1] += f
+            k[2] += ms
+        return tot_f, tot_ms, n, per
+
+
+def level_stats(meta):
+    out = []
+    for size in sorted(meta.levels, reverse=True):
+        lvl = meta.levels[size]
+        r = lvl.subm.get(3)
+        out.append({"size": size, "V": lvl.n, "R": (r.n_rules if r else None)})
+    return out
+
+
+def cpu_baseline(args, batch):
+    """CPU oracle (fp32, SCN-CPU-structured gather -> mm -> scatter-add) on a
+    bounded sample: the first scene of the batch, one fwd+bwd."""
+    from oracle.encoders import OracleEncoder
+    from wsss3d.synthetic import train_merge  # noqa: F401
+
+    threads = int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    off = batch["batch_offsets"]
+    n0 = off[1]
+    coords = torch.from_numpy(batch["coords"][:n0])
+    feats = torch.from_numpy(batch["feats"][:n0])
+    torch.manual_seed(0)
+    ref = OracleEncoder("SparseConvUNet", m=args.m, full_scale=4096, block_reps=args.reps,
+                        residual_blocks=bool(args.residual))
+    lin = torch.nn.Linear(args.m, 20)
+    y = torch.from_numpy(batch["scene_labels"][:1])
+    x = dict(coords=coords, feature=feats, batch_offsets=[0, n0])
+    t0 = time.perf_counter()
+    feats_out = ref(x, istrain=True)
+    loss = torch.nn.functional.multilabel_soft_margin_loss(lin(feats_out), y)
+    loss.backward()
+    dt = time.perf_counter() - t0
+    V0 = len(np.unique(batch["coords"][:n0], axis=0))
+    return {"value": V0 / dt, "unit": "active-voxels/s", "cores": threads, "kind": "port",
+            "sample": f"1 scene of the workload ({n0} points, {V0} L0 voxels), 1 fwd+bwd step, fp32, "
+                      f"oracle/scn_oracle.py on {threads} torch threads ({dt:.2f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="scenes per GPU")
+    ap.add_argument("--scale", type=float, default=50)
+    ap.add_argument("--m", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--residual", type=int, default=1)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    import sparseconvnet as scn
+    from sparseconvnet import _lib
+    from wsss3d import EasyDict, LOSS_REGISTRY, MODEL_REGISTRY
+    from wsss3d.synthetic import make_batch
+
+    _lib.load()
+    # two distinct batches per rank, alternated step to step
+    host_batches = [make_batch(args.batch, args.scale, seed=1000 * rank + k) for k in range(2)]
+    batches = []
+    for b in host_batches:
+        x = EasyDict(coords=torch.from_numpy(b["coords"]).to(dev), feature=torch.from_numpy(b["feats"]).to(dev),
+                     batch_offsets=b["batch_offsets"])
+        y = torch.from_numpy(b["scene_labels"]).to(dev)
+        v0 = len(np.unique(b["coords"], axis=0))
+        batches.append((x, y, v0))
+
+    torch.manual_seed(0)
+    pc = EasyDict(name="SparseConvUNet", m=args.m, dimension=3, full_scale=4096, block_reps=args.reps,
+                  residual_blocks=bool(args.residual))
+    cls, _ = MODEL_REGISTRY.get("MultiLabel")
+    model = cls(pc).to(dev)
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    cls_loss, _ = LOSS_REGISTRY.get("Classification")
+
+    def step(i):
+        x, y, _ = batches[i % len(batches)]
+        opt.zero_grad(set_to_none=True)
+        logits, _ = model((x, None), istrain=True)
+        loss = cls_loss(logits, y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    rec = KernelRecorder()
+    _lib.set_recorder(rec)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    rec.active = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    rec.active = False
+    vox = sum(batches[i % len(batches)][2] for i in range(args.steps))
+    t = torch.tensor([dt, float(vox)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        dt_max, vox_all = tmax.item(), tsum.item()
+    else:
+        dt_max, vox_all = dt, float(vox)
+
+    flops, kms, nlaunch, per = rec.summary()
+    _lib.set_recorder(None)
+
+    # one untimed forward for the per-level statistics and the MAC counter
+    scn.forward_pass_multiplyAdd_count = 0
+    inner = model.module if world > 1 else model
+    x0 = batches[0][0]
+    enc = inner.pc_encoder.encoder
+    with torch.no_grad():
+        t_in = enc[0]([x0.coords, x0.feature])
+        t_out = t_in
+        for mod in list(enc)[1:-1]:
+            t_out = mod(t_out)
+    stats = level_stats(t_in.metadata)
+    macs = scn.forward_pass_multiplyAdd_count
+
+    if rank == 0:
+        achieved = flops / (kms * 1e-3) / 1e12 if kms > 0 else 0.0
+        res = {
+            "metric": "active-voxels/sec fwd+bwd, SparseConvUNet m=32 2cm voxels",
+            "value": vox_all / dt_max,
+            "unit": "active-voxels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic ScanNet-shaped procedural rooms (wsss3d/synthetic.py), trainMerge transform, "
+                    "random-init weights",
+            "config": {
+                "workload": f"SparseConvUNet m={args.m} block_reps={args.reps} residual={bool(args.residual)} "
+                            f"scale={args.scale:g} ({100 / args.scale:g} cm voxels), {args.batch} scenes/GPU, "
+                            "MultiLabel head, Adam step",
+                "scenes_per_gpu": args.batch,
+                "global_batch": args.batch * world,
+                "parallelism": f"dp{world}",
+                "active_voxels_per_step_rank0": batches[0][2],
+                "levels": stats,
+                "fwd_multiply_adds": macs,
+            },
+            "roofline": {
+                "kernel": "msp_conv_tile (submanifold fwd/bwd-data, strided conv fwd, deconv bwd-data)",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                "traffic": None,
+                "launches": nlaunch,
+                "avg_launch_us": kms / max(nlaunch, 1) * 1e3,
+                "per_kind": {k: {"launches": v[0], "tflops": v[1] / (v[2] * 1e-3) / 1e12 if v[2] else 0.0,
+                                 "ms": v[2]} for k, v in per.items()},
+            },
+        }
+        if world == 1 and not args.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(args, host_batches[0])
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

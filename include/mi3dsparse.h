@@ -1,0 +1,180 @@
+/*
+ * mi3dsparse — C ABI of the MI355X-native sparse 3D convolution library.
+ *
+ * This header is the drop-in boundary that replaces SparseConvNet's pybind11
+ * extension `sparseconvnet.SCN` (SCN 0.2 dev, `requirements.txt:2`,
+ * `env_list.txt:246`; not vendored under the reference) for the calls that the
+ * reference's encoders make through the `scn.*` module API
+ * (`models/SparseConvNet.py:57-229`).  The Python namespace
+ * `sparseconvnet` shipped with this library binds these symbols with ctypes;
+ * INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Plain pointers + sizes.  All pointers are device pointers unless a
+ *     parameter is documented as host.  Integer maps are int32, keys uint64,
+ *     features float32 row-major [rows][channels].
+ *   - All buffers, including workspaces, are allocated by the caller; sizes are
+ *     queried with the *_workspace_size functions.  The library never
+ *     allocates or frees device memory and holds no global device state.
+ *   - Every kernel is enqueued on the caller's stream; no entry point
+ *     synchronises the device.  Counts the caller needs on the host are written
+ *     to small device buffers that the caller copies back.
+ *   - Return 0 on success, a negative MSP_E* code on failure; the message is
+ *     thread-local and read with msp_last_error().
+ *   - Offset-major maps: a neighbour / child map with K filter offsets over n
+ *     rows is stored [K][n] (entry -1 = absent).  Filter offsets follow SCN's
+ *     last-axis-fastest order: o = ((dx*f) + dy)*f + dz over the f^3 box.
+ */
+#ifndef MI3DSPARSE_H
+#define MI3DSPARSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* msp_stream_t; /* hipStream_t */
+
+#define MSP_OK 0
+#define MSP_EINVAL (-1)
+#define MSP_EHIP (-2)
+#define MSP_ENOSPACE (-3)
+
+#define MSP_TILE_ROWS 64 /* output rows per wave tile in msp_conv_tile       */
+#define MSP_CHUNK 16     /* rows per MFMA chunk in rulebooks                  */
+
+int msp_abi_version(void);
+const char* msp_last_error(void);
+
+/* ---------------- metadata: voxel indexing (replaces SCN InputLayer rules,
+ * `scn.InputLayer(3, full_scale, mode=4)`, models/SparseConvNet.py:61,77,94,147,200;
+ * modes documented at Function_test.py:35-44) ------------------------------ */
+
+/* coords: n rows of `row_stride` int64, [x, y, z, batch] (batch column last,
+ * dataset/data.py:198).  Writes Morton keys and vals[i] = i.  stats[0] =
+ * number of rows outside [0, spatial_size)^3 or with negative batch id,
+ * stats[1] = max batch id.  stats must be zeroed by the caller. */
+int msp_point_keys(const int64_t* coords, int64_t n, int64_t row_stride, int log2_size, int64_t spatial_size,
+                   uint64_t* keys, int32_t* vals, int64_t* stats, msp_stream_t stream);
+
+size_t msp_sort_workspace_size(int64_t n, int end_bit);
+/* Stable LSD radix sort of (key, value) pairs on bits [0, end_bit). */
+int msp_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* vals_in, int32_t* vals_out,
+                   int64_t n, int end_bit, void* ws, size_t ws_bytes, msp_stream_t stream);
+
+size_t msp_scan_workspace_size(int64_t n);
+/* Group a sorted key array by (key >> shift).  seg_of[i] = group of row i;
+ * uniq_keys[g] = key>>shift of group g; seg_start[g] = first row of group g and
+ * seg_start[G] = n (capacity n+1); n_uniq[0] = G (device int64).  If perm and
+ * p2v are non-NULL, also p2v[perm[i]] = seg_of[i] (point -> voxel map). */
+int msp_segment(const uint64_t* sorted_keys, int64_t n, int shift, const int32_t* perm, int32_t* seg_of,
+                int32_t* p2v, uint64_t* uniq_keys, int32_t* seg_start, int64_t* n_uniq, void* ws,
+                size_t ws_bytes, msp_stream_t stream);
+
+/* ---------------- metadata: hash grid + rulebooks (replaces SCN Metadata's
+ * submanifold / strided rulebooks) ----------------- */
+int64_t msp_hash_capacity(int64_t n);
+/* tkeys must be pre-filled with 0xFF bytes (empty); keys unique. */
+int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* tkeys, int32_t* tvals, int64_t cap,
+                   msp_stream_t stream);
+/* Submanifold neighbour map nbr[K][n], K = filter_size^3 (odd filter_size). */
+int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
+                 const uint64_t* tkeys, const int32_t* tvals, int64_t cap, int32_t* nbr, msp_stream_t stream);
+/* Strided (size == stride == 2^log2_stride) child map: down[K][n_coarse],
+ * K = 8^log2_stride, down[o][parent_of[i]] = i for every fine row i. */
+int msp_down_map(const uint64_t* fine_keys, int64_t n_fine, const int32_t* parent_of, int log2_size_fine,
+                 int log2_stride, int32_t* down, int64_t n_coarse, msp_stream_t stream);
+/* Per-offset pair lists of an offset-major map: for o in [0,K), for every row
+ * r with map[o][r] >= 0 (ascending r): (pair_in, pair_out) = (map[o][r], r).
+ * off_start[K+1] (device int64) gets the list starts.  Pass cap = 0 to only
+ * count (off_start[K] = total), then call again with cap >= total. */
+int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32_t* pair_out, int64_t cap,
+                   int64_t* off_start, void* ws, size_t ws_bytes, msp_stream_t stream);
+/* Output-tile rulebook for msp_conv_tile: rows are cut into tiles of
+ * MSP_TILE_ROWS; inside a tile the present (row, offset) pairs of each offset
+ * are compacted (wavefront ballot + prefix sum) into chunks of MSP_CHUNK.
+ * tile_start[n_tiles+1] (device int64), chunk_off[c] = offset, chunk_src[c*16+j]
+ * = input row (-1 pad), chunk_row[c*16+j] = row inside the tile (64 for pad).
+ * Count-then-fill like msp_pair_lists (total chunks = tile_start[n_tiles]). */
+int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int64_t* tile_start, uint8_t* chunk_off,
+                      int32_t* chunk_src, uint8_t* chunk_row, int64_t chunk_cap, void* ws, size_t ws_bytes,
+                      msp_stream_t stream);
+/* Decode keys back to (x, y, z, batch) int64 rows (SparseToDense, locations). */
+int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coords, msp_stream_t stream);
+
+/* ---------------- sparse convolution (replaces SCN SubmanifoldConvolution /
+ * Convolution / Deconvolution updateOutput + backward) */
+
+/* Output-stationary gather-MFMA convolution over a tile rulebook:
+ *   out[r, :] = sum over chunks of r's tile: sum_j W'[o]^T x[src_j, :]
+ * wt is [K][c_out][c_in] (k contiguous).  If flip, offset o reads
+ * wt[K-1-o] (submanifold backward-data with the forward weight layout).
+ * c_in % 16 == 0, c_out % 16 == 0.  Every output row is written. */
+int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+                  const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                  const uint8_t* chunk_row, int64_t n_rows, float* out, msp_stream_t stream);
+/* One contribution per output row (deconvolution forward, strided
+ * convolution backward-data): out[pair_out[p]] = W'[o]^T x[pair_in[p]] for the
+ * pairs of offset o.  chunk_start[K+1] (device) = prefix sums of
+ * ceil(n_o / 16); n_chunks = chunk_start[K]. */
+int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, const int32_t* pair_in,
+                   const int32_t* pair_out, const int64_t* off_start, const int64_t* chunk_start,
+                   int64_t n_chunks, float* out, msp_stream_t stream);
+/* Weight gradient dW[o] (c_in x c_out) = sum over pairs of offset o of
+ * x[pair_in]^T dy[pair_out].  Blocks of `pairs_per_block` pairs write
+ * partial tiles to slab[n_blocks][c_in][c_out]; block_start[K+1] (device) =
+ * prefix sums of ceil(n_o / pairs_per_block), n_blocks = block_start[K].  A
+ * second kernel reduces the slabs in block order (deterministic) into
+ * dw[K][c_in][c_out]. */
+int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
+                   const int32_t* pair_out, const int64_t* off_start, const int64_t* block_start, int K,
+                   int64_t pairs_per_block, int64_t n_blocks, float* slab, float* dw, msp_stream_t stream);
+
+/* ---------------- batch norm + (leaky) ReLU (replaces SCN BatchNormalization
+ * with leakiness; scn.BatchNormReLU / BatchNormLeakyReLU).
+ * Per-channel statistics are one float array stats[5][C]: mean_hi, mean_lo
+ * (the fp64 mean as an fp32 pair), invstd, scale = weight*invstd,
+ * shift = bias; y = leaky_relu(((x - mean_hi) - mean_lo) * scale + shift). */
+/* Partial-sum buffers hold (msp_bn_partials(V, C) + 1) * 2 * C doubles. */
+int64_t msp_bn_partials(int64_t V, int C);
+int msp_bn_stats(const float* x, int64_t V, int C, double* partial, msp_stream_t stream);
+/* train: batch statistics from partial, running stats updated; eval: running
+ * statistics.  weight/bias may be NULL (non-affine). */
+int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double momentum, int train,
+                    float* running_mean, float* running_var, const float* weight, const float* bias,
+                    float* stats, msp_stream_t stream);
+int msp_bn_apply(const float* x, int64_t V, int C, const float* stats, float leak, float* y, msp_stream_t stream);
+int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const float* stats, float leak,
+                     double* partial, msp_stream_t stream);
+int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,
+                     const float* weight, float leak, int train, float* dx, float* dweight, float* dbias,
+                     msp_stream_t stream);
+
+/* ---------------- input / output / pooling layers */
+/* mode-4 average: out[v] = mean of feats[perm[j]] for j in [vstart[v], vstart[v+1]) */
+int msp_input_avg_fwd(const float* feats, int C, const int32_t* perm, const int32_t* vstart, int64_t V,
+                      float* out, msp_stream_t stream);
+int msp_input_avg_bwd(const float* dout, int C, const int32_t* p2v, const int32_t* vstart, int64_t n_points,
+                      float* dfeats, msp_stream_t stream);
+int msp_output_fwd(const float* in, int C, const int32_t* p2v, int64_t n_points, float* out, msp_stream_t stream);
+int msp_output_bwd(const float* dout, int C, const int32_t* perm, const int32_t* vstart, int64_t V, float* din,
+                   msp_stream_t stream);
+/* out[i] = in[parent_of[i]] */
+int msp_unpool_fwd(const float* in, int C, const int32_t* parent_of, int64_t n_fine, float* out,
+                   msp_stream_t stream);
+/* din[p] = sum of dout over children [child_start[p], child_start[p+1]) */
+int msp_unpool_bwd(const float* dout, int C, const int32_t* child_start, int64_t n_coarse, float* din,
+                   msp_stream_t stream);
+int msp_maxpool_fwd(const float* in, int C, const int32_t* child_start, int64_t n_coarse, float* out,
+                    int32_t* argmax, msp_stream_t stream);
+/* din must be zeroed by the caller */
+int msp_maxpool_bwd(const float* dout, int C, const int32_t* argmax, int64_t n_coarse, float* din,
+                    msp_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MI3DSPARSE_H */

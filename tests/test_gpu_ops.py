@@ -1,0 +1,265 @@
+"""Op-level parity of the HIP path against the CPU oracle (fp64).
+
+Tolerances: features/gradients are fp32 on the device and fp64 in the oracle;
+each check is max|gpu - oracle| <= tol * max(1, max|oracle|) with tol = 1e-5
+for single ops (one fp32 contraction) unless stated.  Integer metadata
+(voxel sets, per-offset rule counts, child maps) must match exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+import sparseconvnet as scn
+from oracle import scn_oracle as O
+from wsss3d.synthetic import make_batch, random_cloud
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def close(a, b, tol=1e-5, what=""):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    err = (a - b).abs().max().item() if a.numel() else 0.0
+    lim = tol * max(1.0, b.abs().max().item() if b.numel() else 0.0)
+    assert err <= lim, f"{what}: max err {err:.3e} > {lim:.3e}"
+
+
+def _inputs(n=3000, extent=24, n_batch=2, n_feat=3, seed=0):
+    coords, feats = random_cloud(n, extent, n_batch=n_batch, seed=seed, n_feat=n_feat, dense_frac=0.3)
+    return torch.from_numpy(coords), torch.from_numpy(feats)
+
+
+def _pair(coords, feats, size=32, mode=4, same_input=True):
+    """InputLayer on both sides; with same_input the oracle continues from the
+    device's voxel features (so each op test isolates that op's error from the
+    fp32 averaging of the input layer)."""
+    g = scn.InputLayer(3, size, mode=mode)([coords.to(DEV), feats.to(DEV)])
+    o = O.InputLayer(3, size, mode=mode)([coords, feats.double()])
+    if same_input:
+        o.features = _to_oracle_order(g, o).detach().double().cpu()
+    return g, o
+
+
+def _to_oracle_order(g_tensor, o_tensor):
+    """Rows of the GPU tensor permuted into the oracle's (raster) row order."""
+    loc = g_tensor.get_spatial_locations().cpu().numpy()
+    lvl = o_tensor.metadata.levels[o_tensor.size]
+    idx = lvl.lookup(loc)
+    assert (idx >= 0).all() and len(np.unique(idx)) == lvl.n == len(loc)
+    perm = np.empty(lvl.n, np.int64)
+    perm[idx] = np.arange(len(loc))
+    return g_tensor.features[torch.from_numpy(perm).to(g_tensor.features.device)]
+
+
+@pytest.mark.parametrize("mode", [3, 4])
+def test_input_output_layer(mode):
+    coords, feats = _inputs()
+    g, o = _pair(coords, feats, mode=mode, same_input=False)
+    assert g.features.shape[0] == o.features.shape[0]
+    close(_to_oracle_order(g, o), o.features, 1e-6, "input features")
+    out_g = scn.OutputLayer(3)(g)
+    out_o = O.OutputLayer(3)(o)
+    close(out_g, out_o, 1e-6, "output layer")
+
+
+def test_input_layer_backward():
+    coords, feats = _inputs()
+    fg = feats.to(DEV).requires_grad_(True)
+    fo = feats.double().requires_grad_(True)
+    g = scn.InputLayer(3, 32, mode=4)([coords.to(DEV), fg])
+    o = O.InputLayer(3, 32, mode=4)([coords, fo])
+    w = torch.randn(g.features.shape[1], 5, dtype=torch.float64)
+    (scn.OutputLayer(3)(g) @ w.float().to(DEV)).square().sum().backward()
+    (O.OutputLayer(3)(o) @ w).square().sum().backward()
+    close(fg.grad, fo.grad, 1e-5, "input grad")
+
+
+def test_levels_match_oracle():
+    coords, feats = _inputs(5000, 60, n_batch=3)
+    g, o = _pair(coords, feats, size=64)
+    meta_g, meta_o = g.metadata, o.metadata
+    size = 64
+    while size >= 2:
+        lg = meta_g.locations(size).cpu().numpy()
+        lo = meta_o.levels[size].coords
+        key = lambda c: np.lexsort((c[:, 2], c[:, 1], c[:, 0], c[:, 3]))  # noqa: E731
+        assert np.array_equal(lg[key(lg)], lo[key(lo)]), f"level {size}"
+        rg = meta_g.level(size).subm_rules(3)
+        ro = meta_o.levels[size].subm_rules(3)
+        assert rg.pairs.counts == [len(a) for a, _ in ro], f"rule counts at {size}"
+        assert rg.pairs.counts == rg.pairs.counts[::-1]  # symmetric neighbourhoods
+        meta_g.downsample(size, 2)
+        meta_o.downsample(size, 2)
+        size //= 2
+
+
+@pytest.mark.parametrize("cin,cout", [(3, 16), (16, 16), (32, 32), (64, 32), (48, 96), (32, 224)])
+def test_subm_conv(cin, cout):
+    torch.manual_seed(cin * 1000 + cout)
+    coords, feats = _inputs(4000, 28, n_feat=cin)
+    g, o = _pair(coords, feats)
+    conv_g = scn.SubmanifoldConvolution(3, cin, cout, 3, False).to(DEV)
+    conv_o = O.SubmanifoldConvolution(3, cin, cout, 3, False).double()
+    conv_o.weight.data.copy_(conv_g.weight.data.double().cpu())
+    xg = g.features.detach().requires_grad_(True)
+    xo = o.features.detach().requires_grad_(True)
+    g.features, o.features = xg, xo
+    yg, yo = conv_g(g), conv_o(o)
+    close(_to_oracle_order(yg, yo), yo.features, 1e-5, "subm fwd")
+    w = torch.randn(cout, dtype=torch.float64)
+    (yg.features * w.float().to(DEV)).square().sum().backward()
+    (yo.features * w).square().sum().backward()
+    close(_to_oracle_order(type(g)(xg.grad, g.metadata, g.spatial_size), o), xo.grad, 1e-5, "subm dx")
+    close(conv_g.weight.grad, conv_o.weight.grad, 1e-5, "subm dW")
+
+
+@pytest.mark.parametrize("stride,cin,cout", [(2, 16, 32), (2, 32, 48), (4, 32, 64)])
+def test_strided_conv_deconv_unpool(stride, cin, cout):
+    torch.manual_seed(stride + cin)
+    coords, feats = _inputs(4000, 40, n_feat=cin)
+    g, o = _pair(coords, feats, size=64)
+    xg = g.features.detach().requires_grad_(True)
+    xo = o.features.detach().requires_grad_(True)
+    g.features, o.features = xg, xo
+    cg = scn.Convolution(3, cin, cout, stride, stride, False).to(DEV)
+    co = O.Convolution(3, cin, cout, stride, stride, False).double()
+    co.weight.data.copy_(cg.weight.data.double().cpu())
+    dg = scn.Deconvolution(3, cout, cin, stride, stride, False).to(DEV)
+    do = O.Deconvolution(3, cout, cin, stride, stride, False).double()
+    do.weight.data.copy_(dg.weight.data.double().cpu())
+    zg, zo = cg(g), co(o)
+    assert int(zg.spatial_size[0]) == 64 // stride
+    close(_to_oracle_order(zg, zo), zo.features, 1e-5, "conv fwd")
+    ug, uo = dg(zg), do(zo)
+    close(_to_oracle_order(ug, uo), uo.features, 1e-5, "deconv fwd")
+    pg, po = scn.UnPooling(3, stride, stride)(zg), O.UnPooling(3, stride, stride)(zo)
+    close(_to_oracle_order(pg, po), po.features, 1e-6, "unpool fwd")
+    mg, mo = scn.MaxPooling(3, stride, stride)(g), O.MaxPooling(3, stride, stride)(o)
+    close(_to_oracle_order(mg, mo), mo.features, 1e-6, "maxpool fwd")
+    w1 = torch.randn(cin, dtype=torch.float64)
+    lg = (ug.features * w1.float().to(DEV)).square().sum() + pg.features.sum() + mg.features.square().sum()
+    lo = (uo.features * w1).square().sum() + po.features.sum() + mo.features.square().sum()
+    lg.backward()
+    lo.backward()
+    close(_to_oracle_order(type(g)(xg.grad, g.metadata, g.spatial_size), o), xo.grad, 1e-5, "dx")
+    close(cg.weight.grad, co.weight.grad, 1e-5, "conv dW")
+    close(dg.weight.grad, do.weight.grad, 1e-5, "deconv dW")
+
+
+@pytest.mark.parametrize("C,leak,train,mu,sd", [(32, 0.0, True, 1.5, 3.0), (48, 0.333, True, 1.5, 3.0),
+                                                (896, 0.0, True, 1.5, 3.0), (16, 0.0, False, 1.5, 3.0),
+                                                (32, 0.0, True, 10.0, 0.01)])
+def test_batchnorm(C, leak, train, mu, sd):
+    """Last case: low-variance channels far from zero (mean/std = 1e3), where
+    folding the mean into the shift loses the ReLU decision (kept as a
+    regression test for that bug)."""
+    torch.manual_seed(C)
+    coords, feats = _inputs(3000, 24, n_feat=C)
+    feats = feats * sd + mu
+    g, o = _pair(coords, feats)
+    bg = scn.BatchNormLeakyReLU(C, leakiness=leak).to(DEV)
+    bo = O.BatchNormLeakyReLU(C, leakiness=leak).double()
+    with torch.no_grad():
+        for b in (bg, bo):
+            b.weight.copy_(torch.linspace(0.5, 1.5, C))
+            b.bias.copy_(torch.linspace(-0.2, 0.3, C))
+            b.running_mean.copy_(torch.linspace(-1, 1, C))
+            b.running_var.copy_(torch.linspace(0.5, 2, C))
+    bg.train(train)
+    bo.train(train)
+    xg = g.features.detach().requires_grad_(True)
+    xo = o.features.detach().requires_grad_(True)
+    g.features, o.features = xg, xo
+    yg, yo = bg(g), bo(o)
+    close(_to_oracle_order(yg, yo), yo.features, 2e-5, "bn fwd")
+    w = torch.randn(C, dtype=torch.float64)
+    (yg.features * w.float().to(DEV)).square().sum().backward()
+    (yo.features * w).square().sum().backward()
+    close(_to_oracle_order(type(g)(xg.grad, g.metadata, g.spatial_size), o), xo.grad, 2e-5, "bn dx")
+    close(bg.weight.grad, bo.weight.grad, 2e-5, "bn dweight")
+    close(bg.bias.grad, bo.bias.grad, 2e-5, "bn dbias")
+    close(bg.running_mean, bo.running_mean, 1e-6, "running mean")
+    close(bg.running_var, bo.running_var, 1e-6, "running var")
+
+
+def test_nin_join_add():
+    coords, feats = _inputs(2000, 20, n_feat=32)
+    g, _ = _pair(coords, feats)
+    nin = scn.NetworkInNetwork(32, 16, False).to(DEV)
+    y = nin(g)
+    torch.testing.assert_close(y.features, g.features @ nin.weight)
+    j = scn.JoinTable()([g, y])
+    assert j.features.shape[1] == 48
+    a = scn.AddTable()([y, y])
+    torch.testing.assert_close(a.features, 2 * y.features)
+
+
+def test_empty_and_single_point():
+    c = torch.tensor([[5, 6, 7, 0]])
+    f = torch.randn(1, 3)
+    net = scn.Sequential(scn.InputLayer(3, 16, mode=4), scn.SubmanifoldConvolution(3, 3, 16, 3, False),
+                         scn.BatchNormReLU(16), scn.OutputLayer(3)).to(DEV)
+    out = net([c.to(DEV), f.to(DEV)])
+    assert out.shape == (1, 16) and torch.isfinite(out).all()
+    with pytest.raises(ValueError):
+        scn.InputLayer(3, 16, mode=4)([torch.tensor([[16, 0, 0, 0]]).to(DEV), f.to(DEV)])
+
+
+def test_cpu_tensor_fails_loudly():
+    coords, feats = _inputs(100, 8)
+    with pytest.raises(RuntimeError):
+        scn.InputLayer(3, 16, mode=4)([coords, feats])
+
+
+def test_full_size_determinism_and_invariants():
+    """C3-sized batch: metadata invariants and bitwise-repeatable forward."""
+    b = make_batch(8, 50, seed=1)
+    coords = torch.from_numpy(b["coords"]).to(DEV)
+    feats = torch.from_numpy(b["feats"]).to(DEV)
+    conv = scn.SubmanifoldConvolution(3, 3, 32, 3, False).to(DEV)
+    outs = []
+    for _ in range(2):
+        t = scn.InputLayer(3, 4096, mode=4)([coords, feats])
+        outs.append(conv(t).features)
+    assert torch.equal(outs[0], outs[1])
+    lvl = t.metadata.level(4096)
+    r = lvl.subm_rules(3)
+    assert r.pairs.counts[13] == lvl.n  # centre offset always present
+    assert r.pairs.counts == r.pairs.counts[::-1]
+    coarse, d = t.metadata.downsample(4096, 2)
+    assert sum(d.pairs.counts) == lvl.n  # every fine site has exactly one parent
+    cs = d.child_start.cpu()
+    assert cs[0] == 0 and cs[-1] == lvl.n and bool((cs[1:] > cs[:-1]).all())
+
+
+@pytest.mark.parametrize("n,cin", [(3000, 64), (12000, 64), (12000, 32)])
+def test_residual_block_grads(n, cin):
+    """ConcatTable(NIN | BN-SubM-BN-SubM) + AddTable: the UNet decoder block
+    whose input gradient sums two branches (models/SparseConvNet.py:112-120)."""
+    torch.manual_seed(n + cin)
+    coords, feats = _inputs(n, 40, n_feat=cin)
+    g, o = _pair(coords, feats, size=64)
+
+    def block(lib, a, b):
+        sc = lib.NetworkInNetwork(a, b, False) if a != b else lib.Identity()
+        return lib.Sequential().add(lib.ConcatTable().add(sc).add(
+            lib.Sequential().add(lib.BatchNormReLU(a)).add(lib.SubmanifoldConvolution(3, a, b, 3, False))
+            .add(lib.BatchNormReLU(b)).add(lib.SubmanifoldConvolution(3, b, b, 3, False)))).add(lib.AddTable())
+
+    bg = block(scn, cin, 32).to(DEV)
+    bo = block(O, cin, 32).double()
+    bo.load_state_dict({k: v.double().cpu() for k, v in bg.state_dict().items()})
+    xg = g.features.detach().requires_grad_(True)
+    xo = o.features.detach().requires_grad_(True)
+    g.features, o.features = xg, xo
+    yg, yo = bg(g), bo(o)
+    close(_to_oracle_order(yg, yo), yo.features, 1e-5, "block fwd")
+    w = torch.randn(32, dtype=torch.float64)
+    (yg.features * w.float().to(DEV)).square().sum().backward()
+    (yo.features * w).square().sum().backward()
+    close(_to_oracle_order(type(g)(xg.grad, g.metadata, g.spatial_size), o), xo.grad, 1e-4, "block dx")
+    pg = dict(bg.named_parameters())
+    for k, p in bo.named_parameters():
+        close(pg[k].grad, p.grad, 1e-4, "grad " + k)
