@@ -1,0 +1,90 @@
+"""Data parallelism for the encoder step: one process per GPU, scenes sharded
+across ranks, gradients averaged by DDP over RCCL (xGMI).
+
+The reference trains on one GPU and has no distributed code (SURVEY.md §0.2,
+§8(e)); `options: [distributed]` in
+`config/3DUNetWithText_scannet_subcloud_uppool_4gpu.yaml:28-29` is never read.
+Scenes are independent, every sparse op is local to a rank's batch, and the
+only exchange is the gradient all-reduce, so this is plain DDP:
+
+* `init_from_env()` reads torchrun's RANK / LOCAL_RANK / WORLD_SIZE and
+  initialises the process group ("nccl" = RCCL on ROCm when a GPU is used,
+  "gloo" otherwise);
+* `balanced_shards()` assigns scenes to ranks by point count (longest
+  processing time first) so per-rank step times stay close -- the step is
+  bound by the slowest rank;
+* `wrap()` builds DDP with local BatchNorm statistics (broadcast_buffers=False,
+  as in a single-GPU reference run at the per-rank batch size; no SyncBN) and
+  gradient buckets sized for ring all-reduce over xGMI.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(device_type: str = "cuda"):
+    """Returns (rank, world, local_rank, device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if device_type == "cuda":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+    return rank, world, local, device
+
+
+def balanced_shards(sizes, world: int):
+    """Split scene indices into `world` shards of equal count (the remainder
+    is dropped, like the reference's drop_last loader, dataset/data.py:239-247)
+    balancing the total point count: scenes are taken in decreasing size and
+    each goes to the lightest shard that still has room."""
+    n = len(sizes) // world * world
+    order = sorted(range(len(sizes)), key=lambda i: (-sizes[i], i))[:n]
+    per = n // world
+    shards = [[] for _ in range(world)]
+    load = [0] * world
+    for i in order:
+        r = min((r for r in range(world) if len(shards[r]) < per), key=lambda r: (load[r], r))
+        shards[r].append(i)
+        load[r] += sizes[i]
+    return [sorted(s) for s in shards]
+
+
+def wrap(model, device, bucket_cap_mb: int = 64):
+    """DDP with local BN statistics.  64 MB buckets: the headline UNet's 120 MB
+    of fp32 gradients go out in two ring all-reduces, each large enough to
+    run every xGMI link at full rate, overlapped with the rest of backward."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return model
+    ids = [device.index] if device.type == "cuda" else None
+    return torch.nn.parallel.DistributedDataParallel(model, device_ids=ids, broadcast_buffers=False,
+                                                     bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+
+
+def max_over_ranks(x: float) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64,
+                     device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64,
+                     device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())

@@ -122,14 +122,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+    from wsss3d import dp
+
+    rank, world, local, dev = dp.init_from_env("cuda")
 
     import sparseconvnet as scn
     from sparseconvnet import _lib
@@ -151,9 +146,7 @@ def main():
     pc = EasyDict(name="SparseConvUNet", m=args.m, dimension=3, full_scale=4096, block_reps=args.reps,
                   residual_blocks=bool(args.residual))
     cls, _ = MODEL_REGISTRY.get("MultiLabel")
-    model = cls(pc).to(dev)
-    if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False)
+    model = dp.wrap(cls(pc).to(dev), dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     cls_loss, _ = LOSS_REGISTRY.get("Classification")
 
@@ -183,15 +176,7 @@ def main():
     dt = time.perf_counter() - t0
     rec.active = False
     vox = sum(batches[i % len(batches)][2] for i in range(args.steps))
-    t = torch.tensor([dt, float(vox)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tmax = t[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t[1:].clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        dt_max, vox_all = tmax.item(), tsum.item()
-    else:
-        dt_max, vox_all = dt, float(vox)
+    dt_max, vox_all = dp.max_over_ranks(dt), dp.sum_over_ranks(float(vox))
 
     flops, kms, nlaunch, per = rec.summary()
     _lib.set_recorder(None)

@@ -1,0 +1,56 @@
+"""The C-ABI library loads and exports exactly what include/*.h declares; the
+ctypes prototypes match the header; argument validation reports through
+msp_last_error without touching a GPU."""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from sparseconvnet import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declarations():
+    decls = {}
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        for m in re.finditer(r"\b(msp_\w+)\s*\(([^)]*)\)\s*;", src):
+            args = [a for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+            decls[m.group(1)] = len(args)
+    return decls
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    decls = _declarations()
+    assert len(decls) >= 30
+    missing = [n for n in decls if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_prototypes_match_header():
+    decls = _declarations()
+    assert set(decls) == set(_lib.PROTOTYPES)
+    for name, n in decls.items():
+        assert len(_lib.PROTOTYPES[name][1]) == n, name
+
+
+def test_queries_and_validation_without_gpu():
+    lib = _lib.load()
+    assert lib.msp_abi_version() == 1
+    assert _lib.query("msp_hash_capacity", 1000) == 2048
+    assert _lib.query("msp_hash_capacity", 10) == 1024
+    assert _lib.query("msp_scan_workspace_size", 5000) > 0
+    assert _lib.query("msp_bn_partials", 10 ** 7, 32) == 1024
+    # invalid arguments are rejected before any HIP call
+    rc = lib.msp_conv_tile(None, 3, None, 27, 0, 16, None, None, None, None, 100, None, None)
+    assert rc == -1 and b"multiples of 16" in lib.msp_last_error()
+    rc = lib.msp_subm_map(None, 10, 12, 4096, 4, None, None, 1024, None, None)
+    assert rc == -1 and b"odd" in lib.msp_last_error()
+    rc = lib.msp_down_map(None, 10, None, 12, 3, None, 5, None)
+    assert rc == -1
+    with pytest.raises(RuntimeError, match="msp_tile_rulebook"):
+        _lib.call("msp_tile_rulebook", None, 300, 10, None, None, None, None, 0, None, 0, None)

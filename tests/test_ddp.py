@@ -1,0 +1,78 @@
+"""World-size-2 data parallel step on CPU (gloo), with the oracle encoder as
+the CPU stand-in for the device model: scenes are sharded by wsss3d.dp,
+gradients averaged by DDP, and the result must equal the mean of the ranks'
+independent local gradients (BN statistics stay per rank, like the
+reference's single-process BN at the per-rank batch size)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "3d-weakly-supervised-semantic-segmentation_amd"), root):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from oracle.encoders import OracleEncoder
+    from wsss3d import dp
+    from wsss3d.synthetic import make_room, train_merge
+
+    r, w, _, dev = dp.init_from_env("cpu")
+    scenes = [make_room(i, spacing=0.15) for i in range(4)]
+    shards = dp.balanced_shards([len(s[0]) for s in scenes], w)
+    mine = [scenes[i] for i in shards[r]]
+    b = train_merge(mine, 12, seed=r)
+    x = dict(coords=torch.from_numpy(b["coords"]), feature=torch.from_numpy(b["feats"]).double(),
+             batch_offsets=b["batch_offsets"])
+    torch.manual_seed(0)
+    local = OracleEncoder("SparseConvUNet", m=8, block_reps=1).double()
+    torch.manual_seed(0)
+    model = dp.wrap(OracleEncoder("SparseConvUNet", m=8, block_reps=1).double(), dev)
+    wv = torch.linspace(-1, 1, 8, dtype=torch.float64)
+    (local(x, istrain=True) * wv).sum().backward()
+    (model(x, istrain=True) * wv).sum().backward()
+    inner = model.module
+    ok = True
+    for (k, p), q in zip(inner.named_parameters(), local.parameters()):
+        g = q.grad.clone()
+        dist.all_reduce(g)
+        g /= w
+        ok &= torch.allclose(p.grad, g, rtol=1e-9, atol=1e-12)
+    # identical parameters on every rank after an optimizer step
+    opt = torch.optim.Adam(inner.parameters(), lr=1e-3)
+    opt.step()
+    flat = torch.cat([p.detach().flatten() for p in inner.parameters()])
+    ref = flat.clone()
+    dist.broadcast(ref, 0)
+    ok &= torch.equal(flat, ref)
+    out[rank] = bool(ok) and len(shards[r]) == 2
+    dist.destroy_process_group()
+
+
+def test_ddp_world2_gloo():
+    ctx = mp.get_context("spawn")
+    manager = ctx.Manager()
+    out = manager.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert dict(out) == {0: True, 1: True}
