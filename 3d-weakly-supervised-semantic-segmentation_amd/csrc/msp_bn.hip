@@ -92,37 +92,59 @@ __global__ __launch_bounds__(kT) void bn_reduce_kernel(const float* __restrict__
   }
 }
 
-__global__ void bn_finalize_kernel(const double* __restrict__ partial, int64_t P, int C, int64_t V, double eps,
-                                   double momentum, int train, float* __restrict__ rmean,
-                                   float* __restrict__ rvar, const float* __restrict__ weight,
-                                   const float* __restrict__ bias, float* __restrict__ stats) {
-  for (int c = threadIdx.x + blockIdx.x * blockDim.x; c < C; c += blockDim.x * gridDim.x) {
-    double mu, var;
-    if (train) {
-      double s = 0.0, ss = 0.0;
-      for (int64_t p = 0; p < P; ++p) {
-        s += partial[p * 2 * C + c];
-        ss += partial[p * 2 * C + C + c];
-      }
-      mu = V > 0 ? s / (double)V : 0.0;
-      var = V > 0 ? ss / (double)V - mu * mu : 0.0;
-      if (var < 0.0) var = 0.0;
-      const double unb = V > 1 ? var * (double)V / (double)(V - 1) : var;
-      rmean[c] = (float)(momentum * rmean[c] + (1.0 - momentum) * mu);
-      rvar[c] = (float)(momentum * rvar[c] + (1.0 - momentum) * unb);
-    } else {
-      mu = rmean[c];
-      var = rvar[c];
-    }
-    const double is = 1.0 / sqrt(var + eps);
-    const double w = weight ? weight[c] : 1.0, b = bias ? bias[c] : 0.0;
-    const float hi = (float)mu;
-    stats[c] = hi;
-    stats[C + c] = (float)(mu - (double)hi);
-    stats[2 * C + c] = (float)is;
-    stats[3 * C + c] = (float)(w * is);
-    stats[4 * C + c] = (float)b;
+// Sum of partial[p][slot][c] over p for one channel per block, fixed order
+// (strided per thread, then a tree over the block): deterministic.
+__device__ inline void sum_partials(const double* __restrict__ partial, int64_t P, int C, int c, double* out2) {
+  __shared__ double red[2][kT];
+  double a = 0.0, b = 0.0;
+  for (int64_t p = threadIdx.x; p < P; p += kT) {
+    a += partial[p * 2 * C + c];
+    b += partial[p * 2 * C + C + c];
   }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int w = kT / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  out2[0] = red[0][0];
+  out2[1] = red[1][0];
+}
+
+// one block per channel
+__global__ __launch_bounds__(kT) void bn_finalize_kernel(const double* __restrict__ partial, int64_t P, int C,
+                                                         int64_t V, double eps, double momentum, int train,
+                                                         float* __restrict__ rmean, float* __restrict__ rvar,
+                                                         const float* __restrict__ weight,
+                                                         const float* __restrict__ bias, float* __restrict__ stats) {
+  const int c = blockIdx.x;
+  double sums[2] = {0.0, 0.0};
+  if (train) sum_partials(partial, P, C, c, sums);
+  if (threadIdx.x != 0) return;
+  double mu, var;
+  if (train) {
+    mu = V > 0 ? sums[0] / (double)V : 0.0;
+    var = V > 0 ? sums[1] / (double)V - mu * mu : 0.0;
+    if (var < 0.0) var = 0.0;
+    const double unb = V > 1 ? var * (double)V / (double)(V - 1) : var;
+    rmean[c] = (float)(momentum * rmean[c] + (1.0 - momentum) * mu);
+    rvar[c] = (float)(momentum * rvar[c] + (1.0 - momentum) * unb);
+  } else {
+    mu = rmean[c];
+    var = rvar[c];
+  }
+  const double is = 1.0 / sqrt(var + eps);
+  const double w = weight ? weight[c] : 1.0, b = bias ? bias[c] : 0.0;
+  const float hi = (float)mu;
+  stats[c] = hi;
+  stats[C + c] = (float)(mu - (double)hi);
+  stats[2 * C + c] = (float)is;
+  stats[3 * C + c] = (float)(w * is);
+  stats[4 * C + c] = (float)b;
 }
 
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ x, int64_t n, int C,
@@ -154,20 +176,18 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ 
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ partial, int64_t P, int C,
-                                       float* __restrict__ dweight, float* __restrict__ dbias,
-                                       double* __restrict__ sums) {
-  for (int c = threadIdx.x + blockIdx.x * blockDim.x; c < C; c += blockDim.x * gridDim.x) {
-    double a = 0.0, b = 0.0;
-    for (int64_t p = 0; p < P; ++p) {
-      a += partial[p * 2 * C + c];
-      b += partial[p * 2 * C + C + c];
-    }
-    sums[c] = a;      // sum dz
-    sums[C + c] = b;  // sum dz * xhat
-    if (dbias) dbias[c] = (float)a;
-    if (dweight) dweight[c] = (float)b;
-  }
+// one block per channel
+__global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const double* __restrict__ partial, int64_t P, int C,
+                                                             float* __restrict__ dweight,
+                                                             float* __restrict__ dbias, double* __restrict__ sums) {
+  const int c = blockIdx.x;
+  double s2[2];
+  sum_partials(partial, P, C, c, s2);
+  if (threadIdx.x != 0) return;
+  sums[c] = s2[0];      // sum dz
+  sums[C + c] = s2[1];  // sum dz * xhat
+  if (dbias) dbias[c] = (float)s2[0];
+  if (dweight) dweight[c] = (float)s2[1];
 }
 
 __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restrict__ x,
@@ -223,7 +243,7 @@ int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double 
                     float* running_mean, float* running_var, const float* weight, const float* bias, float* stats,
                     msp_stream_t stream) {
   MSP_REQUIRE(C > 0, "msp_bn_finalize: bad C");
-  bn_finalize_kernel<<<(unsigned)ceil_div(C, 256), 256, 0, as_stream(stream)>>>(
+  bn_finalize_kernel<<<(unsigned)C, kT, 0, as_stream(stream)>>>(
       partial, bn_parts(V), C, V, eps, momentum, train, running_mean, running_var, weight, bias, stats);
   return check_launch("msp_bn_finalize");
 }
@@ -249,8 +269,7 @@ int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const do
   // The combined per-channel sums go to the extra 2*C doubles at the tail of
   // the partial buffer (it holds (P + 1) * 2 * C doubles, see the header).
   double* sums = const_cast<double*>(partial) + bn_parts(V) * 2 * C;
-  bn_bwd_finalize_kernel<<<(unsigned)ceil_div(C, 256), 256, 0, s>>>(partial, bn_parts(V), C, dweight, dbias,
-                                                                    sums);
+  bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V), C, dweight, dbias, sums);
   const int64_t n = V * C;
   if (n > 0)
     bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, dx);

