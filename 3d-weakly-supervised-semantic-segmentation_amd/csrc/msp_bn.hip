@@ -40,6 +40,91 @@ struct BnStats {
 };
 
 // MODE 0: (sum x, sum x^2).  MODE 1: (sum dz, sum dz*xhat).
+// Vector form (C % 4 == 0, C <= 1024): each thread owns 4 channels (one
+// float4 column) and strides over rows with 4 independent loads in flight;
+// R = 256 / (C/4) rows are covered per pass and folded in LDS in fixed order.
+template <int MODE>
+__global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                        int64_t V, int C, const float* __restrict__ stats,
+                                                        float leak, double* __restrict__ partial) {
+  __shared__ double red[kT][8];
+  const int64_t P = gridDim.x;
+  const int64_t per = (V + P - 1) / P;
+  const int64_t v0 = blockIdx.x * per, v1 = min(V, v0 + per);
+  const int C4 = C >> 2;
+  const int R = kT / C4;
+  const int t = threadIdx.x, c4 = t % C4, ro = t / C4;
+  const BnStats st(stats, C);
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+  float mh[4], ml[4], is[4], sc[4], sh[4];
+  if (MODE == 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * c4 + k;
+      mh[k] = st.mh[c];
+      ml[k] = st.ml[c];
+      is[k] = st.is[c];
+      sc[k] = st.sc[c];
+      sh[k] = st.sh[c];
+    }
+  }
+  auto term = [&](const float4& xv4, const float4& g4) {
+    const float xs[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
+    const float gs[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (MODE == 0) {
+        s0[k] += xs[k];
+        s1[k] += (double)xs[k] * xs[k];
+      } else {
+        const float xc = (xs[k] - mh[k]) - ml[k];
+        const float z = xc * sc[k] + sh[k];
+        const float dz = z > 0.f ? gs[k] : gs[k] * leak;
+        s0[k] += dz;
+        s1[k] += (double)dz * ((double)xc * is[k]);
+      }
+    }
+  };
+  if (ro < R) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* g4 = reinterpret_cast<const float4*>(dy);
+    int64_t v = v0 + ro;
+    for (; v + 3 * R < v1; v += 4 * R) {
+      float4 xa[4], ga[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xa[u] = x4[(v + u * R) * C4 + c4];
+        if (MODE == 1) ga[u] = g4[(v + u * R) * C4 + c4];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) term(xa[u], MODE == 1 ? ga[u] : xa[u]);
+    }
+    for (; v < v1; v += R) term(x4[v * C4 + c4], MODE == 1 ? g4[v * C4 + c4] : x4[v * C4 + c4]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[t][k] = s0[k];
+    red[t][4 + k] = s1[k];
+  }
+  __syncthreads();
+  if (t < C4) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] += red[k * C4 + t][j];
+        b[j] += red[k * C4 + t][4 + j];
+      }
+    double* out0 = partial + (int64_t)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      out0[4 * t + j] = a[j];
+      out0[C + 4 * t + j] = b[j];
+    }
+  }
+}
+
+// MODE 0: (sum x, sum x^2).  MODE 1: (sum dz, sum dz*xhat).
 template <int MODE>
 __global__ __launch_bounds__(kT) void bn_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                        int64_t V, int C, const float* __restrict__ stats,
@@ -149,10 +234,10 @@ __global__ __launch_bounds__(kT) void bn_finalize_kernel(const double* __restric
 
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ x, int64_t n, int C,
                                                       const float* __restrict__ stats, float leak,
-                                                      float* __restrict__ y) {
+                                                      float* __restrict__ y, int vec) {
   const int64_t stride = (int64_t)gridDim.x * kT;
   const BnStats st(stats, C);
-  if ((C & 3) == 0) {
+  if (vec) {
     const int64_t n4 = n >> 2;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n4; i += stride) {
       const float4 v = reinterpret_cast<const float4*>(x)[i];
@@ -195,25 +280,40 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
                                                           int64_t V, const double* __restrict__ sums,
                                                           const float* __restrict__ stats,
                                                           const float* __restrict__ weight, float leak, int train,
-                                                          float* __restrict__ dx) {
+                                                          float* __restrict__ dx, int vec) {
   const int64_t stride = (int64_t)gridDim.x * kT;
   const double invV = V > 0 ? 1.0 / (double)V : 0.0;
   const BnStats st(stats, C);
-  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
-    const int c = (int)(i % C);
-    const float xv = x[i];
-    const float g = dy[i];
+  auto one = [&](float xv, float g, int c) {
     const float dz = st.z(xv, c) > 0.f ? g : g * leak;
     const float w = weight ? weight[c] : 1.f;
     if (train) {
       const float xh = st.centred(xv, c) * st.is[c];
       const float mdz = (float)(sums[c] * invV), mdzx = (float)(sums[C + c] * invV);
-      dx[i] = w * st.is[c] * (dz - mdz - xh * mdzx);
-    } else {
-      dx[i] = w * st.is[c] * dz;
+      return w * st.is[c] * (dz - mdz - xh * mdzx);
     }
+    return w * st.is[c] * dz;
+  };
+  if (vec) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n4; i += stride) {
+      const float4 xv = reinterpret_cast<const float4*>(x)[i];
+      const float4 g = reinterpret_cast<const float4*>(dy)[i];
+      const int c = (int)((i * 4) % C);
+      float4 o;
+      o.x = one(xv.x, g.x, c);
+      o.y = one(xv.y, g.y, c + 1);
+      o.z = one(xv.z, g.z, c + 2);
+      o.w = one(xv.w, g.w, c + 3);
+      reinterpret_cast<float4*>(dx)[i] = o;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride)
+      dx[i] = one(x[i], dy[i], (int)(i % C));
   }
 }
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 inline unsigned ew_grid(int64_t n) {
   int64_t g = (n + kT - 1) / kT;
@@ -234,8 +334,12 @@ int64_t msp_bn_partials(int64_t V, int C) {
 
 int msp_bn_stats(const float* x, int64_t V, int C, double* partial, msp_stream_t stream) {
   MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_stats: bad shape");
-  bn_reduce_kernel<0><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
-                                                                           partial);
+  if (C % 4 == 0 && C <= 4 * kT && aligned16(x))
+    bn_reduce4_kernel<0><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
+                                                                              partial);
+  else
+    bn_reduce_kernel<0><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
+                                                                             partial);
   return check_launch("msp_bn_stats");
 }
 
@@ -251,14 +355,18 @@ int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double 
 int msp_bn_apply(const float* x, int64_t V, int C, const float* stats, float leak, float* y, msp_stream_t stream) {
   const int64_t n = V * C;
   if (n == 0) return MSP_OK;
-  bn_apply_kernel<<<ew_grid(n / 4 + 1), kT, 0, as_stream(stream)>>>(x, n, C, stats, leak, y);
+  const int vec = (C % 4 == 0) && aligned16(x) && aligned16(y);
+  bn_apply_kernel<<<ew_grid(n / 4 + 1), kT, 0, as_stream(stream)>>>(x, n, C, stats, leak, y, vec);
   return check_launch("msp_bn_apply");
 }
 
 int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const float* stats, float leak,
                      double* partial, msp_stream_t stream) {
   MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_bwd_stats: bad shape");
-  bn_reduce_kernel<1><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
+  if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy))
+    bn_reduce4_kernel<1><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
+  else
+    bn_reduce_kernel<1><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
   return check_launch("msp_bn_bwd_stats");
 }
 
@@ -272,7 +380,9 @@ int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const do
   bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V), C, dweight, dbias, sums);
   const int64_t n = V * C;
   if (n > 0)
-    bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, dx);
+    bn_bwd_apply_kernel<<<ew_grid(n / 4 + 1), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, dx,
+                                                          (C % 4 == 0) && aligned16(x) && aligned16(dy) &&
+                                                              aligned16(dx));
   return check_launch("msp_bn_bwd_apply");
 }
 

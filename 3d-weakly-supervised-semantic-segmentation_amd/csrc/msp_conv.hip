@@ -115,159 +115,6 @@ __global__ __launch_bounds__(kThreads) void conv_tile_kernel(
   }
 }
 
-// ---------------------------------------------------------------- conv_tile (v3)
-// Software-pipelined form of conv_tile.  The wave walks "units" = (chunk,
-// 64-channel input slice) of its tile; while the MFMAs of unit u run, the
-// gathers of unit u+1 (16 input rows x 64 channels, one float4 per lane per
-// 16 channels) and its weight slice (4 x NT float4 per lane) are in flight,
-// and the chunk metadata (source rows, offset) of unit u+2 is being read.
-// Consecutive units with the same (offset, slice) reuse the weight registers
-// instead of reloading them.  The ablation of the unpipelined kernel on the
-// headline batch (level 1, c=64) measured the gathers and the weight loads at
-// ~30 % and ~40 % of its time, each exposed rather than overlapped.
-struct UnitMeta {
-  int64_t c;  // chunk
-  int ks;     // input-channel slice
-  int ow;     // weight offset
-  int src;    // this lane's input row (-1 pad)
-};
-
-template <int NT>
-struct UnitRegs {
-  floatx4 a[4];
-  floatx4 b[4][NT];
-};
-
-template <int NT>
-__global__ __launch_bounds__(kThreads) void conv_tile3_kernel(
-    const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
-    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
-    const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
-    int64_t n_tiles, float* __restrict__ out) {
-  constexpr int NC = 16 * NT;
-  constexpr int LS = NC + 4;
-  constexpr int LR = MSP_TILE_ROWS + 1;
-  __shared__ float lds[kWaves][LR * LS];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
-  if (tile >= n_tiles) return;  // wave-uniform; no block barrier in this kernel
-  float* acc_s = lds[wave];
-  for (int i = lane; i < LR * LS; i += 64) acc_s[i] = 0.f;
-  const int c0 = blockIdx.y * NC;
-  const int r = lane & 15, q = lane >> 4;
-  const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
-  const int nks = (c_in + 63) >> 6;
-  const int64_t n_units = (ce - cb) * nks;
-
-  auto meta_of = [&](int64_t u) {
-    UnitMeta m;
-    m.c = cb + u / nks;
-    m.ks = (int)(u % nks);
-    const int o = chunk_off[m.c];
-    m.ow = flip ? (K - 1 - o) : o;
-    m.src = chunk_src[m.c * MSP_CHUNK + r];
-    return m;
-  };
-  auto kcs_of = [&](int ks) { return min(4, (c_in - ks * 64) >> 4); };
-  auto load_a = [&](UnitRegs<NT>& R, const UnitMeta& m) {
-    const int kcs = kcs_of(m.ks);
-    const float* xs = x + (int64_t)(m.src < 0 ? 0 : m.src) * c_in + m.ks * 64 + 4 * q;
-#pragma unroll
-    for (int kc = 0; kc < 4; ++kc)
-      if (kc < kcs) R.a[kc] = *reinterpret_cast<const floatx4*>(xs + kc * 16);
-  };
-  auto load_b = [&](UnitRegs<NT>& R, const UnitMeta& m) {
-    const int kcs = kcs_of(m.ks);
-    const float* wb = wt + ((int64_t)m.ow * c_out + c0 + r) * c_in + m.ks * 64 + 4 * q;
-#pragma unroll
-    for (int kc = 0; kc < 4; ++kc)
-      if (kc < kcs)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) R.b[kc][t] = *reinterpret_cast<const floatx4*>(wb + (int64_t)t * 16 * c_in + kc * 16);
-  };
-  floatx4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](const UnitRegs<NT>& R, const UnitMeta& m) {
-    const int kcs = kcs_of(m.ks);
-    const bool pad = m.src < 0;
-#pragma unroll
-    for (int kc = 0; kc < 4; ++kc) {
-      if (kc < kcs) {
-        const floatx4 a = pad ? floatx4{0.f, 0.f, 0.f, 0.f} : R.a[kc];
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s], R.b[kc][t][s], acc[t]);
-      }
-    }
-    if (m.ks == nks - 1) {
-      const uint32_t rows = *reinterpret_cast<const uint32_t*>(chunk_row + m.c * MSP_CHUNK + 4 * q);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float* dst = acc_s + ((rows >> (8 * j)) & 0xff) * LS + r;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) dst[t * 16] += acc[t][j];
-      }
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-
-  if (n_units > 0) {
-    UnitRegs<NT> R0, R1;
-    UnitMeta m0 = meta_of(0), m1, m2;
-    load_a(R0, m0);
-    load_b(R0, m0);
-    if (n_units > 1) m1 = meta_of(1);
-    int64_t u = 0;
-    for (;;) {
-      // ---- even half: compute R0, prefetch R1
-      if (u + 1 < n_units) {
-        load_a(R1, m1);
-        if (m1.ow == m0.ow && m1.ks == m0.ks) {
-#pragma unroll
-          for (int kc = 0; kc < 4; ++kc)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) R1.b[kc][t] = R0.b[kc][t];
-        } else {
-          load_b(R1, m1);
-        }
-        if (u + 2 < n_units) m2 = meta_of(u + 2);
-      }
-      compute(R0, m0);
-      if (++u >= n_units) break;
-      m0 = m1;
-      m1 = m2;
-      // ---- odd half: compute R1, prefetch R0
-      if (u + 1 < n_units) {
-        load_a(R0, m1);
-        if (m1.ow == m0.ow && m1.ks == m0.ks) {
-#pragma unroll
-          for (int kc = 0; kc < 4; ++kc)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) R0.b[kc][t] = R1.b[kc][t];
-        } else {
-          load_b(R0, m1);
-        }
-        if (u + 2 < n_units) m2 = meta_of(u + 2);
-      }
-      compute(R1, m0);
-      if (++u >= n_units) break;
-      m0 = m1;
-      m1 = m2;
-    }
-  }
-  const int64_t row0 = tile * MSP_TILE_ROWS;
-  const int nr = (int)((n_rows - row0) < MSP_TILE_ROWS ? (n_rows - row0) : MSP_TILE_ROWS);
-  constexpr int V4 = NC / 4;
-  for (int i = lane; i < nr * V4; i += 64) {
-    const int rr = i / V4, cc = (i % V4) * 4;
-    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + cc) =
-        *reinterpret_cast<const floatx4*>(acc_s + rr * LS + cc);
-  }
-}
-
 // ---------------------------------------------------------------- conv_tile (v4)
 // Block-level offset-major form: block = 4 waves = 4 consecutive 64-row
 // tiles, one 16*NT output-channel slice.  The block walks the offsets any of
@@ -275,7 +122,7 @@ __global__ __launch_bounds__(kThreads) void conv_tile3_kernel(
 // slice W'[o][k0:k0+64][c0:c0+16NT] is staged once in LDS (double-buffered,
 // one barrier per step) and every wave applies it to its <= 4 chunks of that
 // offset: all gathers of the step are issued before the first MFMA.
-template <int NT>
+template <int NT, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -394,9 +241,13 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     for (int j = 0; j < 4; ++j) {
       const float* xs = x + (int64_t)(src[j] < 0 ? 0 : src[j]) * c_in + ks * 64 + 4 * q;
 #pragma unroll
-      for (int kc = 0; kc < 4; ++kc)
-        a[j][kc] = (j < gn && kc < kcs) ? *reinterpret_cast<const floatx4*>(xs + kc * 16)
-                                        : floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < 4; ++kc) {
+        if (ABL & 1)
+          a[j][kc] = floatx4{(float)src[j], (float)kc, 1.f, 2.f};
+        else
+          a[j][kc] = (j < gn && kc < kcs) ? *reinterpret_cast<const floatx4*>(xs + kc * 16)
+                                          : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     const floatx4* wb = wbuf[step & 1];
 #pragma unroll
@@ -404,7 +255,10 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
       if (kc < kcs) {
         floatx4 b[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) b[t] = wb[(kc * 4 + q) * NC + t * 16 + r];
+        for (int t = 0; t < NT; ++t) {
+          if (ABL & 2) b[t] = floatx4{(float)t, (float)kc, 0.5f, (float)o_cur};
+          else b[t] = wb[(kc * 4 + q) * NC + t * 16 + r];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j < gn) {
@@ -421,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (j < gn) {
-          const uint32_t rows = *reinterpret_cast<const uint32_t*>(chunk_row + (g0 + j) * MSP_CHUNK + 4 * q);
+          const uint32_t rows = (ABL & 4) ? 0x40404040u : *reinterpret_cast<const uint32_t*>(chunk_row + (g0 + j) * MSP_CHUNK + 4 * q);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float* dst = acc_s + ((rows >> (8 * i)) & 0xff) * LS + r;
@@ -431,7 +285,7 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
         }
       }
     }
-    if (more) store_slice((step + 1) & 1);
+    if (more && !(ABL & 2)) store_slice((step + 1) & 1);
     o_cur = o_nx;
     ks = ks_nx;
   }
@@ -670,9 +524,11 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
   return check_launch("msp_conv_tile");
 }
 
-// Experiment hook (not part of the public ABI): conv_tile with parts of the
-// data movement replaced by constants to find the limiter.  abl bits: 1 no
-// gather loads, 2 no weight loads, 4 no LDS accumulation.  nt forces NT.
+// Experiment hook (not part of the public ABI; scripts/kbench_conv.py): the
+// two conv_tile forms with parts of their data movement replaced by constants
+// to find the limiter.  abl 0-7: per-wave form (bits: 1 no gathers, 2 no
+// weight loads, 4 no LDS accumulation); abl 16-23: block offset-major form
+// (same bits).  nt forces NT.
 int msp_debug_conv_tile(int abl, int nt, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
                         const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                         const uint8_t* chunk_row, int64_t n_rows, float* out, msp_stream_t stream) {
@@ -688,18 +544,13 @@ int msp_debug_conv_tile(int abl, int nt, const float* x, int c_in, const float* 
                                                      chunk_src, chunk_row, n_rows, n_tiles, out);
 #define LN(N) L(N, 0) L(N, 1) L(N, 2) L(N, 3) L(N, 4) L(N, 5) L(N, 6) L(N, 7)
   LN(1) LN(2) LN(4)
-#define L3(N)                                                                                              \
-  if (NT == N && abl == 8)                                                                                 \
-    conv_tile3_kernel<N><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,     \
-                                                   chunk_src, chunk_row, n_rows, n_tiles, out);
-  L3(1) L3(2) L3(4)
-#undef L3
-#define L4(N)                                                                                              \
-  if (NT == N && abl == 9)                                                                                 \
-    conv_tile4_kernel<N><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,     \
-                                                   chunk_src, chunk_row, n_rows, n_tiles, out);
-  L4(1) L4(2) L4(4)
+#define L4(N, A)                                                                                           \
+  if (NT == N && abl == 16 + A)                                                                            \
+    conv_tile4_kernel<N, A><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,  \
+                                                      chunk_src, chunk_row, n_rows, n_tiles, out);
+  L4(2, 0) L4(2, 1) L4(2, 2) L4(2, 3) L4(2, 4) L4(2, 7)
 #undef L4
+
 #undef LN
 #undef L
   return check_launch("msp_debug_conv_tile");

@@ -59,17 +59,14 @@ class SparseConvBase_(nn.Module):
         return self.postProcessing(out, x["batch_offsets"]) if istrain else out
 
 
-def _wrap(dimension, full_scale, body, out_planes):
+def _wrap(dimension, full_scale, m, make_body, out_planes):
     """InputLayer(mode 4) -> SubM(3 -> m) -> body -> BNReLU -> OutputLayer:
-    the frame every reference encoder uses."""
-    first = body[0]
-    return scn.Sequential(
-        scn.InputLayer(dimension, full_scale, mode=4),
-        scn.SubmanifoldConvolution(dimension, 3, first, 3, False),
-        body[1],
-        scn.BatchNormReLU(out_planes),
-        scn.OutputLayer(dimension),
-    )
+    the frame every reference encoder uses.  Modules are created in the
+    reference's order (the first SubM before the body), so a seeded init draws
+    the same weights as the reference's getEncoder."""
+    inp = scn.InputLayer(dimension, full_scale, mode=4)
+    first = scn.SubmanifoldConvolution(dimension, 3, m, 3, False)
+    return scn.Sequential(inp, first, make_body(), scn.BatchNormReLU(out_planes), scn.OutputLayer(dimension))
 
 
 def _levels(m, depth=7):
@@ -81,8 +78,7 @@ class SparseConvUNet(SparseConvBase_):
     """models/SparseConvNet.py:57-71"""
 
     def getEncoder(self, m, dimension, full_scale, block_reps, residual_blocks):
-        unet = scn.UNet(dimension, block_reps, _levels(m), residual_blocks)
-        return _wrap(dimension, full_scale, (m, unet), m)
+        return _wrap(dimension, full_scale, m, lambda: scn.UNet(dimension, block_reps, _levels(m), residual_blocks), m)
 
 
 @MODEL_REGISTRY.register(embed_length=lambda m: 7 * (7 + 1) * m // 2)
@@ -92,8 +88,8 @@ class SparseConvFCNet(SparseConvBase_):
     def getEncoder(self, m, dimension, full_scale, block_reps, residual_blocks, depth: int = 7,
                    downsample=[2, 2]):
         planes = _levels(m, depth)
-        fcn = scn.FullyConvolutionalNet(dimension, block_reps, planes, residual_blocks, downsample=downsample)
-        return _wrap(dimension, full_scale, (m, fcn), sum(planes))
+        return _wrap(dimension, full_scale, m, lambda: scn.FullyConvolutionalNet(
+            dimension, block_reps, planes, residual_blocks, downsample=downsample), sum(planes))
 
 
 @MODEL_REGISTRY.register(embed_length=lambda m: sum([m, 64, 128, 192, 256]))
@@ -103,8 +99,8 @@ class SparseConvFCNetNarrow(SparseConvBase_):
     def getEncoder(self, m, dimension, full_scale, block_reps, residual_blocks,
                    nPlanes: List[int] = [64, 128, 192, 256], downsample=[2, 2]):
         planes = [m] + list(nPlanes)
-        fcn = scn.FullyConvolutionalNet(dimension, block_reps, planes, residual_blocks, downsample=downsample)
-        return _wrap(dimension, full_scale, (m, fcn), sum(planes))
+        return _wrap(dimension, full_scale, m, lambda: scn.FullyConvolutionalNet(
+            dimension, block_reps, planes, residual_blocks, downsample=downsample), sum(planes))
 
 
 class _DirectUpPool(SparseConvBase_):
@@ -120,8 +116,8 @@ class _DirectUpPool(SparseConvBase_):
     def getEncoder(self, m, dimension, full_scale, block_reps, residual_blocks, nPlanes=None, downsample=None):
         planes = [m] + list(self.default_planes if nPlanes is None else nPlanes)
         ds = self.default_downsample if downsample is None else downsample
-        body = self.FCNEncoder(dimension, block_reps, planes, residual_blocks, downsample=ds)
-        return _wrap(dimension, full_scale, (m, body), planes[-1])
+        return _wrap(dimension, full_scale, m, lambda: self.FCNEncoder(
+            dimension, block_reps, planes, residual_blocks, downsample=ds), planes[-1])
 
 
 @MODEL_REGISTRY.register(embed_length=lambda m: 256)
@@ -151,5 +147,5 @@ class SparseConvFCNetEncoder(SparseConvBase_):
     def getEncoder(self, m, dimension, full_scale, block_reps, residual_blocks, depth: int = 7,
                    downsample=[2, 2]):
         planes = _levels(m, depth)
-        body = scn.FullyConvolutionalNetEncoder(dimension, block_reps, planes, residual_blocks, downsample)
-        return _wrap(dimension, full_scale, (m, body), planes[-1])
+        return _wrap(dimension, full_scale, m, lambda: scn.FullyConvolutionalNetEncoder(
+            dimension, block_reps, planes, residual_blocks, downsample), planes[-1])

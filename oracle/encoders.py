@@ -44,13 +44,10 @@ def _body(name, m, reps, residual):
 class OracleEncoder(nn.Module):
     def __init__(self, name, m, dimension=3, full_scale=4096, block_reps=1, residual_blocks=False):
         super().__init__()
+        inp = O.InputLayer(3, full_scale, mode=4)
+        first = O.SubmanifoldConvolution(3, 3, m, 3, False)  # created before the body, as the reference does
         body, out = _body(name, m, block_reps, residual_blocks)
-        self.encoder = O.Sequential(
-            O.InputLayer(3, full_scale, mode=4),
-            O.SubmanifoldConvolution(3, 3, m, 3, False),
-            body,
-            O.BatchNormReLU(out),
-            O.OutputLayer(3))
+        self.encoder = O.Sequential(inp, first, body, O.BatchNormReLU(out), O.OutputLayer(3))
 
     def forward(self, x, istrain=False):
         out = self.encoder([x["coords"], x["feature"]])

@@ -170,3 +170,32 @@ def test_balanced_shards():
     assert len(set(sh[0]) | set(sh[1])) == 8 and 3 not in sh[0] + sh[1]  # smallest scene dropped
     loads = [sum(sizes[i] for i in s) for s in sh]
     assert abs(loads[0] - loads[1]) <= 20
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present (GPU box)")
+def test_reference_model_file_runs_on_this_package():
+    """Drop-in check: the reference's models/SparseConvNet.py, loaded unmodified
+    with THIS package as `sparseconvnet`, registers its encoders and builds
+    module trees identical (keys, shapes, seeded values) to wsss3d's."""
+    import importlib.util
+    import sys
+    import types
+    sys.modules["easydict"] = types.SimpleNamespace(EasyDict=EasyDict)
+    if REF not in sys.path:
+        sys.path.append(REF)
+    spec = importlib.util.spec_from_file_location("ref_models_on_mi3dsparse", os.path.join(REF, "models", "SparseConvNet.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.scn is scn
+    for name, m, reps, res in [("SparseConvUNet", 32, 2, True), ("SparseConvFCNet", 16, 1, False),
+                               ("SparseConvFCNetDirectUpPoolLight", 16, 1, True)]:
+        torch.manual_seed(5)
+        ref_enc = getattr(mod, name)(name, m=m, dimension=3, full_scale=4096, block_reps=reps, residual_blocks=res)
+        torch.manual_seed(5)
+        ours = MODEL_REGISTRY.get(name)[0](name, m=m, dimension=3, full_scale=4096, block_reps=reps,
+                                           residual_blocks=res)
+        a, b = ref_enc.state_dict(), ours.state_dict()
+        assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a), name
