@@ -234,30 +234,44 @@ __global__ __launch_bounds__(kT) void bn_finalize_kernel(const double* __restric
 
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ x, int64_t n, int C,
                                                       const float* __restrict__ stats, float leak,
-                                                      float* __restrict__ y, int vec) {
+                                                      float* __restrict__ y) {
   const int64_t stride = (int64_t)gridDim.x * kT;
   const BnStats st(stats, C);
-  if (vec) {
-    const int64_t n4 = n >> 2;
-    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n4; i += stride) {
-      const float4 v = reinterpret_cast<const float4*>(x)[i];
-      const int c = (int)((i * 4) % C);
-      float4 o;
-      o.x = st.z(v.x, c);
-      o.y = st.z(v.y, c + 1);
-      o.z = st.z(v.z, c + 2);
-      o.w = st.z(v.w, c + 3);
-      o.x = o.x > 0.f ? o.x : o.x * leak;
-      o.y = o.y > 0.f ? o.y : o.y * leak;
-      o.z = o.z > 0.f ? o.z : o.z * leak;
-      o.w = o.w > 0.f ? o.w : o.w * leak;
-      reinterpret_cast<float4*>(y)[i] = o;
-    }
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
-      const float z = st.z(x[i], (int)(i % C));
-      y[i] = z > 0.f ? z : z * leak;
-    }
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
+    const float z = st.z(x[i], (int)(i % C));
+    y[i] = z > 0.f ? z : z * leak;
+  }
+}
+
+// Vector form (C % 4 == 0, C <= 1024): thread t owns the float4 column
+// t % (C/4) for all its rows, so the per-channel constants sit in registers
+// and the loop has no index division; rows advance by gridDim * R.
+__global__ __launch_bounds__(kT) void bn_apply4_kernel(const float* __restrict__ x, int64_t V, int C,
+                                                       const float* __restrict__ stats, float leak,
+                                                       float* __restrict__ y) {
+  const int C4 = C >> 2, R = kT / C4;
+  const int t = threadIdx.x, c4 = t % C4, ro = t / C4;
+  if (ro >= R) return;
+  const BnStats st(stats, C);
+  float mh[4], ml[4], sc[4], sh[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * c4 + k;
+    mh[k] = st.mh[c];
+    ml[k] = st.ml[c];
+    sc[k] = st.sc[c];
+    sh[k] = st.sh[c];
+  }
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  float4* y4 = reinterpret_cast<float4*>(y);
+  const int64_t step = (int64_t)gridDim.x * R;
+  auto f = [&](float v, int k) {
+    const float z = ((v - mh[k]) - ml[k]) * sc[k] + sh[k];
+    return z > 0.f ? z : z * leak;
+  };
+  for (int64_t v = (int64_t)blockIdx.x * R + ro; v < V; v += step) {
+    const float4 a = x4[v * C4 + c4];
+    y4[v * C4 + c4] = make_float4(f(a.x, 0), f(a.y, 1), f(a.z, 2), f(a.w, 3));
   }
 }
 
@@ -280,40 +294,75 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
                                                           int64_t V, const double* __restrict__ sums,
                                                           const float* __restrict__ stats,
                                                           const float* __restrict__ weight, float leak, int train,
-                                                          float* __restrict__ dx, int vec) {
+                                                          float* __restrict__ dx) {
   const int64_t stride = (int64_t)gridDim.x * kT;
   const double invV = V > 0 ? 1.0 / (double)V : 0.0;
   const BnStats st(stats, C);
-  auto one = [&](float xv, float g, int c) {
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % C);
+    const float xv = x[i], g = dy[i];
     const float dz = st.z(xv, c) > 0.f ? g : g * leak;
     const float w = weight ? weight[c] : 1.f;
     if (train) {
       const float xh = st.centred(xv, c) * st.is[c];
       const float mdz = (float)(sums[c] * invV), mdzx = (float)(sums[C + c] * invV);
-      return w * st.is[c] * (dz - mdz - xh * mdzx);
+      dx[i] = w * st.is[c] * (dz - mdz - xh * mdzx);
+    } else {
+      dx[i] = w * st.is[c] * dz;
     }
-    return w * st.is[c] * dz;
+  }
+}
+
+// Vector form of the above (same column ownership as bn_apply4_kernel).
+__global__ __launch_bounds__(kT) void bn_bwd_apply4_kernel(const float* __restrict__ x,
+                                                           const float* __restrict__ dy, int64_t V, int C,
+                                                           const double* __restrict__ sums,
+                                                           const float* __restrict__ stats,
+                                                           const float* __restrict__ weight, float leak, int train,
+                                                           float* __restrict__ dx) {
+  const int C4 = C >> 2, R = kT / C4;
+  const int t = threadIdx.x, c4 = t % C4, ro = t / C4;
+  if (ro >= R) return;
+  const double invV = V > 0 ? 1.0 / (double)V : 0.0;
+  const BnStats st(stats, C);
+  float mh[4], ml[4], is[4], sc[4], sh[4], ws[4], mdz[4], mdzx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * c4 + k;
+    mh[k] = st.mh[c];
+    ml[k] = st.ml[c];
+    is[k] = st.is[c];
+    sc[k] = st.sc[c];
+    sh[k] = st.sh[c];
+    ws[k] = (weight ? weight[c] : 1.f) * is[k];
+    mdz[k] = train ? (float)(sums[c] * invV) : 0.f;
+    mdzx[k] = train ? (float)(sums[C + c] * invV) : 0.f;
+  }
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const float4* g4 = reinterpret_cast<const float4*>(dy);
+  float4* d4 = reinterpret_cast<float4*>(dx);
+  const int64_t step = (int64_t)gridDim.x * R;
+  auto f = [&](float xv, float g, int k) {
+    const float xc = (xv - mh[k]) - ml[k];
+    const float dz = xc * sc[k] + sh[k] > 0.f ? g : g * leak;
+    if (!train) return ws[k] * dz;
+    return ws[k] * (dz - mdz[k] - (xc * is[k]) * mdzx[k]);
   };
-  if (vec) {
-    const int64_t n4 = n >> 2;
-    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n4; i += stride) {
-      const float4 xv = reinterpret_cast<const float4*>(x)[i];
-      const float4 g = reinterpret_cast<const float4*>(dy)[i];
-      const int c = (int)((i * 4) % C);
-      float4 o;
-      o.x = one(xv.x, g.x, c);
-      o.y = one(xv.y, g.y, c + 1);
-      o.z = one(xv.z, g.z, c + 2);
-      o.w = one(xv.w, g.w, c + 3);
-      reinterpret_cast<float4*>(dx)[i] = o;
-    }
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride)
-      dx[i] = one(x[i], dy[i], (int)(i % C));
+  for (int64_t v = (int64_t)blockIdx.x * R + ro; v < V; v += step) {
+    const float4 a = x4[v * C4 + c4], g = g4[v * C4 + c4];
+    d4[v * C4 + c4] = make_float4(f(a.x, g.x, 0), f(a.y, g.y, 1), f(a.z, g.z, 2), f(a.w, g.w, 3));
   }
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// blocks for the column-owning vector kernels: R = 256 / (C/4) rows per block pass
+inline unsigned rows_grid(int64_t V, int C) {
+  const int64_t R = kT / (C / 4);
+  int64_t g = (V + R - 1) / R;
+  if (g > 4096) g = 4096;
+  return (unsigned)(g < 1 ? 1 : g);
+}
 
 inline unsigned ew_grid(int64_t n) {
   int64_t g = (n + kT - 1) / kT;
@@ -355,8 +404,10 @@ int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double 
 int msp_bn_apply(const float* x, int64_t V, int C, const float* stats, float leak, float* y, msp_stream_t stream) {
   const int64_t n = V * C;
   if (n == 0) return MSP_OK;
-  const int vec = (C % 4 == 0) && aligned16(x) && aligned16(y);
-  bn_apply_kernel<<<ew_grid(n / 4 + 1), kT, 0, as_stream(stream)>>>(x, n, C, stats, leak, y, vec);
+  if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(y))
+    bn_apply4_kernel<<<rows_grid(V, C), kT, 0, as_stream(stream)>>>(x, V, C, stats, leak, y);
+  else
+    bn_apply_kernel<<<ew_grid(n), kT, 0, as_stream(stream)>>>(x, n, C, stats, leak, y);
   return check_launch("msp_bn_apply");
 }
 
@@ -379,10 +430,12 @@ int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const do
   double* sums = const_cast<double*>(partial) + bn_parts(V) * 2 * C;
   bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V), C, dweight, dbias, sums);
   const int64_t n = V * C;
-  if (n > 0)
-    bn_bwd_apply_kernel<<<ew_grid(n / 4 + 1), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, dx,
-                                                          (C % 4 == 0) && aligned16(x) && aligned16(dy) &&
-                                                              aligned16(dx));
+  if (n > 0) {
+    if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx))
+      bn_bwd_apply4_kernel<<<rows_grid(V, C), kT, 0, s>>>(x, dy, V, C, sums, stats, weight, leak, train, dx);
+    else
+      bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, dx);
+  }
   return check_launch("msp_bn_bwd_apply");
 }
 

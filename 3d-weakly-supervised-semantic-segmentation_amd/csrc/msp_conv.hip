@@ -29,29 +29,49 @@ __device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
+// with its own L2.  Neighbouring tiles gather the same input rows, so give
+// every XCD a contiguous range of logical blocks (bijective for any count).
+__device__ inline int64_t xcd_linear(int64_t bid, int64_t nb) {
+  const int64_t q = nb >> 3, rem = nb & 7, x = bid & 7;
+  return (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + (bid >> 3);
+}
+
+// LDS tile accumulator [64 rows][NC] with the 16-byte column groups XOR-
+// swizzled by row: 16 distinct consecutive rows at one column group land on
+// 16 distinct bank quads (ds_read/write_b128 are served per 16 lanes).
+template <int NC>
+__device__ inline int acc_pos(int row, int g) {
+  constexpr int RP = 64 / NC, GM = NC / 4 - 1;
+  return row * NC + 4 * (g ^ ((row / RP) & GM));
+}
+
 // ---------------------------------------------------------------- conv_tile
-// One wave owns one 64-row output tile and 16*NT output channels.  For each
-// 16-row chunk of its rulebook (all rows share one filter offset) it gathers
-// the 16 input rows, multiplies them by that offset's weights with MFMA and
-// adds the 16 x 16NT result into a wave-private LDS accumulator at the chunk's
-// row positions (padding rows go to sink row 64).  The tile is stored once.
+// Both forms run the MFMA transposed, D = W^T X^T: lane (r, q) then holds
+// output channels 16t + 4q .. +3 of chunk row r, so a chunk is added into the
+// LDS tile accumulator with one 16-byte read-modify-write per lane and t;
+// padding lanes (row 64) skip it.  Logical block l covers tile group l / n_y and channel slice
+// l % n_y: the slices of a tile group run back to back on one XCD.
+//
+// Per-wave form: one wave owns one 64-row output tile and 16*NT output
+// channels; for each 16-row chunk (all rows share one filter offset) it
+// gathers the 16 input rows and the weight fragment straight into registers.
 template <int NT, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void conv_tile_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
-    int64_t n_tiles, float* __restrict__ out) {
+    int64_t n_tiles, int n_y, float* __restrict__ out) {
   constexpr int NC = 16 * NT;
-  constexpr int LS = NC + 4;  // LDS row stride (floats)
-  constexpr int LR = MSP_TILE_ROWS + 1;
-  __shared__ float lds[kWaves][LR * LS];
+  __shared__ floatx4 lds4[kWaves][MSP_TILE_ROWS * NC / 4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t tile = (lb / n_y) * kWaves + wave;
   if (tile >= n_tiles) return;  // wave-uniform; the kernel has no block barrier
-  float* acc_s = lds[wave];
-  for (int i = lane; i < LR * LS; i += 64) acc_s[i] = 0.f;
+  float* acc_s = reinterpret_cast<float*>(lds4[wave]);
+  for (int i = lane; i < MSP_TILE_ROWS * NC / 4; i += 64) lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const int c0 = blockIdx.y * NC;
+  const int c0 = (int)(lb % n_y) * NC;
   const int r = lane & 15, q = lane >> 4;
   const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
   const int kcn = c_in >> 4;
@@ -62,7 +82,7 @@ __global__ __launch_bounds__(kThreads) void conv_tile_kernel(
     const int o = chunk_off[c];
     const int ow = flip ? (K - 1 - o) : o;
     const int src = chunk_src[c * MSP_CHUNK + r];
-    const uint32_t rows = *reinterpret_cast<const uint32_t*>(chunk_row + c * MSP_CHUNK + 4 * q);
+    const int row = chunk_row[c * MSP_CHUNK + r];
     const float* xs = x + (int64_t)(src < 0 ? 0 : src) * c_in + 4 * q;
     const float* wb = wt + ((int64_t)ow * c_out + c0 + r) * c_in + 4 * q;
     floatx4 acc[NT];
@@ -85,20 +105,15 @@ __global__ __launch_bounds__(kThreads) void conv_tile_kernel(
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s], b[t][s], acc[t]);
+        for (int t = 0; t < NT; ++t) acc[t] = mfma4(b[t][s], a[s], acc[t]);
       }
     }
     if (ABL & 4) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) sink[t] += acc[t];
-    } else {
+    } else if (row < MSP_TILE_ROWS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = (rows >> (8 * j)) & 0xff;
-        float* dst = acc_s + row * LS + r;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) dst[t * 16] += acc[t][j];
-      }
+      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
     }
   }
   if (ABL & 4) {
@@ -109,31 +124,117 @@ __global__ __launch_bounds__(kThreads) void conv_tile_kernel(
   const int nr = (int)((n_rows - row0) < MSP_TILE_ROWS ? (n_rows - row0) : MSP_TILE_ROWS);
   constexpr int V4 = NC / 4;
   for (int i = lane; i < nr * V4; i += 64) {
-    const int rr = i / V4, cc = (i % V4) * 4;
-    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + cc) =
-        *reinterpret_cast<const floatx4*>(acc_s + rr * LS + cc);
+    const int rr = i / V4, g = i % V4;
+    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
+        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
   }
 }
 
-// ---------------------------------------------------------------- conv_tile (v4)
+// Pipelined per-wave form for c_in = 16*KC <= 64: chunk indices are loaded
+// two chunks ahead, input rows and weight fragments one chunk ahead, so a
+// wave always has the next chunk's loads in flight while it runs MFMAs.
+template <int NT, int KC>
+__global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
+    const float* __restrict__ x, const float* __restrict__ wt, int K, int flip, int c_out,
+    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
+    const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
+    int64_t n_tiles, int n_y, float* __restrict__ out) {
+  constexpr int NC = 16 * NT, C_IN = 16 * KC;
+  __shared__ floatx4 lds4[kWaves][MSP_TILE_ROWS * NC / 4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t tile = (lb / n_y) * kWaves + wave;
+  if (tile >= n_tiles) return;  // wave-uniform; the kernel has no block barrier
+  float* acc_s = reinterpret_cast<float*>(lds4[wave]);
+  for (int i = lane; i < MSP_TILE_ROWS * NC / 4; i += 64) lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int c0 = (int)(lb % n_y) * NC;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
+
+  struct St {
+    int o, src, row;
+  };
+  auto ld_idx = [&](int64_t c, St& d) {
+    if (c < ce) {
+      d.o = chunk_off[c];
+      d.src = chunk_src[c * MSP_CHUNK + r];
+      d.row = chunk_row[c * MSP_CHUNK + r];
+    } else {
+      d.o = 0;
+      d.src = -1;
+      d.row = MSP_TILE_ROWS;
+    }
+  };
+  auto ld_val = [&](const St& d, floatx4 (&av)[KC], floatx4 (&bv)[NT][KC]) {
+    const float* xs = x + (int64_t)(d.src < 0 ? 0 : d.src) * C_IN + 4 * q;
+    const int ow = flip ? (K - 1 - d.o) : d.o;
+    const float* wb = wt + ((int64_t)ow * c_out + c0 + r) * C_IN + 4 * q;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      av[kc] = d.src >= 0 ? *reinterpret_cast<const floatx4*>(xs + kc * 16) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bv[t][kc] = *reinterpret_cast<const floatx4*>(wb + t * 16 * C_IN + kc * 16);
+    }
+  };
+  St s0, s1;
+  ld_idx(cb, s0);
+  ld_idx(cb + 1, s1);
+  floatx4 a0[KC], b0[NT][KC];
+  if (cb < ce) ld_val(s0, a0, b0);
+  for (int64_t c = cb; c < ce; ++c) {
+    St s2;
+    ld_idx(c + 2, s2);
+    floatx4 a1[KC], b1[NT][KC];
+    if (c + 1 < ce) ld_val(s1, a1, b1);
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma4(b0[t][kc][s], a0[kc][s], acc[t]);
+    if (s0.row < MSP_TILE_ROWS) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(s0.row, 4 * t + q)) += acc[t];
+    }
+    s0 = s1;
+    s1 = s2;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      a0[kc] = a1[kc];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b0[t][kc] = b1[t][kc];
+    }
+  }
+  const int64_t row0 = tile * MSP_TILE_ROWS;
+  const int nr = (int)((n_rows - row0) < MSP_TILE_ROWS ? (n_rows - row0) : MSP_TILE_ROWS);
+  constexpr int V4 = NC / 4;
+  for (int i = lane; i < nr * V4; i += 64) {
+    const int rr = i / V4, g = i % V4;
+    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
+        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
+  }
+}
+
+// ---------------------------------------------------------------- conv_tile (block form)
 // Block-level offset-major form: block = 4 waves = 4 consecutive 64-row
 // tiles, one 16*NT output-channel slice.  The block walks the offsets any of
 // its tiles needs in (offset, 64-channel slice) steps; each step the weight
 // slice W'[o][k0:k0+64][c0:c0+16NT] is staged once in LDS (double-buffered,
 // one barrier per step) and every wave applies it to its <= 4 chunks of that
 // offset: all gathers of the step are issued before the first MFMA.
-template <int NT, int ABL = 0>
+template <int NT, int ABL = 0, bool PF = false>
 __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
-    int64_t n_tiles, float* __restrict__ out) {
+    int64_t n_tiles, int n_y, float* __restrict__ out) {
   constexpr int NC = 16 * NT;
-  constexpr int LS = NC + 2;
-  constexpr int LR = MSP_TILE_ROWS + 1;
   constexpr int BF4 = 16 * NC;  // float4 per 64-channel weight slice, [k/4][n]
   constexpr int SPT = (BF4 + kThreads - 1) / kThreads;
-  __shared__ float acc_lds[kWaves][LR * LS];
+  __shared__ floatx4 acc_lds4[kWaves][MSP_TILE_ROWS * NC / 4];
   __shared__ floatx4 wbuf[2][BF4];
   __shared__ unsigned long long need[2];
   __shared__ int16_t gfirst[kWaves][128];
@@ -141,11 +242,12 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 15, q = lane >> 4;
-  const int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t tile = (lb / n_y) * kWaves + wave;
   const bool active = tile < n_tiles;
-  const int c0 = blockIdx.y * NC;
-  float* acc_s = acc_lds[wave];
-  for (int i = lane; i < LR * LS; i += 64) acc_s[i] = 0.f;
+  const int c0 = (int)(lb % n_y) * NC;
+  float* acc_s = reinterpret_cast<float*>(acc_lds4[wave]);
+  for (int i = lane; i < MSP_TILE_ROWS * NC / 4; i += 64) acc_lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
   for (int i = lane; i < 128; i += 64) {
     gcount[wave][i] = 0;
     gfirst[wave][i] = 0x7fff;
@@ -205,50 +307,76 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     }
   };
 
+  // Chunk indices of a step are loaded one step ahead; with PF the input rows
+  // are gathered one step ahead too, so the only exposed latency per step is
+  // the barrier.
+  struct Idx {
+    int src[4], row[4], gn;
+  };
+  auto load_idx = [&](int o, Idx& d) {
+    d.gn = gcount[wave][o];
+    const int64_t g0 = cb + gfirst[wave][o];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      d.src[j] = (j < d.gn) ? chunk_src[(g0 + j) * MSP_CHUNK + r] : -1;
+      d.row[j] = (j < d.gn) ? (int)chunk_row[(g0 + j) * MSP_CHUNK + r] : MSP_TILE_ROWS;
+    }
+  };
+  auto gather = [&](const Idx& d, int kslice, floatx4 (&av)[4][4]) {
+    const int kcs = min(4, (c_in - kslice * 64) >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* xs = x + (int64_t)(d.src[j] < 0 ? 0 : d.src[j]) * c_in + kslice * 64 + 4 * q;
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) {
+        if (ABL & 1)
+          av[j][kc] = floatx4{(float)d.src[j], (float)kc, 1.f, 2.f};
+        else
+          av[j][kc] = (d.src[j] >= 0 && kc < kcs) ? *reinterpret_cast<const floatx4*>(xs + kc * 16)
+                                                  : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
   int o_cur = 0, ks = 0;
+  Idx ic;
+  floatx4 a[4][4];
   if (n_steps > 0) {
     o_cur = next_offset(it0, it1);
     load_slice(o_cur, 0);
     store_slice(0);
+    load_idx(o_cur, ic);
+    if (PF) gather(ic, 0, a);
   }
   floatx4 acc[4][NT];
+  floatx4 sink[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) sink[t] = floatx4{0.f, 0.f, 0.f, 0.f};
   for (int step = 0; step < n_steps; ++step) {
-    const int gn = gcount[wave][o_cur];
-    const int64_t g0 = cb + gfirst[wave][o_cur];
+    const int gn = ic.gn;
     if (ks == 0) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[j][t] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-    __syncthreads();  // wbuf[step & 1] holds this step's slice; the other buffer is free
+    if (!(ABL & 8)) __syncthreads();  // wbuf[step & 1] holds this step's slice; the other buffer is free
     const bool more = step + 1 < n_steps;
     int o_nx = o_cur, ks_nx = ks + 1;
-    if (more) {
-      if (ks_nx == nks) {
-        ks_nx = 0;
-        o_nx = next_offset(it0, it1);
-      }
-      load_slice(o_nx, ks_nx);
+    if (more && ks_nx == nks) {
+      ks_nx = 0;
+      o_nx = next_offset(it0, it1);
+    }
+    if (more) load_slice(o_nx, ks_nx);
+    Idx in = ic;
+    if (more && ks_nx == 0) load_idx(o_nx, in);
+    floatx4 an[4][4];
+    if (PF) {
+      if (more) gather(in, ks_nx, an);
+    } else {
+      gather(ic, ks, a);
     }
     const int kcs = min(4, (c_in - ks * 64) >> 4);
-    // gathers of all chunks of this step, issued before any MFMA
-    int src[4];
-    floatx4 a[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) src[j] = (j < gn) ? chunk_src[(g0 + j) * MSP_CHUNK + r] : -1;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float* xs = x + (int64_t)(src[j] < 0 ? 0 : src[j]) * c_in + ks * 64 + 4 * q;
-#pragma unroll
-      for (int kc = 0; kc < 4; ++kc) {
-        if (ABL & 1)
-          a[j][kc] = floatx4{(float)src[j], (float)kc, 1.f, 2.f};
-        else
-          a[j][kc] = (j < gn && kc < kcs) ? *reinterpret_cast<const floatx4*>(xs + kc * 16)
-                                          : floatx4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
     const floatx4* wb = wbuf[step & 1];
 #pragma unroll
     for (int kc = 0; kc < 4; ++kc) {
@@ -262,25 +390,29 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j < gn) {
-            const floatx4 av = src[j] < 0 ? floatx4{0.f, 0.f, 0.f, 0.f} : a[j][kc];
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
-              for (int t = 0; t < NT; ++t) acc[j][t] = mfma4(av[s], b[t][s], acc[j][t]);
+              for (int t = 0; t < NT; ++t) acc[j][t] = mfma4(b[t][s], a[j][kc][s], acc[j][t]);
           }
         }
       }
     }
-    if (ks == nks - 1) {
+    if ((ABL & 4) && ks == nks - 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < gn)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) sink[t] += acc[j][t];
+    } else if (ks == nks - 1) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (j < gn) {
-          const uint32_t rows = (ABL & 4) ? 0x40404040u : *reinterpret_cast<const uint32_t*>(chunk_row + (g0 + j) * MSP_CHUNK + 4 * q);
+          const int row = ic.row[j];
+          if (row < MSP_TILE_ROWS) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float* dst = acc_s + ((rows >> (8 * i)) & 0xff) * LS + r;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) dst[t * 16] += acc[j][t][i];
+            for (int t = 0; t < NT; ++t)
+              *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[j][t];
           }
         }
       }
@@ -288,13 +420,26 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     if (more && !(ABL & 2)) store_slice((step + 1) & 1);
     o_cur = o_nx;
     ks = ks_nx;
+    ic = in;
+    if (PF) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) a[j][kc] = an[j][kc];
+    }
+  }
+  if (ABL & 4) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc_s[lane] += sink[t][0] + sink[t][1] + sink[t][2] + sink[t][3];
   }
   if (!active) return;
   const int64_t row0 = tile * MSP_TILE_ROWS;
   const int nr = (int)((n_rows - row0) < MSP_TILE_ROWS ? (n_rows - row0) : MSP_TILE_ROWS);
-  for (int i = lane; i < nr * NC; i += 64) {
-    const int rr = i / NC, cc = i % NC;
-    out[(row0 + rr) * c_out + c0 + cc] = acc_s[rr * LS + cc];
+  constexpr int V4 = NC / 4;
+  for (int i = lane; i < nr * V4; i += 64) {
+    const int rr = i / V4, g = i % V4;
+    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
+        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
   }
 }
 
@@ -505,21 +650,26 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
   const int64_t n_tiles = ceil_div(n_rows, MSP_TILE_ROWS);
   if (n_tiles == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
-  if (c_in >= 64 && (c_out / 16) % 2 == 0) {
+  const int64_t n_tb = ceil_div(n_tiles, kWaves);
+  const int NT = (c_out / 16) % 2 == 0 ? 2 : 1;
+  const int n_y = c_out / (16 * NT);
+  const unsigned grid = (unsigned)(n_tb * n_y);
+  if (c_in >= 64 && NT == 2) {
     // block offset-major form: weights staged once per block and offset
-    dim3 grid((unsigned)ceil_div(n_tiles, kWaves), (unsigned)(c_out / 32));
-    conv_tile4_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
-                                                   chunk_src, chunk_row, n_rows, n_tiles, out);
+    conv_tile4_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src,
+                                                   chunk_row, n_rows, n_tiles, n_y, out);
+  } else if (c_in <= 64) {
+    // narrow inputs (level 0 of m=32, m=16 nets): pipelined per-wave form, no barriers
+#define LP(N, C)                                                                                              \
+  if (NT == N && c_in == 16 * C)                                                                              \
+    conv_tilep_kernel<N, C><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, \
+                                                      chunk_row, n_rows, n_tiles, n_y, out);
+    LP(1, 1) LP(1, 2) LP(1, 3) LP(1, 4) LP(2, 1) LP(2, 2) LP(2, 3)
+#undef LP
   } else {
-    // narrow inputs (level 0 of m=32, m=16 nets): per-wave form, no barriers
-    const int NT = (c_out / 16) % 2 == 0 ? 2 : 1;
-    dim3 grid((unsigned)ceil_div(n_tiles, kWaves), (unsigned)(c_out / (16 * NT)));
-    if (NT == 2)
-      conv_tile_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
-                                                    chunk_src, chunk_row, n_rows, n_tiles, out);
-    else
-      conv_tile_kernel<1><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
-                                                    chunk_src, chunk_row, n_rows, n_tiles, out);
+    // wide inputs with an odd number of 16-channel output groups (m=16 nets)
+    conv_tile_kernel<1><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src,
+                                                  chunk_row, n_rows, n_tiles, n_y, out);
   }
   return check_launch("msp_conv_tile");
 }
@@ -528,7 +678,9 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
 // two conv_tile forms with parts of their data movement replaced by constants
 // to find the limiter.  abl 0-7: per-wave form (bits: 1 no gathers, 2 no
 // weight loads, 4 no LDS accumulation); abl 16-23: block offset-major form
-// (same bits).  nt forces NT.
+// (same bits, + 8: no per-step barrier -- wrong results, timing only); 32:
+// block form with gathers one step ahead; 48: pipelined per-wave form.  nt
+// forces NT.
 int msp_debug_conv_tile(int abl, int nt, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
                         const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                         const uint8_t* chunk_row, int64_t n_rows, float* out, msp_stream_t stream) {
@@ -536,20 +688,34 @@ int msp_debug_conv_tile(int abl, int nt, const float* x, int c_in, const float* 
   if (n_tiles == 0) return MSP_OK;
   const int NT = nt > 0 ? nt : pick_tile(c_out / 16);
   MSP_REQUIRE((c_out / 16) % NT == 0, "bad nt");
-  dim3 grid((unsigned)ceil_div(n_tiles, kWaves), (unsigned)(c_out / (16 * NT)));
+  const int n_y = c_out / (16 * NT);
+  const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
   hipStream_t s = as_stream(stream);
 #define L(N, A)                                                                                            \
   if (NT == N && abl == A)                                                                                 \
     conv_tile_kernel<N, A><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,   \
-                                                     chunk_src, chunk_row, n_rows, n_tiles, out);
+                                                     chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
 #define LN(N) L(N, 0) L(N, 1) L(N, 2) L(N, 3) L(N, 4) L(N, 5) L(N, 6) L(N, 7)
   LN(1) LN(2) LN(4)
 #define L4(N, A)                                                                                           \
   if (NT == N && abl == 16 + A)                                                                            \
     conv_tile4_kernel<N, A><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,  \
-                                                      chunk_src, chunk_row, n_rows, n_tiles, out);
-  L4(2, 0) L4(2, 1) L4(2, 2) L4(2, 3) L4(2, 4) L4(2, 7)
+                                                      chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
+  L4(2, 0) L4(2, 1) L4(2, 2) L4(2, 3) L4(2, 4) L4(2, 7) L4(2, 8) L4(2, 15)
 #undef L4
+  if (abl == 48) {
+    const int KC = c_in / 16;
+#define LP(N, C)                                                                                         \
+  if (NT == N && KC == C)                                                                                \
+    conv_tilep_kernel<N, C><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, \
+                                                      chunk_row, n_rows, n_tiles, n_y, out);
+    MSP_REQUIRE(c_in % 16 == 0 && KC <= 4, "tilep: c_in");
+    LP(1, 1) LP(1, 2) LP(1, 3) LP(1, 4) LP(2, 1) LP(2, 2) LP(2, 3) LP(2, 4)
+#undef LP
+  }
+  if (NT == 2 && abl == 32)
+    conv_tile4_kernel<2, 0, true><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
+                                                            chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
 
 #undef LN
 #undef L

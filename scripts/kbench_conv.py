@@ -47,8 +47,8 @@ for L, (size, c) in enumerate(zip(sizes, [32, 64, 96])):
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / 10
             extra = ""
-            if abl == 0:
+            if abl == variants[0]:
                 ref_out = out.clone()
-            elif abl >= 8:
+            else:
                 extra = f"  max|diff vs abl0|={(out - ref_out).abs().max().item():.2e}"
             print(f"   nt={nt} abl={abl}: {ms:.3f} ms  {flops / ms / 1e9:.1f} TF(alg){extra}")
