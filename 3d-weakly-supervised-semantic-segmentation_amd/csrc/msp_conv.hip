@@ -616,6 +616,126 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(
   }
 }
 
+// Vector form of the weight gradient.  Block = one slice of <= ppb pairs of
+// one offset and one (16WA x 16WB) tile of dW; MFMA k-step = 4 pairs, pair
+// 4g+q feeding lane group q.  Lane r loads WA consecutive input channels
+// m0 + WA*r .. and WB consecutive output channels n0 + WB*r .. of its pair
+// (16 lanes read whole 64-wide row slices), and the WA x WB MFMAs of a k-step
+// take component (sa, sb): accumulator (sa, sb) holds
+//   dW[m0 + WA*(4q + j) + sa][n0 + WB*r + sb]   (register j of lane (r, q)).
+// Indices run two k-steps ahead, values one.  Waves take k-steps round-robin;
+// their tiles are summed in fixed order into the block's slab (deterministic).
+template <int W>
+__device__ inline void load_vec(const float* p, float (&v)[W]) {
+  if (W == 4) {
+    const floatx4 t = *reinterpret_cast<const floatx4*>(p);
+#pragma unroll
+    for (int i = 0; i < W; ++i) v[i] = t[i];
+  } else if (W == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x;
+    v[W - 1] = t.y;
+  } else {
+#pragma unroll
+    for (int i = 0; i < W; ++i) v[i] = p[i];
+  }
+}
+
+template <int WA, int WB>
+__global__ __launch_bounds__(kThreads) void conv_wgrad4_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
+    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
+    const int64_t* __restrict__ block_start, int K, int64_t ppb, int n_ty, float* __restrict__ slab) {
+  constexpr int TM = 16 * WA, TN = 16 * WB;
+  __shared__ float red[TM * TN];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t b = lb / n_ty;
+  const int ty = (int)(lb % n_ty);
+  const int n_tj = c_out / TN;
+  const int m0 = (ty / n_tj) * TM, n0 = (ty % n_tj) * TN;
+  const int o = find_offset(block_start, K, b);
+  const int64_t p0 = off_start[o] + (b - block_start[o]) * ppb;
+  const int64_t p1 = min(p0 + ppb, off_start[o + 1]);
+
+  floatx4 acc[WA][WB];
+#pragma unroll
+  for (int i = 0; i < WA; ++i)
+#pragma unroll
+    for (int t = 0; t < WB; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  struct Ix {
+    int32_t i, o;
+  };
+  struct Vals {
+    float a[WA], b[WB];
+  };
+  auto ld_idx = [&](int64_t g, Ix& d) {
+    const int64_t pp = g + q;
+    const bool ok = pp < p1;
+    d.i = ok ? pin[pp] : -1;
+    d.o = ok ? pout[pp] : -1;
+  };
+  auto ld_val = [&](const Ix& d, Vals& v) {
+    if (d.i >= 0) {
+      load_vec<WA>(x + (int64_t)d.i * c_in + m0 + WA * r, v.a);
+      load_vec<WB>(dy + (int64_t)d.o * c_out + n0 + WB * r, v.b);
+    } else {
+#pragma unroll
+      for (int i = 0; i < WA; ++i) v.a[i] = 0.f;
+#pragma unroll
+      for (int t = 0; t < WB; ++t) v.b[t] = 0.f;
+    }
+  };
+  auto compute = [&](const Vals& v) {
+#pragma unroll
+    for (int i = 0; i < WA; ++i)
+#pragma unroll
+      for (int t = 0; t < WB; ++t) acc[i][t] = mfma4(v.a[i], v.b[t], acc[i][t]);
+  };
+
+  constexpr int64_t kStride = 4 * kWaves;
+  int64_t g = p0 + 4 * wave;
+  if (g < p1) {
+    Ix i0, i1;
+    Vals v0;
+    ld_idx(g, i0);
+    ld_idx(g + kStride, i1);
+    ld_val(i0, v0);
+    for (; g < p1; g += kStride) {
+      Ix i2;
+      Vals v1;
+      ld_idx(g + 2 * kStride, i2);
+      const bool more = g + kStride < p1;
+      if (more) ld_val(i1, v1);
+      compute(v0);
+      i1 = i2;
+      if (more) v0 = v1;
+    }
+  }
+  // deterministic cross-wave sum: wave 0 stores, waves 1..3 add in order
+  for (int w = 0; w < kWaves; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < WA; ++i)
+#pragma unroll
+        for (int t = 0; t < WB; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float* d = red + (WA * (4 * q + j) + i) * TN + WB * r + t;
+            *d = (w == 0) ? acc[i][t][j] : (*d + acc[i][t][j]);
+          }
+    }
+    __syncthreads();
+  }
+  float* sb = slab + b * (int64_t)c_in * c_out;
+  for (int e = threadIdx.x; e < TM * TN; e += kThreads) {
+    const int i = e / TN, j = e % TN;
+    sb[(int64_t)(m0 + i) * c_out + n0 + j] = red[e];
+  }
+}
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab,
                                                            const int64_t* __restrict__ block_start,
                                                            int64_t cc, float* __restrict__ dw) {
@@ -746,20 +866,21 @@ int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const i
                    int64_t pairs_per_block, int64_t n_blocks, float* slab, float* dw, msp_stream_t stream) {
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_wgrad: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
-  MSP_REQUIRE(pairs_per_block > 0 && pairs_per_block % 16 == 0, "msp_conv_wgrad: pairs_per_block % 16");
+  MSP_REQUIRE(pairs_per_block > 0 && pairs_per_block % 4 == 0, "msp_conv_wgrad: pairs_per_block % 4");
   hipStream_t s = as_stream(stream);
-  // dW tiles of at most 32 x 32 per block: the register pipeline holds two
-  // groups of operand values plus the accumulators (94 VGPRs at 2 x 2)
-  auto pick = [](int n16) { return n16 % 2 == 0 ? 2 : (n16 % 3 == 0 ? 3 : 1); };
-  const int MT = pick(c_in / 16), NT = pick(c_out / 16);
+  // dW tiles of up to 64 x 64 per block: the largest divisor <= 4 of the
+  // 16-channel group counts
+  auto pick = [](int n16) { return n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1)); };
+  const int WA = pick(c_in / 16), WB = pick(c_out / 16);
   if (n_blocks > 0) {
-    dim3 grid((unsigned)n_blocks, (unsigned)((c_in / (16 * MT)) * (c_out / (16 * NT))));
-#define LAUNCH(A, B)                                                                                  \
-  if (MT == A && NT == B)                                                                             \
-    conv_wgrad_kernel<A, B><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, \
-                                                      block_start, K, pairs_per_block, slab);
-#define LAUNCH_ROW(A) LAUNCH(A, 1) LAUNCH(A, 2) LAUNCH(A, 3)
-    LAUNCH_ROW(1) LAUNCH_ROW(2) LAUNCH_ROW(3)
+    const int n_ty = (c_in / (16 * WA)) * (c_out / (16 * WB));
+    const unsigned grid = (unsigned)(n_blocks * n_ty);
+#define LAUNCH(A, B)                                                                                           \
+  if (WA == A && WB == B)                                                                                      \
+    conv_wgrad4_kernel<A, B><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start,      \
+                                                       block_start, K, pairs_per_block, n_ty, slab);
+#define LAUNCH_ROW(A) LAUNCH(A, 1) LAUNCH(A, 2) LAUNCH(A, 3) LAUNCH(A, 4)
+    LAUNCH_ROW(1) LAUNCH_ROW(2) LAUNCH_ROW(3) LAUNCH_ROW(4)
 #undef LAUNCH_ROW
 #undef LAUNCH
   }

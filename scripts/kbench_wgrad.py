@@ -1,0 +1,41 @@
+"""Micro-benchmark of msp_conv_wgrad on the headline batch's real submanifold
+pair lists (levels 0-2), checked against a torch fp64 reference."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
+import __graft_entry__ as g; g.add_path()
+import torch
+import sparseconvnet as scn
+from sparseconvnet import ops
+from wsss3d.synthetic import make_batch
+b = make_batch(8, 50, seed=1)
+t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
+meta = t.metadata
+sizes = [4096, 2048, 1024, 512]
+for s_ in sizes[:-1]:
+    meta.downsample(s_, 2)
+for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 128])):
+    rules = meta.level(size).subm_rules(3)
+    p = rules.pairs
+    V = meta.level(size).n
+    x = torch.randn(V, c, device="cuda")
+    dy = torch.randn(V, c, device="cuda")
+    for _ in range(2):
+        dw = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    offs = p.off_start.cpu().tolist()
+    pin, pout = p.pair_in.long(), p.pair_out.long()
+    err = 0.0
+    for o in range(27):
+        s0, s1 = offs[o], offs[o + 1]
+        ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
+        err = max(err, ((dw[o].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
+    flops = 2.0 * rules.n_rules * c * c
+    print(f"L{L} V={V} R={rules.n_rules} blocks={p.n_blocks} ppb={p.pairs_per_block}: {ms:.3f} ms "
+          f"{flops / ms / 1e9:.1f} TF  max rel err {err:.2e}", flush=True)
