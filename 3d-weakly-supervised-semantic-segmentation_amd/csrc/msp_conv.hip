@@ -6,8 +6,9 @@
 //               (submanifold fwd + bwd-data, strided conv fwd, deconv bwd-data)
 //   conv_pairs  one contribution per output row over per-offset pair lists
 //               (deconv fwd, strided conv bwd-data)
-//   conv_wgrad  per-offset x^T dy reductions over pair lists with a
-//               deterministic slab reduction (every weight gradient)
+//   conv_wgrad  per-offset x^T dy reductions over row-band pieces of the
+//               pair lists with a deterministic slab reduction (every
+//               weight gradient)
 //
 // The f32-input MFMA computes exact fp32 fmaf chains (no xf32 on gfx950), so
 // results match an fp32 CPU reference up to summation order.
@@ -166,26 +167,19 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
     }
   };
   auto ld_val = [&](const St& d, floatx4 (&av)[KC], floatx4 (&bv)[NT][KC]) {
-    const float* xs = x + (int64_t)(d.src < 0 ? 0 : d.src) * C_IN + 4 * q;
+    // padding slots hold a present row (see the header); their result column
+    // is never stored
+    const float* xs = x + (int64_t)d.src * C_IN + 4 * q;
     const int ow = flip ? (K - 1 - d.o) : d.o;
     const float* wb = wt + ((int64_t)ow * c_out + c0 + r) * C_IN + 4 * q;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      av[kc] = d.src >= 0 ? *reinterpret_cast<const floatx4*>(xs + kc * 16) : floatx4{0.f, 0.f, 0.f, 0.f};
+      av[kc] = *reinterpret_cast<const floatx4*>(xs + kc * 16);
 #pragma unroll
       for (int t = 0; t < NT; ++t) bv[t][kc] = *reinterpret_cast<const floatx4*>(wb + t * 16 * C_IN + kc * 16);
     }
   };
-  St s0, s1;
-  ld_idx(cb, s0);
-  ld_idx(cb + 1, s1);
-  floatx4 a0[KC], b0[NT][KC];
-  if (cb < ce) ld_val(s0, a0, b0);
-  for (int64_t c = cb; c < ce; ++c) {
-    St s2;
-    ld_idx(c + 2, s2);
-    floatx4 a1[KC], b1[NT][KC];
-    if (c + 1 < ce) ld_val(s1, a1, b1);
+  auto run = [&](const floatx4 (&av)[KC], const floatx4 (&bv)[NT][KC], int row) {
     floatx4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -194,19 +188,31 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma4(b0[t][kc][s], a0[kc][s], acc[t]);
-    if (s0.row < MSP_TILE_ROWS) {
+        for (int t = 0; t < NT; ++t) acc[t] = mfma4(bv[t][kc][s], av[kc][s], acc[t]);
+    if (row < MSP_TILE_ROWS) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(s0.row, 4 * t + q)) += acc[t];
+      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
     }
-    s0 = s1;
-    s1 = s2;
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      a0[kc] = a1[kc];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) b0[t][kc] = b1[t][kc];
-    }
+  };
+  // Two register sets used in turn (no copies of loaded registers, which
+  // would make the wave wait for them early): while chunk c computes from one
+  // set, chunk c+1's rows and weights load into the other and chunk c+2's
+  // indices into c's index slot.
+  St iA, iB;
+  floatx4 aA[KC], bA[NT][KC], aB[KC], bB[NT][KC];
+  ld_idx(cb, iA);
+  ld_idx(cb + 1, iB);
+  if (cb < ce) ld_val(iA, aA, bA);
+  for (int64_t c = cb; c < ce; c += 2) {
+    int row = iA.row;
+    if (c + 1 < ce) ld_val(iB, aB, bB);
+    ld_idx(c + 2, iA);
+    run(aA, bA, row);
+    if (c + 1 >= ce) break;
+    row = iB.row;
+    if (c + 2 < ce) ld_val(iA, aA, bA);
+    ld_idx(c + 3, iB);
+    run(aB, bB, row);
   }
   const int64_t row0 = tile * MSP_TILE_ROWS;
   const int nr = (int)((n_rows - row0) < MSP_TILE_ROWS ? (n_rows - row0) : MSP_TILE_ROWS);
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
 // one barrier per step) and every wave applies it to its <= 4 chunks of that
 // offset: all gathers of the step are issued before the first MFMA.
 template <int NT, int ABL = 0, bool PF = false>
-__global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void conv_tile4_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
@@ -271,20 +277,26 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     }
   }
   __syncthreads();
-  unsigned long long it0 = need[0], it1 = need[1];
+  // wave-uniform offset masks in scalar registers
+  auto uniform64 = [](unsigned long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+  };
+  unsigned long long it0 = uniform64(need[0]), it1 = uniform64(need[1]);
   const int nks = (c_in + 63) >> 6;
   const int n_steps = (__popcll(it0) + __popcll(it1)) * nks;
 
   floatx4 stage[SPT];
   auto next_offset = [&](unsigned long long& m0, unsigned long long& m1) {
-    int o;
-    if (m0) {
-      o = __ffsll((long long)m0) - 1;
-      m0 &= m0 - 1;
-    } else {
-      o = 64 + __ffsll((long long)m1) - 1;
-      m1 &= m1 - 1;
-    }
+    // branch-free (a data-dependent choice between the two references made
+    // the compiler keep them in scratch)
+    const bool lo = m0 != 0ull;
+    const unsigned long long mm = lo ? m0 : m1;
+    const int o = (lo ? 0 : 64) + __ffsll((long long)mm) - 1;
+    const unsigned long long nm = mm & (mm - 1);
+    m0 = lo ? nm : m0;
+    m1 = lo ? m1 : nm;
     return o;
   };
   auto load_slice = [&](int o, int ks) {
@@ -314,8 +326,8 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     int src[4], row[4], gn;
   };
   auto load_idx = [&](int o, Idx& d) {
-    d.gn = gcount[wave][o];
-    const int64_t g0 = cb + gfirst[wave][o];
+    d.gn = __builtin_amdgcn_readfirstlane(gcount[wave][o]);
+    const int64_t g0 = cb + __builtin_amdgcn_readfirstlane(gfirst[wave][o]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       d.src[j] = (j < d.gn) ? chunk_src[(g0 + j) * MSP_CHUNK + r] : -1;
@@ -326,14 +338,17 @@ __global__ __launch_bounds__(kThreads) void conv_tile4_kernel(
     const int kcs = min(4, (c_in - kslice * 64) >> 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float* xs = x + (int64_t)(d.src[j] < 0 ? 0 : d.src[j]) * c_in + kslice * 64 + 4 * q;
+      // padding slots hold a present row (see the header); their result
+      // column is never stored
+      const float* xs = x + (int64_t)d.src[j] * c_in + kslice * 64 + 4 * q;
+      if (j < d.gn) {
 #pragma unroll
-      for (int kc = 0; kc < 4; ++kc) {
-        if (ABL & 1)
-          av[j][kc] = floatx4{(float)d.src[j], (float)kc, 1.f, 2.f};
-        else
-          av[j][kc] = (d.src[j] >= 0 && kc < kcs) ? *reinterpret_cast<const floatx4*>(xs + kc * 16)
-                                                  : floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int kc = 0; kc < 4; ++kc) {
+          if (ABL & 1)
+            av[j][kc] = floatx4{(float)d.src[j], (float)kc, 1.f, 2.f};
+          else if (kc < kcs)
+            av[j][kc] = *reinterpret_cast<const floatx4*>(xs + kc * 16);
+        }
       }
     }
   };
@@ -500,130 +515,15 @@ __global__ __launch_bounds__(kThreads) void conv_pairs_kernel(
 }
 
 // ---------------------------------------------------------------- conv_wgrad
-// Block = one slice of <= pairs_per_block pairs of one offset and one
-// (16MT x 16NT) tile of dW.  The contraction runs over pairs: MFMA k-step s of
-// lane group q takes pair 4q+s of a 16-pair group, so each lane reads its 4
-// pairs' indices as one int4, and its operand values X[pair][m0+16i+r],
-// dY[pair][n0+16t+r] as scalars (16 lanes = 64 contiguous bytes of a row).
-// Software pipeline: the indices of group g+2 and the values of group g+1 are
-// in flight while group g's MFMAs run.  The four waves interleave groups; their
-// tiles are summed in fixed order and written to the block's slab.
-template <int MT, int NT>
-struct WgVals {
-  float x[4][MT];
-  float y[4][NT];
-};
-
-template <int MT, int NT>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(
-    const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
-    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
-    const int64_t* __restrict__ block_start, int K, int64_t ppb, float* __restrict__ slab) {
-  __shared__ float red[16 * MT * 16 * NT];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 15, q = lane >> 4;
-  const int64_t b = blockIdx.x;
-  const int o = find_offset(block_start, K, b);
-  const int64_t p0 = off_start[o] + (b - block_start[o]) * ppb;
-  const int64_t p1 = min(p0 + ppb, off_start[o + 1]);
-  const int n_tj = c_out / (16 * NT);
-  const int m0 = (blockIdx.y / n_tj) * 16 * MT, n0 = (blockIdx.y % n_tj) * 16 * NT;
-
-  floatx4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // groups of this wave: g_k = p0 + 16 * (wave + 4k)
-  const int64_t gstride = 16 * kWaves;
-  auto load_idx = [&](int64_t g, int32_t (&ii)[4], int32_t (&io)[4]) {
-    const int64_t pp = g + 4 * q;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bool ok = pp + s < p1;
-      ii[s] = ok ? pin[pp + s] : -1;
-      io[s] = ok ? pout[pp + s] : -1;
-    }
-  };
-  auto load_vals = [&](const int32_t (&ii)[4], const int32_t (&io)[4], WgVals<MT, NT>& v) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float* xr = x + (int64_t)(ii[s] < 0 ? 0 : ii[s]) * c_in + m0 + r;
-      const float* yr = dy + (int64_t)(io[s] < 0 ? 0 : io[s]) * c_out + n0 + r;
-#pragma unroll
-      for (int i = 0; i < MT; ++i) v.x[s][i] = ii[s] < 0 ? 0.f : xr[16 * i];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) v.y[s][t] = io[s] < 0 ? 0.f : yr[16 * t];
-    }
-  };
-  auto compute = [&](const WgVals<MT, NT>& v) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[i][t] = mfma4(v.x[s][i], v.y[s][t], acc[i][t]);
-  };
-
-  int64_t g = p0 + 16 * wave;
-  if (g < p1) {
-    int32_t ia[4], oa[4], ib[4], ob[4];
-    WgVals<MT, NT> va, vb;
-    load_idx(g, ia, oa);
-    load_vals(ia, oa, va);
-    load_idx(g + gstride, ib, ob);
-    for (;;) {
-      // even: compute va (group g); values of g+stride -> vb; indices of g+2*stride -> ia
-      const bool n1 = g + gstride < p1;
-      if (n1) {
-        load_vals(ib, ob, vb);
-        load_idx(g + 2 * gstride, ia, oa);
-      }
-      compute(va);
-      g += gstride;
-      if (!n1) break;
-      const bool n2 = g + gstride < p1;
-      if (n2) {
-        load_vals(ia, oa, va);
-        load_idx(g + 2 * gstride, ib, ob);
-      }
-      compute(vb);
-      g += gstride;
-      if (!n2) break;
-    }
-  }
-  // deterministic cross-wave sum: wave 0 stores, waves 1..3 add in order
-  constexpr int RN = 16 * NT;
-  for (int w = 0; w < kWaves; ++w) {
-    if (wave == w) {
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float* d = red + (i * 16 + 4 * q + j) * RN + t * 16 + r;
-            *d = (w == 0) ? acc[i][t][j] : (*d + acc[i][t][j]);
-          }
-    }
-    __syncthreads();
-  }
-  float* sb = slab + b * (int64_t)c_in * c_out;
-  for (int e = threadIdx.x; e < 16 * MT * RN; e += kThreads) {
-    const int i = e / RN, j = e % RN;
-    sb[(int64_t)(m0 + i) * c_out + n0 + j] = red[e];
-  }
-}
-
-// Vector form of the weight gradient.  Block = one slice of <= ppb pairs of
-// one offset and one (16WA x 16WB) tile of dW; MFMA k-step = 4 pairs, pair
-// 4g+q feeding lane group q.  Lane r loads WA consecutive input channels
+// Weight gradient.  Block = piece j of offset o's pair list (see
+// msp_conv_wgrad in the header) and one (16WA x 16WB) tile of dW; MFMA k-step = 4 pairs, one per
+// lane group q.  Lane r loads WA consecutive input channels
 // m0 + WA*r .. and WB consecutive output channels n0 + WB*r .. of its pair
 // (16 lanes read whole 64-wide row slices), and the WA x WB MFMAs of a k-step
 // take component (sa, sb): accumulator (sa, sb) holds
 //   dW[m0 + WA*(4q + j) + sa][n0 + WB*r + sb]   (register j of lane (r, q)).
-// Indices run two k-steps ahead, values one.  Waves take k-steps round-robin;
+// Indices run two 16-pair super-steps ahead, values one.  Waves take
+// super-steps round-robin;
 // their tiles are summed in fixed order into the block's slab (deterministic).
 template <int W>
 __device__ inline void load_vec(const float* p, float (&v)[W]) {
@@ -642,22 +542,26 @@ __device__ inline void load_vec(const float* p, float (&v)[W]) {
 }
 
 template <int WA, int WB>
-__global__ __launch_bounds__(kThreads) void conv_wgrad4_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WA * WB > 9 ? 2 : 3))) void conv_wgrad4_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
     const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
-    const int64_t* __restrict__ block_start, int K, int64_t ppb, int n_ty, float* __restrict__ slab) {
+    int K, int64_t n_pieces, int n_ty, float* __restrict__ slab) {
   constexpr int TM = 16 * WA, TN = 16 * WB;
   __shared__ float red[TM * TN];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
+  // logical block = ((piece j * K) + offset o) * n_ty + channel tile: the K
+  // pieces of one row band and their channel tiles are adjacent on one XCD
   const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
-  const int64_t b = lb / n_ty;
+  const int64_t b = lb / n_ty;  // slab index j * K + o
   const int ty = (int)(lb % n_ty);
   const int n_tj = c_out / TN;
   const int m0 = (ty / n_tj) * TM, n0 = (ty % n_tj) * TN;
-  const int o = find_offset(block_start, K, b);
-  const int64_t p0 = off_start[o] + (b - block_start[o]) * ppb;
-  const int64_t p1 = min(p0 + ppb, off_start[o + 1]);
+  const int o = (int)(b % K);
+  const int64_t j = b / K;
+  const int64_t os = off_start[o], cnt = off_start[o + 1] - os;
+  const int64_t p0 = os + cnt * j / n_pieces;
+  const int64_t p1 = os + cnt * (j + 1) / n_pieces;
 
   floatx4 acc[WA][WB];
 #pragma unroll
@@ -665,53 +569,75 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad4_kernel(
 #pragma unroll
     for (int t = 0; t < WB; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // super-step = 16 pairs: lane group q takes pairs g + 4q .. g + 4q + 3 as
+  // its four k-steps.  Loads are branch-free and nothing is computed from a
+  // loaded value until it is consumed (a select right after a load would make
+  // the wave wait for every younger load too): positions past the piece are
+  // clamped to its last pair and masked out when the MFMA operands are formed.
   struct Ix {
-    int32_t i, o;
+    int32_t i[4], o[4];
+    bool ok[4];
   };
   struct Vals {
-    float a[WA], b[WB];
+    float a[4][WA], b[4][WB];
+    bool ok[4];
   };
   auto ld_idx = [&](int64_t g, Ix& d) {
-    const int64_t pp = g + q;
-    const bool ok = pp < p1;
-    d.i = ok ? pin[pp] : -1;
-    d.o = ok ? pout[pp] : -1;
+    const int64_t pp = g + 4 * q;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t pc = min(pp + k, p1 - 1);
+      d.ok[k] = pp + k < p1;
+      d.i[k] = pin[pc];
+      d.o[k] = pout[pc];
+    }
   };
   auto ld_val = [&](const Ix& d, Vals& v) {
-    if (d.i >= 0) {
-      load_vec<WA>(x + (int64_t)d.i * c_in + m0 + WA * r, v.a);
-      load_vec<WB>(dy + (int64_t)d.o * c_out + n0 + WB * r, v.b);
-    } else {
 #pragma unroll
-      for (int i = 0; i < WA; ++i) v.a[i] = 0.f;
-#pragma unroll
-      for (int t = 0; t < WB; ++t) v.b[t] = 0.f;
+    for (int k = 0; k < 4; ++k) {
+      load_vec<WA>(x + (int64_t)d.i[k] * c_in + m0 + WA * r, v.a[k]);
+      load_vec<WB>(dy + (int64_t)d.o[k] * c_out + n0 + WB * r, v.b[k]);
+      v.ok[k] = d.ok[k];
     }
   };
   auto compute = [&](const Vals& v) {
 #pragma unroll
-    for (int i = 0; i < WA; ++i)
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int t = 0; t < WB; ++t) acc[i][t] = mfma4(v.a[i], v.b[t], acc[i][t]);
+      for (int i = 0; i < WA; ++i) {
+        const float av = v.ok[k] ? v.a[k][i] : 0.f;
+#pragma unroll
+        for (int t = 0; t < WB; ++t) acc[i][t] = mfma4(av, v.b[k][t], acc[i][t]);
+      }
   };
 
-  constexpr int64_t kStride = 4 * kWaves;
-  int64_t g = p0 + 4 * wave;
+  // two register sets used in turn (no copies), so a set's loads are only
+  // waited for when that set is computed, one super-step later
+  constexpr int64_t kStride = 16 * kWaves;
+  int64_t g = p0 + 16 * wave;
   if (g < p1) {
-    Ix i0, i1;
-    Vals v0;
-    ld_idx(g, i0);
-    ld_idx(g + kStride, i1);
-    ld_val(i0, v0);
-    for (; g < p1; g += kStride) {
-      Ix i2;
-      Vals v1;
-      ld_idx(g + 2 * kStride, i2);
-      const bool more = g + kStride < p1;
-      if (more) ld_val(i1, v1);
-      compute(v0);
-      i1 = i2;
-      if (more) v0 = v1;
+    Ix ia, ib;
+    Vals va, vb;
+    ld_idx(g, ia);
+    ld_val(ia, va);
+    ld_idx(g + kStride, ib);
+    for (;;) {
+      const bool n1 = g + kStride < p1;
+      if (n1) {
+        ld_val(ib, vb);
+        ld_idx(g + 2 * kStride, ia);
+      }
+      compute(va);
+      g += kStride;
+      if (!n1) break;
+      const bool n2 = g + kStride < p1;
+      if (n2) {
+        ld_val(ia, va);
+        ld_idx(g + 2 * kStride, ib);
+      }
+      compute(vb);
+      g += kStride;
+      if (!n2) break;
     }
   }
   // deterministic cross-wave sum: wave 0 stores, waves 1..3 add in order
@@ -736,15 +662,16 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad4_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                           const int64_t* __restrict__ block_start,
-                                                           int64_t cc, float* __restrict__ dw) {
+// dw[o][e] = sum over pieces j (in order) of slab[j][o][e]
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int64_t n_pieces,
+                                                           int K, int64_t cc, float* __restrict__ dw) {
   const int o = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= cc) return;
-  const int64_t b0 = block_start[o], b1 = block_start[o + 1];
+  const float* p = slab + (int64_t)o * cc + e;
+  const int64_t stride = (int64_t)K * cc;
   float s = 0.f;
-  for (int64_t b = b0; b < b1; ++b) s += slab[b * cc + e];
+  for (int64_t j = 0; j < n_pieces; ++j) s += p[j * stride];
   dw[(int64_t)o * cc + e] = s;
 }
 
@@ -861,32 +788,39 @@ int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, 
   return check_launch("msp_conv_pairs");
 }
 
+int64_t msp_wgrad_pieces(int64_t total_pairs, int K) {
+  // about 512 pairs per piece and at most ~3072 pieces x offsets per launch
+  if (K < 1) return 1;
+  int64_t n = total_pairs / ((int64_t)K * 512);
+  const int64_t cap = 3072 / K > 1 ? 3072 / K : 1;
+  if (n > cap) n = cap;
+  return n < 1 ? 1 : n;
+}
+
 int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
-                   const int32_t* pair_out, const int64_t* off_start, const int64_t* block_start, int K,
-                   int64_t pairs_per_block, int64_t n_blocks, float* slab, float* dw, msp_stream_t stream) {
+                   const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
+                   float* dw, msp_stream_t stream) {
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_wgrad: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
-  MSP_REQUIRE(pairs_per_block > 0 && pairs_per_block % 4 == 0, "msp_conv_wgrad: pairs_per_block % 4");
+  MSP_REQUIRE(K >= 1 && n_pieces >= 1, "msp_conv_wgrad: K=%d n_pieces=%lld", K, (long long)n_pieces);
   hipStream_t s = as_stream(stream);
   // dW tiles of up to 64 x 64 per block: the largest divisor <= 4 of the
   // 16-channel group counts
   auto pick = [](int n16) { return n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1)); };
   const int WA = pick(c_in / 16), WB = pick(c_out / 16);
-  if (n_blocks > 0) {
-    const int n_ty = (c_in / (16 * WA)) * (c_out / (16 * WB));
-    const unsigned grid = (unsigned)(n_blocks * n_ty);
-#define LAUNCH(A, B)                                                                                           \
-  if (WA == A && WB == B)                                                                                      \
-    conv_wgrad4_kernel<A, B><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start,      \
-                                                       block_start, K, pairs_per_block, n_ty, slab);
+  const int n_ty = (c_in / (16 * WA)) * (c_out / (16 * WB));
+  const unsigned grid = (unsigned)(n_pieces * K * n_ty);
+#define LAUNCH(A, B)                                                                                         \
+  if (WA == A && WB == B)                                                                                    \
+    conv_wgrad4_kernel<A, B><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, K, \
+                                                       n_pieces, n_ty, slab);
 #define LAUNCH_ROW(A) LAUNCH(A, 1) LAUNCH(A, 2) LAUNCH(A, 3) LAUNCH(A, 4)
-    LAUNCH_ROW(1) LAUNCH_ROW(2) LAUNCH_ROW(3) LAUNCH_ROW(4)
+  LAUNCH_ROW(1) LAUNCH_ROW(2) LAUNCH_ROW(3) LAUNCH_ROW(4)
 #undef LAUNCH_ROW
 #undef LAUNCH
-  }
   const int64_t cc = (int64_t)c_in * c_out;
   dim3 g2((unsigned)ceil_div(cc, 256), (unsigned)K);
-  wgrad_reduce_kernel<<<g2, 256, 0, s>>>(slab, block_start, cc, dw);
+  wgrad_reduce_kernel<<<g2, 256, 0, s>>>(slab, n_pieces, K, cc, dw);
   return check_launch("msp_conv_wgrad");
 }
 

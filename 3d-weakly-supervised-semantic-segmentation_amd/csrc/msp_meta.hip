@@ -246,6 +246,9 @@ __global__ __launch_bounds__(kThreads) void tile_fill_kernel(const int32_t* __re
     const int pc = __popcll(m);
     if (pc == 0) continue;
     const int nch = (pc + kChunk - 1) / kChunk;
+    // padding slots repeat the offset's first present input row (in bounds and
+    // nearby for the gather); chunk_row = kTile marks them
+    const int32_t vfirst = __shfl(v, __ffsll((long long)m) - 1);
     if (v >= 0) {
       const int pos = mbcnt64(m);
       const int64_t e = (c + pos / kChunk) * kChunk + (pos % kChunk);
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(kThreads) void tile_fill_kernel(const int32_t* __re
     }
     if (lane >= pc && lane < nch * kChunk) {  // padding slots of the last chunk
       const int64_t e = (c + lane / kChunk) * kChunk + (lane % kChunk);
-      chunk_src[e] = -1;
+      chunk_src[e] = vfirst;
       chunk_row[e] = (uint8_t)kTile;
     }
     if (lane < nch) chunk_off[c + lane] = (uint8_t)o;

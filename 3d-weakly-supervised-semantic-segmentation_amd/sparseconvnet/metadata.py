@@ -81,14 +81,6 @@ class PairLists:
             cs.append(cs[-1] + (c + CHUNK - 1) // CHUNK)
         self.n_chunks = cs[-1]
         self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(device, non_blocking=True)
-        # weight-gradient blocks: about 2048 blocks in total
-        ppb = max(256, -(-self.total // 2048))
-        self.pairs_per_block = ((ppb + CHUNK - 1) // CHUNK) * CHUNK
-        bs = [0]
-        for c in self.counts:
-            bs.append(bs[-1] + (c + self.pairs_per_block - 1) // self.pairs_per_block)
-        self.n_blocks = bs[-1]
-        self.block_start = torch.tensor(bs, dtype=torch.int64).to(device, non_blocking=True)
 
 
 class SubmRules:

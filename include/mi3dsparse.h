@@ -96,7 +96,9 @@ int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32
  * MSP_TILE_ROWS; inside a tile the present (row, offset) pairs of each offset
  * are compacted (wavefront ballot + prefix sum) into chunks of MSP_CHUNK.
  * tile_start[n_tiles+1] (device int64), chunk_off[c] = offset, chunk_src[c*16+j]
- * = input row (-1 pad), chunk_row[c*16+j] = row inside the tile (64 for pad).
+ * = input row, chunk_row[c*16+j] = row inside the tile.  Padding slots of a
+ * chunk have chunk_row = 64 and repeat a present input row of the same tile
+ * and offset (so every gather stays in bounds).
  * Count-then-fill like msp_pair_lists (total chunks = tile_start[n_tiles]). */
 int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int64_t* tile_start, uint8_t* chunk_off,
                       int32_t* chunk_src, uint8_t* chunk_row, int64_t chunk_cap, void* ws, size_t ws_bytes,
@@ -123,14 +125,17 @@ int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, 
                    const int32_t* pair_out, const int64_t* off_start, const int64_t* chunk_start,
                    int64_t n_chunks, float* out, msp_stream_t stream);
 /* Weight gradient dW[o] (c_in x c_out) = sum over pairs of offset o of
- * x[pair_in]^T dy[pair_out].  Blocks of `pairs_per_block` pairs write
- * partial tiles to slab[n_blocks][c_in][c_out]; block_start[K+1] (device) =
- * prefix sums of ceil(n_o / pairs_per_block), n_blocks = block_start[K].  A
- * second kernel reduces the slabs in block order (deterministic) into
- * dw[K][c_in][c_out]. */
+ * x[pair_in]^T dy[pair_out].  Each offset's pair list (sorted by one side's
+ * row) is cut into n_pieces equal pieces; piece j of every offset covers
+ * about the same row band, and the K pieces of a band run together so the
+ * band's rows are read from L2 once.  Piece (j, o) writes its partial tile to
+ * slab[n_pieces][K][c_in][c_out]; a second kernel reduces the pieces in order
+ * j = 0, 1, ... (deterministic) into dw[K][c_in][c_out].  msp_wgrad_pieces
+ * gives the piece count the library is tuned for. */
+int64_t msp_wgrad_pieces(int64_t total_pairs, int K);
 int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
-                   const int32_t* pair_out, const int64_t* off_start, const int64_t* block_start, int K,
-                   int64_t pairs_per_block, int64_t n_blocks, float* slab, float* dw, msp_stream_t stream);
+                   const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
+                   float* dw, msp_stream_t stream);
 
 /* ---------------- batch norm + (leaky) ReLU (replaces SCN BatchNormalization
  * with leakiness; scn.BatchNormReLU / BatchNormLeakyReLU).

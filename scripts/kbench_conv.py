@@ -34,6 +34,8 @@ for L, (size, c) in enumerate(zip(sizes, [32, 64, 96])):
         if (c // 16) % nt:
             continue
         for abl in variants:
+            if abl == 48 and c > 64:
+                continue
             args = (abl, nt, ptr(x), c, ptr(wt), 27, 0, c, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
                     ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), _lib.stream())
             for _ in range(3):

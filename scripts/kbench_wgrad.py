@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
 import __graft_entry__ as g; g.add_path()
 import torch
 import sparseconvnet as scn
-from sparseconvnet import ops
+from sparseconvnet import ops, _lib
 from wsss3d.synthetic import make_batch
 b = make_batch(8, 50, seed=1)
 t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
@@ -37,5 +37,5 @@ for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 128])):
         ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
         err = max(err, ((dw[o].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
     flops = 2.0 * rules.n_rules * c * c
-    print(f"L{L} V={V} R={rules.n_rules} blocks={p.n_blocks} ppb={p.pairs_per_block}: {ms:.3f} ms "
+    print(f"L{L} V={V} R={rules.n_rules} pieces={_lib.query('msp_wgrad_pieces', _lib.I64(p.total), 27)}: {ms:.3f} ms "
           f"{flops / ms / 1e9:.1f} TF  max rel err {err:.2e}", flush=True)

@@ -1,0 +1,43 @@
+"""Per-dispatch view of rocprofv3 --pmc passes: for kernels matching FILTER,
+group dispatches by (kernel, grid size) -- one group per problem size -- and
+print every counter's mean per dispatch plus derived ratios.
+Usage: pmc_dispatch.py DIR FILTER"""
+import csv, glob, os, sys
+from collections import defaultdict
+
+root, filt = sys.argv[1], sys.argv[2]
+groups = defaultdict(lambda: defaultdict(list))
+order = []
+for f in sorted(glob.glob(os.path.join(root, "pass*", "**", "*counter_collection.csv"), recursive=True)):
+    for r in csv.DictReader(open(f)):
+        name = r["Kernel_Name"].split("(")[0]
+        if filt not in name:
+            continue
+        key = (name.replace("void msp::", "")[:40], int(r["Grid_Size"]))
+        if key not in groups:
+            order.append(key)
+        groups[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        groups[key]["_dur_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+for key in order:
+    c = {k: sum(v) / len(v) for k, v in groups[key].items()}
+    out = [f"{key[0]} grid={key[1]} dur={c['_dur_ns'] / 1e3:.0f}us"]
+    g = c.get("GRBM_GUI_ACTIVE")
+    if g and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+        out.append(f"mfma_util={c['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * 1024):.2f}")
+    if "SQ_WAVE_CYCLES" in c:
+        w = c["SQ_WAVE_CYCLES"]
+        out.append(f"wait_any={c['SQ_WAIT_ANY'] / w:.2f} wait_inst={c['SQ_WAIT_INST_ANY'] / w:.2f} "
+                   f"active={c['SQ_ACTIVE_INST_ANY'] / w:.2f}")
+    if "TCP_TCC_READ_REQ_sum" in c:
+        out.append(f"l2_lat={c['TCP_TCC_READ_REQ_LATENCY_sum'] / max(c['TCP_TCC_READ_REQ_sum'], 1):.0f}cyc "
+                   f"l2_reqs={c['TCP_TCC_READ_REQ_sum']:.3g}")
+    if "TA_BUSY_avr" in c and g:
+        out.append(f"ta_busy={c['TA_BUSY_avr'] / g:.2f}")
+    if "TCC_HIT_sum" in c:
+        out.append(f"l2_hit={c['TCC_HIT_sum'] / max(c['TCC_HIT_sum'] + c['TCC_MISS_sum'], 1):.2f}")
+    if "FETCH_SIZE" in c:
+        out.append(f"fetch={2 * c['FETCH_SIZE'] / 1e3:.0f}MB(x2)")
+    if "TCP_PENDING_STALL_CYCLES_sum" in c and g:
+        out.append(f"tcp_pend={c['TCP_PENDING_STALL_CYCLES_sum'] / g / 256:.2f} "
+                   f"tcr_stall={c['TCP_TCR_TCP_STALL_CYCLES_sum'] / g / 256:.2f}")
+    print(" ".join(out))
