@@ -43,8 +43,13 @@ __device__ inline int64_t xcd_linear(int64_t bid, int64_t nb) {
 // 16 distinct bank quads (ds_read/write_b128 are served per 16 lanes).
 template <int NC>
 __device__ inline int acc_pos(int row, int g) {
-  constexpr int RP = 64 / NC, GM = NC / 4 - 1;
-  return row * NC + 4 * (g ^ ((row / RP) & GM));
+  constexpr int G = NC / 4;
+  if constexpr ((G & (G - 1)) == 0) {
+    constexpr int RP = NC >= 64 ? 1 : 64 / NC;
+    return row * NC + 4 * (g ^ ((row / RP) & (G - 1)));
+  } else {
+    return row * NC + 4 * ((g + row) % G);
+  }
 }
 
 // ---------------------------------------------------------------- conv_tile
@@ -61,7 +66,7 @@ template <int NT, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void conv_tile_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
-    const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
+    const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
     int64_t n_tiles, int n_y, float* __restrict__ out) {
   constexpr int NC = 16 * NT;
   __shared__ floatx4 lds4[kWaves][MSP_TILE_ROWS * NC / 4];
@@ -134,20 +139,20 @@ __global__ __launch_bounds__(kThreads) void conv_tile_kernel(
 // Pipelined per-wave form for c_in = 16*KC <= 64: chunk indices are loaded
 // two chunks ahead, input rows and weight fragments one chunk ahead, so a
 // wave always has the next chunk's loads in flight while it runs MFMAs.
-template <int NT, int KC>
+template <int NT, int KC, int TR = MSP_TILE_ROWS>
 __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
     const float* __restrict__ x, const float* __restrict__ wt, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
-    const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
+    const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
     int64_t n_tiles, int n_y, float* __restrict__ out) {
   constexpr int NC = 16 * NT, C_IN = 16 * KC;
-  __shared__ floatx4 lds4[kWaves][MSP_TILE_ROWS * NC / 4];
+  __shared__ floatx4 lds4[kWaves][TR * NC / 4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
   const int64_t tile = (lb / n_y) * kWaves + wave;
   if (tile >= n_tiles) return;  // wave-uniform; the kernel has no block barrier
   float* acc_s = reinterpret_cast<float*>(lds4[wave]);
-  for (int i = lane; i < MSP_TILE_ROWS * NC / 4; i += 64) lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int i = lane; i < TR * NC / 4; i += 64) lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int c0 = (int)(lb % n_y) * NC;
   const int r = lane & 15, q = lane >> 4;
   const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
@@ -163,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
     } else {
       d.o = 0;
       d.src = -1;
-      d.row = MSP_TILE_ROWS;
+      d.row = TR;
     }
   };
   auto ld_val = [&](const St& d, floatx4 (&av)[KC], floatx4 (&bv)[NT][KC]) {
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] = mfma4(bv[t][kc][s], av[kc][s], acc[t]);
-    if (row < MSP_TILE_ROWS) {
+    if (row < TR) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
     }
@@ -214,8 +219,8 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
     ld_idx(c + 3, iB);
     run(aB, bB, row);
   }
-  const int64_t row0 = tile * MSP_TILE_ROWS;
-  const int nr = (int)((n_rows - row0) < MSP_TILE_ROWS ? (n_rows - row0) : MSP_TILE_ROWS);
+  const int64_t row0 = tile * TR;
+  const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
   constexpr int V4 = NC / 4;
   for (int i = lane; i < nr * V4; i += 64) {
     const int rr = i / V4, g = i % V4;
@@ -235,7 +240,7 @@ template <int NT, int ABL = 0, bool PF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void conv_tile4_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
-    const int32_t* __restrict__ chunk_src, const uint8_t* __restrict__ chunk_row, int64_t n_rows,
+    const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
     int64_t n_tiles, int n_y, float* __restrict__ out) {
   constexpr int NC = 16 * NT;
   constexpr int BF4 = 16 * NC;  // float4 per 64-channel weight slice, [k/4][n]
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
 #pragma unroll
     for (int i = 0; i < SPT; ++i) {
       const int f = tid + kThreads * i;
-      if (f < BF4) wbuf[buf][(f & 15) * NC + (f >> 4)] = stage[i];
+      if (f < BF4) wbuf[buf][(f & 15) * NC + ((f >> 4) ^ (f & 15))] = stage[i];  // n ^ kq: conflict-free
     }
   };
 
@@ -400,7 +405,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           if (ABL & 2) b[t] = floatx4{(float)t, (float)kc, 0.5f, (float)o_cur};
-          else b[t] = wb[(kc * 4 + q) * NC + t * 16 + r];
+          else b[t] = wb[(kc * 4 + q) * NC + ((t * 16 + r) ^ (kc * 4 + q))];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -456,6 +461,315 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) v
     *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
         *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
   }
+}
+
+// ---------------------------------------------------------------- conv_tile (shared tile, software pipelined)
+// Block = 4 waves sharing ONE output tile of TR rows and one 16*NT
+// output-channel slice, accumulated in LDS.  The block walks the offsets the
+// tile needs in (offset, 64-channel k-slice) steps; the weight slice is
+// staged in LDS once per step (double-buffered, one barrier per step) and the
+// offset's chunks are dealt round-robin to the waves (wave w takes chunks w,
+// w+4, ...).  Chunks of one offset cover distinct rows, so the waves' LDS
+// read-modify-writes of a step never collide, and the per-step barrier
+// orders steps.  Compared with per-wave 64-row tiles the larger tile packs
+// the chunks denser (fewer padding rows) and the waves of a step carry
+// equal work.  The kernel is written so that no load is ever
+// waited for before it is consumed: every load is unconditional (indices and
+// channel offsets are clamped into range; the work they would feed is
+// skipped by uniform branches), loaded registers are never copied, and the
+// register sets of consecutive steps alternate by unrolling the step loop
+// by two.  Per step s, in issue order:
+//   barrier | src(s+2) | weights(s+1) | gathers(s+1) | MFMAs(s) | LDS
+//   read-modify-write(s) | rows(s+2) | weights(s+1) -> LDS
+// so the gathers of a step have a whole step of MFMAs to land, and the
+// index loads two.
+template <int NT, int TR, int ABL = 0>
+__global__ __launch_bounds__(kThreads) void conv_tile7_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int flip, int c_out,
+    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
+    const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
+    int n_y, int n_split, float* __restrict__ out) {
+  constexpr int NC = 16 * NT;
+  constexpr int BF4 = 16 * NC;  // float4 per 64-channel weight slice, [k/4][n]
+  constexpr int SPT = (BF4 + kThreads - 1) / kThreads;
+  constexpr int MJ = TR / (16 * kWaves);  // chunk slots per wave and step
+  __shared__ floatx4 acc4[TR * NC / 4];
+  __shared__ floatx4 wbuf[2][BF4];
+  __shared__ unsigned long long need[2];
+  __shared__ int gfirst[128];
+  __shared__ int gcount[128];
+  __shared__ uint8_t olist[128];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  // logical block = (tile, channel slice, split): the splits of a tile are
+  // adjacent (one XCD).  With n_split > 1 split sp takes the sp-th share of
+  // the tile's offsets and writes its partial sums to out + sp*n_rows*c_out
+  // (summed in split order by split_reduce_kernel).
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int sp = (int)(lb % n_split);
+  const int64_t rest = lb / n_split;
+  const int64_t tile = rest / n_y;
+  const int c0 = (int)(rest % n_y) * NC;
+  float* dst = out + (int64_t)sp * n_rows * c_out;
+  float* acc_s = reinterpret_cast<float*>(acc4);
+  for (int i = tid; i < TR * NC / 4; i += kThreads) acc4[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (tid < 128) gcount[tid] = 0;
+  if (tid < 2) need[tid] = 0ull;
+  __syncthreads();
+  const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
+  for (int64_t c = cb + tid; c < ce; c += kThreads) {
+    const int o = chunk_off[c];
+    if (c == cb || chunk_off[c - 1] != o) {  // chunks are sorted by offset
+      gfirst[o] = (int)(c - cb);
+      atomicOr(&need[o >> 6], 1ull << (o & 63));
+    }
+    atomicAdd(&gcount[o], 1);
+  }
+  __syncthreads();
+  if (tid < 128) {  // olist[i] = i-th needed offset (ascending)
+    const unsigned long long m0 = need[0], m1 = need[1];
+    const bool has = tid < 64 ? ((m0 >> tid) & 1ull) : ((m1 >> (tid - 64)) & 1ull);
+    const int below = tid < 64 ? __popcll(m0 & ((1ull << tid) - 1ull))
+                               : __popcll(m0) + __popcll(m1 & ((1ull << (tid - 64)) - 1ull));
+    if (has) olist[below] = (uint8_t)tid;
+  }
+  // (readfirstlane returns int: go through unsigned so bit 31 does not sign-extend)
+  auto uniform64 = [](unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+  };
+  const int n_off_all = __popcll(uniform64(need[0])) + __popcll(uniform64(need[1]));
+  const int oi0 = sp * n_off_all / n_split;
+  const int n_off = (sp + 1) * n_off_all / n_split - oi0;
+  __syncthreads();
+  const int nks = (c_in + 63) >> 6;
+  const int n_steps = n_off * nks;
+  if (n_steps == 0) {
+    // no rules: the tile's rows are zero
+    const int64_t row0 = tile * TR;
+    const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
+    for (int i = tid; i < nr * NC / 4; i += kThreads)
+      *reinterpret_cast<floatx4*>(dst + (row0 + i / (NC / 4)) * c_out + c0 + 4 * (i % (NC / 4))) =
+          floatx4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+
+  // Step descriptor, all scalar: offset index oi into olist, k-slice ks,
+  // offset o, first chunk l0, chunk count cnt and this wave's chunk count gn.
+  // Built incrementally (one LDS read per step); past the last step it
+  // repeats the last one so its loads stay in range.
+  struct Step {
+    int oi, ks, o, l0, cnt, gn;
+  };
+  auto fill = [&](Step& d) {
+    const bool live = d.oi < n_off;
+    const int oc = live ? d.oi : n_off - 1;
+    d.o = __builtin_amdgcn_readfirstlane(olist[oi0 + oc]);
+    d.cnt = __builtin_amdgcn_readfirstlane(gcount[d.o]);
+    d.l0 = __builtin_amdgcn_readfirstlane(gfirst[d.o]);
+    const int gn = (d.cnt - wave + kWaves - 1) / kWaves;
+    d.gn = !live || gn < 0 ? 0 : (gn > MJ ? MJ : gn);  // steps past the end do nothing
+  };
+  auto advance = [&](const Step& d) {
+    Step e;
+    e.ks = d.ks + 1;
+    e.oi = d.oi;
+    if (e.ks == nks) {
+      e.ks = 0;
+      e.oi = d.oi + 1;
+    }
+    fill(e);
+    return e;
+  };
+  // chunk slot j of this wave; slots past the offset's chunks read its first chunk
+  auto chunk_elem = [&](const Step& d, int j) {
+    const int l = wave + kWaves * j;
+    return (cb + d.l0 + (l < d.cnt ? l : 0)) * MSP_CHUNK + r;
+  };
+  struct Src {
+    int32_t v[MJ];
+  };
+  struct Row {
+    int v[MJ];
+  };
+  struct Val {
+    floatx4 a[MJ][4];
+  };
+  floatx4 stage[SPT];
+  auto ld_src = [&](const Step& sd, Src& d) {
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) d.v[j] = chunk_src[chunk_elem(sd, j)];
+  };
+  auto ld_row = [&](const Step& sd, Row& d) {
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) d.v[j] = chunk_row[chunk_elem(sd, j)];
+  };
+  auto ld_w = [&](const Step& sd) {
+    const int ow = flip ? (K - 1 - sd.o) : sd.o;
+    const float* wo = wt + ((int64_t)ow * c_out + c0) * c_in;
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) {
+      const int f = (tid + kThreads * i) < BF4 ? tid + kThreads * i : BF4 - 1;
+      const int kq = f & 15, n = f >> 4;
+      const int k = min(sd.ks * 64 + kq * 4, c_in - 4);
+      stage[i] = *reinterpret_cast<const floatx4*>(wo + n * c_in + k);
+    }
+  };
+  auto st_w = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) {
+      const int f = tid + kThreads * i;
+      if (f < BF4) wbuf[buf][(f & 15) * NC + ((f >> 4) ^ (f & 15))] = stage[i];
+    }
+  };
+  // 32-bit byte offsets from the uniform base (x < 4 GiB): saddr + voffset loads
+  const char* xb = reinterpret_cast<const char*>(x);
+  const uint32_t row_bytes = (uint32_t)c_in * 4u;
+  auto gather = [&](const Step& sd, const Src& sv, Val& v) {
+    const int kb = sd.ks * 64;
+    const bool full = kb + 64 <= c_in;  // uniform
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const uint32_t ro = (uint32_t)sv.v[j] * row_bytes + 16u * q;
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) {
+        const int k = full ? kb + kc * 16 : min(kb + kc * 16, c_in - 16);
+        if (ABL & 2)
+          v.a[j][kc] = floatx4{(float)sv.v[j], (float)kc, 1.f, 2.f};
+        else
+          v.a[j][kc] = *reinterpret_cast<const floatx4*>(xb + (ro + 4u * (uint32_t)k));
+      }
+    }
+  };
+  floatx4 acc[MJ][NT];
+  auto mma = [&](const Step& sd, int buf, const Val& v) {
+    if (sd.ks == 0) {
+#pragma unroll
+      for (int j = 0; j < MJ; ++j)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[j][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int kcs = min(4, (c_in - sd.ks * 64) >> 4);
+    const floatx4* wb = wbuf[buf];
+    auto ld_b = [&](int kc, floatx4 (&b)[NT]) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[t] = wb[(kc * 4 + q) * NC + ((t * 16 + r) ^ (kc * 4 + q))];
+    };
+    auto mm = [&](int kc, const floatx4 (&b)[NT]) {
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        if (j < sd.gn) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[j][t] = mfma4(b[t][s], v.a[j][kc][s], acc[j][t]);
+        }
+      }
+    };
+    {
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) {
+        if (kc < kcs) {
+          floatx4 b[NT];
+          ld_b(kc, b);
+          mm(kc, b);
+        }
+      }
+    }
+  };
+  // Mark loaded registers as read on every path (slots a step skipped by a
+  // uniform branch included), so the compiler never finds a load into them
+  // still in flight when it reuses them later and does not insert a wait for
+  // every younger load there.  Placed where these loads are complete anyway.
+  auto consume_val = [&](const Val& v) {
+#pragma unroll
+    for (int j = 0; j < MJ; ++j)
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) asm volatile("" ::"v"(v.a[j][kc]));
+  };
+  auto consume_row = [&](const Row& rw) {
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) asm volatile("" ::"v"(rw.v[j]));
+  };
+  auto rmw = [&](const Step& sd, const Row& rw) {
+    if (sd.ks != nks - 1) return;
+    if (ABL & 4) {  // ablation: no LDS accumulation (sum into one slot)
+#pragma unroll
+      for (int j = 0; j < MJ; ++j)
+        if (j < sd.gn)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc_s[lane] += acc[j][t][0] + acc[j][t][1] + acc[j][t][2] + acc[j][t][3];
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      if (j < sd.gn && rw.v[j] < TR) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(rw.v[j], 4 * t + q)) += acc[j][t];
+      }
+    }
+  };
+
+  Step d0;
+  d0.oi = 0;
+  d0.ks = 0;
+  fill(d0);
+  Step d1 = advance(d0);
+  Src s0, s1;
+  Row r0, r1;
+  Val v0, v1;
+  ld_src(d0, s0);
+  ld_src(d1, s1);
+  ld_w(d0);
+  ld_row(d0, r0);
+  ld_row(d1, r1);
+  gather(d0, s0, v0);
+  st_w(0);
+  // one step: dc = this step, dn = the next one; returns the step after dn
+  auto body = [&](int st, const Step& dc, const Step& dn, Src& s_cur, Src& s_nxt, Row& r_cur, Val& v_cur,
+                  Val& v_nxt) {
+    const Step d2 = advance(dn);
+    if (!(ABL & 1)) __syncthreads();  // wbuf[st & 1] holds this step's slice; all step st-1 LDS updates are done
+    ld_src(d2, s_cur);
+    ld_w(dn);
+    gather(dn, s_nxt, v_nxt);
+    mma(dc, st & 1, v_cur);
+    consume_val(v_cur);
+    rmw(dc, r_cur);
+    consume_row(r_cur);
+    ld_row(d2, r_cur);
+    st_w((st + 1) & 1);
+    return d2;
+  };
+  // even trip count: a step past the end loads in range and computes nothing
+  for (int st = 0; st < n_steps; st += 2) {
+    const Step d2 = body(st, d0, d1, s0, s1, r0, v0, v1);
+    const Step d3 = body(st + 1, d1, d2, s1, s0, r1, v1, v0);
+    d0 = d2;
+    d1 = d3;
+  }
+  __syncthreads();
+  const int64_t row0 = tile * TR;
+  const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
+  constexpr int V4 = NC / 4;
+  for (int i = tid; i < nr * V4; i += kThreads) {
+    const int rr = i / V4, g = i % V4;
+    *reinterpret_cast<floatx4*>(dst + (row0 + rr) * c_out + c0 + 4 * g) =
+        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
+  }
+}
+
+// out[i] = sum over splits sp = 0, 1, ... (in order) of part[sp][i]
+__global__ __launch_bounds__(256) void split_reduce_kernel(const floatx4* __restrict__ part, int n_split, int64_t n4,
+                                                           floatx4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  floatx4 s = part[i];
+  for (int k = 1; k < n_split; ++k) s += part[(int64_t)k * n4 + i];
+  out[i] = s;
 }
 
 // Largest o with starts[o] <= v (starts non-decreasing, starts[0] = 0).
@@ -688,56 +1002,179 @@ using namespace msp;
 
 extern "C" {
 
-int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+namespace {
+
+// Shared-tile plan: NT (16-channel groups per block) and the offset split.
+// NT is the largest of 4, 3, 2 dividing the output groups that still gives
+// >= 2048 blocks, else the smallest of them (more blocks); small grids split
+// each tile's offsets over up to 8 blocks (partials reduced in split order).
+struct Plan7 {
+  int nt, n_y, split;
+};
+
+Plan7 plan7(int64_t n_tiles, int c_out) {
+  const int n16 = c_out / 16;
+  Plan7 p{1, n16, 1};
+  int smallest = 0;
+  for (int nt : {2, 3, 4})
+    if (n16 % nt == 0 && !smallest) smallest = nt;
+  for (int nt : {4, 3, 2}) {
+    if (n16 % nt == 0 && n_tiles * (n16 / nt) >= 2048) {
+      p.nt = nt;
+      break;
+    }
+  }
+  if (p.nt == 1 && smallest) p.nt = smallest;
+  p.n_y = n16 / p.nt;
+  const int64_t blocks = n_tiles * p.n_y;
+  if (blocks < 1024) {
+    const int64_t sp = (1024 + blocks - 1) / blocks;
+    p.split = (int)(sp > 8 ? 8 : sp);
+  }
+  return p;
+}
+
+int launch_tile7(int nt, int tile_rows, int split, const float* x, int c_in, const float* wt, int K, int flip,
+                 int c_out, const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                 const uint16_t* chunk_row, int64_t n_rows, float* out, float* part, hipStream_t s) {
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
+  const int n_y = c_out / (16 * nt);
+  const unsigned grid = (unsigned)(n_tiles * n_y * split);
+  float* dst = split > 1 ? part : out;
+  bool launched = false;
+#define L7(N, T)                                                                                              \
+  if (!launched && nt == N && tile_rows == T) {                                                               \
+    conv_tile7_kernel<N, T><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,     \
+                                                      chunk_src, chunk_row, n_rows, n_y, split, dst);         \
+    launched = true;                                                                                          \
+  }
+  L7(1, 128) L7(2, 128) L7(3, 128) L7(4, 128) L7(2, 256) L7(4, 256)
+#undef L7
+  if (!launched) {
+    set_error("msp_conv_tile: no shared-tile kernel for nt=%d tile_rows=%d", nt, tile_rows);
+    return MSP_EINVAL;
+  }
+  if (split > 1) {
+    const int64_t n4 = n_rows * c_out / 4;
+    split_reduce_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, s>>>(reinterpret_cast<const floatx4*>(part), split,
+                                                                    n4, reinterpret_cast<floatx4*>(out));
+  }
+  return MSP_OK;
+}
+
+}  // namespace
+
+int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out) {
+  (void)n_rows;
+  (void)c_in;
+  // narrow outputs: per-wave 64-row tiles (no barriers); otherwise shared
+  // 128-row tiles
+  return c_out <= 32 ? 64 : 128;
+}
+
+size_t msp_conv_tile_workspace_size(int64_t n_rows, int c_in, int c_out, int tile_rows) {
+  (void)c_in;
+  if (tile_rows != 128 || n_rows <= 0 || c_out <= 0) return 0;
+  const Plan7 p = plan7(ceil_div(n_rows, tile_rows), c_out);
+  return p.split > 1 ? (size_t)p.split * (size_t)n_rows * (size_t)c_out * sizeof(float) : 0;
+}
+
+int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
-                  const uint8_t* chunk_row, int64_t n_rows, float* out, msp_stream_t stream) {
+                  const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                  msp_stream_t stream) {
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_tile: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= 128, "msp_conv_tile: K must be in [1, 128] (got %d)", K);
-  const int64_t n_tiles = ceil_div(n_rows, MSP_TILE_ROWS);
+  MSP_REQUIRE(tile_rows == 64 || tile_rows == 128 || tile_rows == 256,
+              "msp_conv_tile: tile_rows must be 64, 128 or 256 (got %d)", tile_rows);
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
-  const int64_t n_tb = ceil_div(n_tiles, kWaves);
-  const int NT = (c_out / 16) % 2 == 0 ? 2 : 1;
-  const int n_y = c_out / (16 * NT);
-  const unsigned grid = (unsigned)(n_tb * n_y);
-  if (c_in >= 64 && NT == 2) {
-    // block offset-major form: weights staged once per block and offset
-    conv_tile4_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src,
-                                                   chunk_row, n_rows, n_tiles, n_y, out);
-  } else if (c_in <= 64) {
-    // narrow inputs (level 0 of m=32, m=16 nets): pipelined per-wave form, no barriers
+  if (tile_rows == 64) {
+    const int64_t n_tb = ceil_div(n_tiles, kWaves);
+    const int NT = (c_out / 16) % 2 == 0 ? 2 : 1;
+    const int n_y = c_out / (16 * NT);
+    const unsigned grid = (unsigned)(n_tb * n_y);
+    if (c_in >= 64 && NT == 2) {
+      // block offset-major form over 4 per-wave tiles
+      conv_tile4_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
+                                                     chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
+    } else if (c_in <= 64) {
 #define LP(N, C)                                                                                              \
   if (NT == N && c_in == 16 * C)                                                                              \
-    conv_tilep_kernel<N, C><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, \
-                                                      chunk_row, n_rows, n_tiles, n_y, out);
-    LP(1, 1) LP(1, 2) LP(1, 3) LP(1, 4) LP(2, 1) LP(2, 2) LP(2, 3)
+    conv_tilep_kernel<N, C, 64><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off,      \
+                                                          chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
+      LP(1, 1) LP(1, 2) LP(1, 3) LP(1, 4) LP(2, 1) LP(2, 2) LP(2, 3) LP(2, 4)
 #undef LP
-  } else {
-    // wide inputs with an odd number of 16-channel output groups (m=16 nets)
-    conv_tile_kernel<1><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src,
-                                                  chunk_row, n_rows, n_tiles, n_y, out);
+    } else {
+      conv_tile_kernel<1><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
+                                                    chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
+    }
+    return check_launch("msp_conv_tile");
   }
-  return check_launch("msp_conv_tile");
+  if (tile_rows == 256) {
+    MSP_REQUIRE((c_out / 16) % 2 == 0, "msp_conv_tile: 256-row tiles need an even number of 16-channel groups");
+    const int rc = launch_tile7((c_out / 16) % 4 == 0 ? 4 : 2, 256, 1, x, c_in, wt, K, flip, c_out, tile_start,
+                                chunk_off, chunk_src, chunk_row, n_rows, out, nullptr, s);
+    return rc ? rc : check_launch("msp_conv_tile");
+  }
+  const Plan7 p = plan7(n_tiles, c_out);
+  const size_t need = msp_conv_tile_workspace_size(n_rows, c_in, c_out, tile_rows);
+  MSP_REQUIRE(ws_bytes >= need, "msp_conv_tile: workspace too small (%zu < %zu)", ws_bytes, need);
+  const int rc = launch_tile7(p.nt, tile_rows, p.split, x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
+                              chunk_src, chunk_row, n_rows, out, static_cast<float*>(ws), s);
+  return rc ? rc : check_launch("msp_conv_tile");
 }
 
 // Experiment hook (not part of the public ABI; scripts/kbench_conv.py): the
-// two conv_tile forms with parts of their data movement replaced by constants
-// to find the limiter.  abl 0-7: per-wave form (bits: 1 no gathers, 2 no
-// weight loads, 4 no LDS accumulation); abl 16-23: block offset-major form
-// (same bits, + 8: no per-step barrier -- wrong results, timing only); 32:
-// block form with gathers one step ahead; 48: pipelined per-wave form.  nt
-// forces NT.
+// conv_tile forms with parts of their data movement replaced by constants
+// to find the limiter (64-row tiles).  abl 0-7: per-wave form (bits: 1 no
+// gathers, 2 no weight loads, 4 no LDS accumulation); abl 16-23: block
+// offset-major form (same bits, + 8: no per-step barrier -- wrong results,
+// timing only); 32: block form with gathers one step ahead; 48: pipelined
+// per-wave form (any tile_rows <= 128); 80 + s (s = 1..8): shared-tile form
+// with an s-way offset split (ws = s*n_rows*c_out floats); 68-74:
+// shared-tile ablations (bits of abl-67: 1 no barrier, 2 no gathers, 4 no
+// LDS accumulation; tile_rows 128, nt 4).  nt forces NT.
 int msp_debug_conv_tile(int abl, int nt, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
-                        const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
-                        const uint8_t* chunk_row, int64_t n_rows, float* out, msp_stream_t stream) {
-  const int64_t n_tiles = ceil_div(n_rows, MSP_TILE_ROWS);
+                        int tile_rows, const int64_t* tile_start, const uint8_t* chunk_off,
+                        const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows, float* out, float* ws,
+                        msp_stream_t stream) {
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
   const int NT = nt > 0 ? nt : pick_tile(c_out / 16);
   MSP_REQUIRE((c_out / 16) % NT == 0, "bad nt");
   const int n_y = c_out / (16 * NT);
   const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
   hipStream_t s = as_stream(stream);
+  if (abl > 80 && abl <= 88) {
+    const int rc = launch_tile7(NT, tile_rows, abl - 80, x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
+                                chunk_src, chunk_row, n_rows, out, ws, s);
+    return rc ? rc : check_launch("msp_debug_conv_tile");
+  }
+  if (abl >= 68 && abl <= 74 && tile_rows == 128 && NT == 4) {
+    const unsigned g7 = (unsigned)(ceil_div(n_rows, 128) * (c_out / 64));
+#define A7(A)                                                                                                 \
+  if (abl - 67 == A)                                                                                          \
+    conv_tile7_kernel<4, 128, A><<<g7, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,  \
+                                                         chunk_src, chunk_row, n_rows, c_out / 64, 1, out);
+    A7(1) A7(2) A7(3) A7(4) A7(5) A7(6) A7(7)
+#undef A7
+    return check_launch("msp_debug_conv_tile");
+  }
+  if (abl == 48) {
+    const int KC = c_in / 16;
+    MSP_REQUIRE(c_in % 16 == 0 && KC <= 4 && tile_rows <= 128, "tilep: c_in / tile_rows");
+#define LP(N, C, T)                                                                                         \
+  if (NT == N && KC == C && tile_rows == T)                                                                 \
+    conv_tilep_kernel<N, C, T><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off,      \
+                                                         chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
+    LP(1, 2, 64) LP(2, 2, 64) LP(2, 4, 64) LP(1, 2, 128) LP(2, 2, 128) LP(2, 4, 128)
+#undef LP
+    return check_launch("msp_debug_conv_tile");
+  }
+  MSP_REQUIRE(tile_rows == 64, "debug variants %d need 64-row tiles", abl);
 #define L(N, A)                                                                                            \
   if (NT == N && abl == A)                                                                                 \
     conv_tile_kernel<N, A><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,   \
@@ -750,20 +1187,9 @@ int msp_debug_conv_tile(int abl, int nt, const float* x, int c_in, const float* 
                                                       chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
   L4(2, 0) L4(2, 1) L4(2, 2) L4(2, 3) L4(2, 4) L4(2, 7) L4(2, 8) L4(2, 15)
 #undef L4
-  if (abl == 48) {
-    const int KC = c_in / 16;
-#define LP(N, C)                                                                                         \
-  if (NT == N && KC == C)                                                                                \
-    conv_tilep_kernel<N, C><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, \
-                                                      chunk_row, n_rows, n_tiles, n_y, out);
-    MSP_REQUIRE(c_in % 16 == 0 && KC <= 4, "tilep: c_in");
-    LP(1, 1) LP(1, 2) LP(1, 3) LP(1, 4) LP(2, 1) LP(2, 2) LP(2, 3) LP(2, 4)
-#undef LP
-  }
   if (NT == 2 && abl == 32)
     conv_tile4_kernel<2, 0, true><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
                                                             chunk_src, chunk_row, n_rows, n_tiles, n_y, out);
-
 #undef LN
 #undef L
   return check_launch("msp_debug_conv_tile");

@@ -208,59 +208,99 @@ __global__ __launch_bounds__(kThreads) void pair_fill_kernel(const int32_t* __re
 }
 
 // ---------------------------------------------------------------- tile rulebook
-// One wave per 64-row output tile.  For each filter offset the wave ballots
-// which of its rows have that neighbour, and the present rows are compacted
-// (mbcnt prefix) into 16-row chunks that share the offset.
-constexpr int kTile = MSP_TILE_ROWS;
+// Output tiles of TW*64 rows; one wave per 64-row band, TW waves per tile
+// (a block of kThreads holds 4/TW tiles).  For each filter offset every wave
+// ballots which of its rows have that neighbour, the TW wave counts are
+// combined through LDS, and the present rows are compacted (wave prefix +
+// mbcnt) into 16-row chunks that share the offset.
 constexpr int kChunk = MSP_CHUNK;
-static_assert(kTile == 64, "one wave per tile");
 
+template <int TW>
 __global__ __launch_bounds__(kThreads) void tile_count_kernel(const int32_t* __restrict__ map, int K, int64_t n,
-                                                              int64_t n_tiles, int64_t* __restrict__ cnt) {
-  const int64_t t = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (t >= n_tiles) return;
-  const int64_t r = t * kTile + (threadIdx.x & 63);
+                                                              int64_t n_tiles, int64_t* __restrict__ cnt,
+                                                              int64_t* __restrict__ max_cnt) {
+  __shared__ int pc_s[kThreads / 64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = wave % TW;
+  const int64_t t = (int64_t)blockIdx.x * (kThreads / 64 / TW) + wave / TW;
+  const int64_t r = t * (64 * TW) + sub * 64 + lane;
+  const bool live = t < n_tiles && r < n;
   int64_t nch = 0;
   for (int o = 0; o < K; ++o) {
-    const bool p = r < n && map[(int64_t)o * n + r] >= 0;
-    const int pc = __popcll(ballot64(p));
-    nch += (pc + kChunk - 1) / kChunk;
+    const int pc = __popcll(ballot64(live && map[(int64_t)o * n + r] >= 0));
+    int tot = pc;
+    if (TW > 1) {
+      if (lane == 0) pc_s[wave] = pc;
+      __syncthreads();
+      tot = 0;
+#pragma unroll
+      for (int w = 0; w < TW; ++w) tot += pc_s[wave - sub + w];
+      __syncthreads();
+    }
+    nch += (tot + kChunk - 1) / kChunk;
   }
-  if ((threadIdx.x & 63) == 0) cnt[t] = nch;
+  if (sub == 0 && lane == 0 && t < n_tiles) {
+    cnt[t] = nch;
+    atomicMax(reinterpret_cast<unsigned long long*>(max_cnt), (unsigned long long)nch);
+  }
 }
 
+template <int TW>
 __global__ __launch_bounds__(kThreads) void tile_fill_kernel(const int32_t* __restrict__ map, int K, int64_t n,
                                                              int64_t n_tiles,
                                                              const int64_t* __restrict__ tile_start,
                                                              uint8_t* __restrict__ chunk_off,
                                                              int32_t* __restrict__ chunk_src,
-                                                             uint8_t* __restrict__ chunk_row) {
-  const int64_t t = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (t >= n_tiles) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t r = t * kTile + lane;
-  int64_t c = tile_start[t];
+                                                             uint16_t* __restrict__ chunk_row) {
+  constexpr int TR = 64 * TW;
+  __shared__ int pc_s[kThreads / 64];
+  __shared__ int32_t first_s[kThreads / 64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = wave % TW;
+  const int64_t t = (int64_t)blockIdx.x * (kThreads / 64 / TW) + wave / TW;
+  const int slot = sub * 64 + lane;  // row inside the tile
+  const int64_t r = t * TR + slot;
+  const bool live = t < n_tiles && r < n;
+  int64_t c = t < n_tiles ? tile_start[t] : 0;
   for (int o = 0; o < K; ++o) {
-    const int32_t v = (r < n) ? map[(int64_t)o * n + r] : -1;
+    const int32_t v = live ? map[(int64_t)o * n + r] : -1;
     const unsigned long long m = ballot64(v >= 0);
     const int pc = __popcll(m);
-    if (pc == 0) continue;
-    const int nch = (pc + kChunk - 1) / kChunk;
-    // padding slots repeat the offset's first present input row (in bounds and
-    // nearby for the gather); chunk_row = kTile marks them
-    const int32_t vfirst = __shfl(v, __ffsll((long long)m) - 1);
+    // first present input row of this wave (padding slots repeat the tile's
+    // first present row of this offset: in bounds and nearby for the gather)
+    const int32_t vf = m ? __shfl(v, __ffsll((long long)m) - 1) : -1;
+    int before = 0, tot = pc;
+    int32_t vfirst = vf;
+    if (TW > 1) {
+      if (lane == 0) {
+        pc_s[wave] = pc;
+        first_s[wave] = vf;
+      }
+      __syncthreads();
+      tot = 0;
+      vfirst = -1;
+#pragma unroll
+      for (int w = 0; w < TW; ++w) {
+        const int p = pc_s[wave - sub + w];
+        if (w < sub) before += p;
+        tot += p;
+        const int32_t f = first_s[wave - sub + w];
+        if (vfirst < 0) vfirst = f;
+      }
+      __syncthreads();
+    }
+    if (tot == 0) continue;  // uniform over the tile
+    const int nch = (tot + kChunk - 1) / kChunk;
     if (v >= 0) {
-      const int pos = mbcnt64(m);
+      const int pos = before + mbcnt64(m);
       const int64_t e = (c + pos / kChunk) * kChunk + (pos % kChunk);
       chunk_src[e] = v;
-      chunk_row[e] = (uint8_t)lane;
+      chunk_row[e] = (uint16_t)slot;
     }
-    if (lane >= pc && lane < nch * kChunk) {  // padding slots of the last chunk
-      const int64_t e = (c + lane / kChunk) * kChunk + (lane % kChunk);
+    if (t < n_tiles && slot >= tot && slot < nch * kChunk) {  // padding slots of the last chunk
+      const int64_t e = (c + slot / kChunk) * kChunk + (slot % kChunk);
       chunk_src[e] = vfirst;
-      chunk_row[e] = (uint8_t)kTile;
+      chunk_row[e] = (uint16_t)TR;
     }
-    if (lane < nch) chunk_off[c + lane] = (uint8_t)o;
+    if (t < n_tiles && slot < nch) chunk_off[c + slot] = (uint8_t)o;
     c += nch;
   }
 }
@@ -400,26 +440,41 @@ int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32
   return check_launch("msp_pair_lists");
 }
 
-int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int64_t* tile_start, uint8_t* chunk_off,
-                      int32_t* chunk_src, uint8_t* chunk_row, int64_t chunk_cap, void* ws, size_t ws_bytes,
-                      msp_stream_t stream) {
+int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64_t* tile_start,
+                      uint8_t* chunk_off, int32_t* chunk_src, uint16_t* chunk_row, int64_t chunk_cap, void* ws,
+                      size_t ws_bytes, msp_stream_t stream) {
   MSP_REQUIRE(K >= 1 && K <= 255 && n >= 0, "msp_tile_rulebook: K must be in [1,255]");
+  MSP_REQUIRE(tile_rows == 64 || tile_rows == 128 || tile_rows == 256,
+              "msp_tile_rulebook: tile_rows must be 64, 128 or 256 (got %d)", tile_rows);
   hipStream_t s = as_stream(stream);
-  const int64_t n_tiles = ceil_div(n, kTile);
+  const int64_t n_tiles = ceil_div(n, tile_rows);
   const size_t need = (size_t)(n_tiles + 1) * sizeof(int64_t) + scan_ws_bytes(n_tiles);
   MSP_REQUIRE(ws_bytes >= need, "msp_tile_rulebook: workspace too small (%zu < %zu)", ws_bytes, need);
   if (n_tiles == 0) {
-    MSP_HIP(hipMemsetAsync(tile_start, 0, sizeof(int64_t), s), "msp_tile_rulebook");
+    MSP_HIP(hipMemsetAsync(tile_start, 0, 2 * sizeof(int64_t), s), "msp_tile_rulebook");
     return MSP_OK;
   }
   int64_t* cnt = reinterpret_cast<int64_t*>(ws);
   void* sws = cnt + n_tiles + 1;
-  const unsigned g = (unsigned)ceil_div(n_tiles, kThreads / 64);
-  tile_count_kernel<<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt);
+  const int tw = tile_rows / 64;
+  MSP_HIP(hipMemsetAsync(tile_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_tile_rulebook");
+  const unsigned g = (unsigned)ceil_div(n_tiles, kThreads / 64 / tw);
+#define TW_CASE(W)                                                                              \
+  case W:                                                                                       \
+    tile_count_kernel<W><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, tile_start + n_tiles + 1);                      \
+    break;
+  switch (tw) { TW_CASE(1) TW_CASE(2) TW_CASE(4) }
+#undef TW_CASE
   int rc = scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
   if (rc) return rc;
   if (chunk_cap > 0) {
-    tile_fill_kernel<<<g, kThreads, 0, s>>>(map, K, n, n_tiles, tile_start, chunk_off, chunk_src, chunk_row);
+#define TW_CASE(W)                                                                                     \
+  case W:                                                                                              \
+    tile_fill_kernel<W><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, tile_start, chunk_off, chunk_src,  \
+                                               chunk_row);                                            \
+    break;
+    switch (tw) { TW_CASE(1) TW_CASE(2) TW_CASE(4) }
+#undef TW_CASE
   }
   return check_launch("msp_tile_rulebook");
 }

@@ -31,9 +31,11 @@ PROTOTYPES = {
     "msp_subm_map": (I, [P, I64, I, I64, I, P, P, I64, P, P]),
     "msp_down_map": (I, [P, I64, P, I, I, P, I64, P]),
     "msp_pair_lists": (I, [P, I, I64, P, P, I64, P, P, SZ, P]),
-    "msp_tile_rulebook": (I, [P, I, I64, P, P, P, P, I64, P, SZ, P]),
+    "msp_tile_rulebook": (I, [P, I, I64, I, P, P, P, P, I64, P, SZ, P]),
     "msp_decode_keys": (I, [P, I64, I, P, P]),
-    "msp_conv_tile": (I, [P, I, P, I, I, I, P, P, P, P, I64, P, P]),
+    "msp_conv_tile_rows": (I, [I64, I, I]),
+    "msp_conv_tile_workspace_size": (SZ, [I64, I, I, I]),
+    "msp_conv_tile": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_pairs": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
     "msp_wgrad_pieces": (I64, [I64, I]),
     "msp_conv_wgrad": (I, [P, I, P, I, P, P, P, I, I64, P, P, P]),
@@ -86,6 +88,9 @@ def stream(device=None):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_SYNC = os.environ.get("MI3DSPARSE_SYNC") == "1"  # debugging: synchronise after every call
+
+
 def call(name, *args):
     """Invoke an int-returning entry point; raise RuntimeError on failure."""
     lib = load()
@@ -93,6 +98,11 @@ def call(name, *args):
     if rc != 0:
         msg = lib.msp_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
+    if _SYNC:
+        try:
+            torch.cuda.synchronize()
+        except Exception as e:  # name the entry point whose kernels faulted
+            raise RuntimeError(f"{name}: device fault after this call: {e}") from e
 
 
 def query(name, *args):

@@ -26,7 +26,6 @@ import torch
 from . import _lib
 from ._lib import I64, call, ptr, query
 
-TILE_ROWS = 64  # MSP_TILE_ROWS
 CHUNK = 16      # MSP_CHUNK
 
 
@@ -38,22 +37,25 @@ def _log2_ceil(n: int) -> int:
     return max(1, int(math.ceil(math.log2(max(2, int(n))))))
 
 
-def tile_rulebook(m, K, n, device, s):
+def tile_rulebook(m, K, n, device, s, tile_rows=64):
     """Output-tile rulebook of an offset-major map m[K][n] (two passes:
     count, then fill; one host read of the chunk total)."""
-    n_tiles = (n + TILE_ROWS - 1) // TILE_ROWS
-    tile_start = torch.empty(n_tiles + 1, dtype=torch.int64, device=device)
+    tr = int(tile_rows)
+    n_tiles = (n + tr - 1) // tr
+    # tile_start[n_tiles + 1] = largest chunk count of one tile
+    tile_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=device)
     ws = _ws((n_tiles + 1) * 8 + query("msp_scan_workspace_size", I64(n_tiles)), device)
-    call("msp_tile_rulebook", ptr(m), K, n, ptr(tile_start), None, None, None, 0, ptr(ws), ws.numel(), s)
-    n_chunks = int(tile_start[-1].item()) if n_tiles else 0
+    call("msp_tile_rulebook", ptr(m), K, n, tr, ptr(tile_start), None, None, None, 0, ptr(ws), ws.numel(), s)
+    n_chunks, max_chunks = (int(v) for v in tile_start[n_tiles:].tolist())
     chunk_off = torch.empty(max(n_chunks, 1), dtype=torch.uint8, device=device)
     chunk_src = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int32, device=device)
-    chunk_row = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.uint8, device=device)
+    # uint16 row-in-tile; stored in an int16 tensor (same bytes, rows < 2^15)
+    chunk_row = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int16, device=device)
     if n_chunks:
-        call("msp_tile_rulebook", ptr(m), K, n, ptr(tile_start), ptr(chunk_off), ptr(chunk_src), ptr(chunk_row),
+        call("msp_tile_rulebook", ptr(m), K, n, tr, ptr(tile_start), ptr(chunk_off), ptr(chunk_src), ptr(chunk_row),
              n_chunks, ptr(ws), ws.numel(), s)
     return dict(tile_start=tile_start, chunk_off=chunk_off, chunk_src=chunk_src, chunk_row=chunk_row,
-                n_chunks=n_chunks)
+                n_chunks=n_chunks, tile_rows=tr, max_chunks=max_chunks)
 
 
 class PairLists:
@@ -94,9 +96,18 @@ class SubmRules:
         if V:
             call("msp_subm_map", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(tkeys), ptr(tvals),
                  cap, ptr(self.nbr), s)
-        self.tiles = tile_rulebook(self.nbr, K, V, dev, s)
+        self._tiles = {}
+        self._map, self._n = self.nbr, V
         self.pairs = PairLists(self.nbr, K, V, dev, s)
         self.n_rules = self.pairs.total  # = SCN rulebook size (centre included)
+
+    def tiles_for(self, tile_rows):
+        """Tile rulebook with tile_rows-row tiles, built on first use."""
+        t = self._tiles.get(tile_rows)
+        if t is None:
+            t = self._tiles[tile_rows] = tile_rulebook(self._map, self.K, self._n, self._map.device,
+                                                       _lib.stream(self._map.device), tile_rows)
+        return t
 
 
 class DownRules:
@@ -111,9 +122,12 @@ class DownRules:
         self.down = torch.empty((K, max(coarse.n, 1)), dtype=torch.int32, device=dev)
         call("msp_down_map", ptr(fine.keys), fine.n, ptr(parent_of), fine.log2, log2_stride, ptr(self.down),
              coarse.n, s)
-        self.tiles = tile_rulebook(self.down, K, coarse.n, dev, s)
+        self._tiles = {}
+        self._map, self._n = self.down, coarse.n
         # pair_in = fine row, pair_out = coarse row, grouped by child offset
         self.pairs = PairLists(self.down, K, coarse.n, dev, s)
+
+    tiles_for = SubmRules.tiles_for
 
 
 class Level:

@@ -53,13 +53,21 @@ def _record(kind, flops, fn):
 
 
 # ------------------------------------------------------------------ convolution helpers
-def conv_tile(x, wt, K, flip, c_out, tiles, n_rows, kind="conv_tile", flops=0):
+def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
+    """Output-stationary convolution over the rulebook's tile form; the tile
+    height (and so which rulebook) is the library's choice for these channel
+    counts (msp_conv_tile_rows)."""
+    c_in = x.size(1)
+    tr = int(_lib.query("msp_conv_tile_rows", _lib.I64(n_rows), c_in, c_out))
+    tiles = rules.tiles_for(tr)
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
     if n_rows:
+        wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(n_rows), c_in, c_out, tr))
+        ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
         _record(kind, flops, lambda: call(
-            "msp_conv_tile", ptr(x), x.size(1), ptr(wt), K, int(flip), c_out, ptr(tiles["tile_start"]),
+            "msp_conv_tile", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tr, ptr(tiles["tile_start"]),
             ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), n_rows, ptr(out),
-            _stream(x)))
+            ptr(ws), wsb, _stream(x)))
     return out[:n_rows]
 
 
@@ -94,7 +102,7 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
         wt = wp.transpose(1, 2).contiguous()  # [K][cout][cin]
         V = x.size(0)
-        out = conv_tile(xp, wt, K, 0, cout_p, rules.tiles, V, "subm_fwd",
+        out = conv_tile(xp, wt, K, 0, cout_p, rules, V, "subm_fwd",
                         2.0 * rules.n_rules * cin * cout)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims = rules, (cin, cout)
@@ -108,7 +116,7 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         g = _pad_cols(gout.contiguous(), cout_p)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dxp = conv_tile(g, wp, K, 1, cin_p, rules.tiles, xp.size(0), "subm_bwd_data",
+            dxp = conv_tile(g, wp, K, 1, cin_p, rules, xp.size(0), "subm_bwd_data",
                             2.0 * rules.n_rules * cin * cout)
             dx = dxp if cin_p == cin else dxp[:, :cin]
         if ctx.needs_input_grad[1]:
@@ -130,7 +138,7 @@ class ConvolutionFunction(torch.autograd.Function):
         xp = _pad_cols(x.contiguous(), cin_p)
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
         wt = wp.transpose(1, 2).contiguous()
-        out = conv_tile(xp, wt, K, 0, cout_p, rules.tiles, n_coarse, "conv_fwd", 2.0 * x.size(0) * cin * cout)
+        out = conv_tile(xp, wt, K, 0, cout_p, rules, n_coarse, "conv_fwd", 2.0 * x.size(0) * cin * cout)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims = rules, (cin, cout)
         return out if cout_p == cout else out[:, :cout].contiguous()
@@ -179,7 +187,7 @@ class DeconvolutionFunction(torch.autograd.Function):
         p = rules.pairs
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dxp = conv_tile(g, wp, K, 0, cin_p, rules.tiles, xp.size(0), "deconv_bwd_data",
+            dxp = conv_tile(g, wp, K, 0, cin_p, rules, xp.size(0), "deconv_bwd_data",
                             2.0 * g.size(0) * cin * cout)
             dx = dxp if cin_p == cin else dxp[:, :cin]
         if ctx.needs_input_grad[1]:

@@ -42,7 +42,7 @@ typedef void* msp_stream_t; /* hipStream_t */
 #define MSP_EHIP (-2)
 #define MSP_ENOSPACE (-3)
 
-#define MSP_TILE_ROWS 64 /* output rows per wave tile in msp_conv_tile       */
+#define MSP_TILE_ROWS 64 /* rows of a per-wave tile (tile_rows = 64)         */
 #define MSP_CHUNK 16     /* rows per MFMA chunk in rulebooks                  */
 
 int msp_abi_version(void);
@@ -93,30 +93,42 @@ int msp_down_map(const uint64_t* fine_keys, int64_t n_fine, const int32_t* paren
 int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32_t* pair_out, int64_t cap,
                    int64_t* off_start, void* ws, size_t ws_bytes, msp_stream_t stream);
 /* Output-tile rulebook for msp_conv_tile: rows are cut into tiles of
- * MSP_TILE_ROWS; inside a tile the present (row, offset) pairs of each offset
- * are compacted (wavefront ballot + prefix sum) into chunks of MSP_CHUNK.
- * tile_start[n_tiles+1] (device int64), chunk_off[c] = offset, chunk_src[c*16+j]
+ * tile_rows (64, 128 or 256); inside a tile the present (row, offset) pairs of
+ * each offset are compacted (wavefront ballot + prefix sum across the tile's
+ * waves) into chunks of MSP_CHUNK, chunks sorted by offset.
+ * tile_start[n_tiles+2] (device int64; tile_start[n_tiles+1] = the largest
+ * chunk count of one tile), chunk_off[c] = offset, chunk_src[c*16+j]
  * = input row, chunk_row[c*16+j] = row inside the tile.  Padding slots of a
- * chunk have chunk_row = 64 and repeat a present input row of the same tile
- * and offset (so every gather stays in bounds).
+ * chunk have chunk_row = tile_rows and repeat a present input row of the same
+ * tile and offset (so every gather stays in bounds).
  * Count-then-fill like msp_pair_lists (total chunks = tile_start[n_tiles]). */
-int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int64_t* tile_start, uint8_t* chunk_off,
-                      int32_t* chunk_src, uint8_t* chunk_row, int64_t chunk_cap, void* ws, size_t ws_bytes,
-                      msp_stream_t stream);
+int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64_t* tile_start,
+                      uint8_t* chunk_off, int32_t* chunk_src, uint16_t* chunk_row, int64_t chunk_cap, void* ws,
+                      size_t ws_bytes, msp_stream_t stream);
 /* Decode keys back to (x, y, z, batch) int64 rows (SparseToDense, locations). */
 int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coords, msp_stream_t stream);
 
 /* ---------------- sparse convolution (replaces SCN SubmanifoldConvolution /
  * Convolution / Deconvolution updateOutput + backward) */
 
-/* Output-stationary gather-MFMA convolution over a tile rulebook:
+/* Output-stationary gather-MFMA convolution over a tile rulebook built with
+ * the same tile_rows:
  *   out[r, :] = sum over chunks of r's tile: sum_j W'[o]^T x[src_j, :]
  * wt is [K][c_out][c_in] (k contiguous).  If flip, offset o reads
  * wt[K-1-o] (submanifold backward-data with the forward weight layout).
- * c_in % 16 == 0, c_out % 16 == 0.  Every output row is written. */
-int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+ * c_in % 16 == 0, c_out % 16 == 0.  Every output row is written.
+ * tile_rows 64: per-wave tiles; 128 / 256: one tile shared by the 4 waves of
+ * a block; with 128-row tiles small grids split each tile's offsets over
+ * several blocks, whose partial sums go to the workspace (ws_bytes >=
+ * msp_conv_tile_workspace_size(n_rows, c_in, c_out, tile_rows)) and are
+ * added in a fixed order.  msp_conv_tile_rows gives the tile height the
+ * library is tuned for. */
+int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out);
+size_t msp_conv_tile_workspace_size(int64_t n_rows, int c_in, int c_out, int tile_rows);
+int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
-                  const uint8_t* chunk_row, int64_t n_rows, float* out, msp_stream_t stream);
+                  const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                  msp_stream_t stream);
 /* One contribution per output row (deconvolution forward, strided
  * convolution backward-data): out[pair_out[p]] = W'[o]^T x[pair_in[p]] for the
  * pairs of offset o.  chunk_start[K+1] (device) = prefix sums of

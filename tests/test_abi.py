@@ -40,17 +40,27 @@ def test_prototypes_match_header():
 
 def test_queries_and_validation_without_gpu():
     lib = _lib.load()
-    assert lib.msp_abi_version() == 1
+    assert lib.msp_abi_version() == 2
     assert _lib.query("msp_hash_capacity", 1000) == 2048
     assert _lib.query("msp_hash_capacity", 10) == 1024
     assert _lib.query("msp_scan_workspace_size", 5000) > 0
     assert _lib.query("msp_bn_partials", 10 ** 7, 32) == 1024
+    assert _lib.query("msp_conv_tile_rows", 10 ** 6, 32, 32) == 64
+    assert _lib.query("msp_conv_tile_rows", 10 ** 6, 64, 64) == 128
+    assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 64, 64, 128) == 0  # big grid: no offset split
+    assert _lib.query("msp_conv_tile_workspace_size", 2000, 192, 192, 128) > 0  # small grid: split partials
     # invalid arguments are rejected before any HIP call
-    rc = lib.msp_conv_tile(None, 3, None, 27, 0, 16, None, None, None, None, 100, None, None)
+    rc = lib.msp_conv_tile(None, 3, None, 27, 0, 16, 64, None, None, None, None, 100, None, None, 0, None)
+    assert rc == -1 and b"multiples of 16" in lib.msp_last_error()
+    rc = lib.msp_conv_tile(None, 16, None, 27, 0, 16, 96, None, None, None, None, 100, None, None, 0, None)
+    assert rc == -1 and b"tile_rows" in lib.msp_last_error()
+    rc = lib.msp_conv_tile(None, 3, None, 27, 0, 16, 64, None, None, None, None, 100, None, None, 0, None)
     assert rc == -1 and b"multiples of 16" in lib.msp_last_error()
     rc = lib.msp_subm_map(None, 10, 12, 4096, 4, None, None, 1024, None, None)
     assert rc == -1 and b"odd" in lib.msp_last_error()
     rc = lib.msp_down_map(None, 10, None, 12, 3, None, 5, None)
     assert rc == -1
     with pytest.raises(RuntimeError, match="msp_tile_rulebook"):
-        _lib.call("msp_tile_rulebook", None, 300, 10, None, None, None, None, 0, None, 0, None)
+        _lib.call("msp_tile_rulebook", None, 300, 10, 64, None, None, None, None, 0, None, 0, None)
+    with pytest.raises(RuntimeError, match="tile_rows"):
+        _lib.call("msp_tile_rulebook", None, 27, 10, 32, None, None, None, None, 0, None, 0, None)
