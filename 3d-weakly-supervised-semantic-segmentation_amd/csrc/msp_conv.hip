@@ -976,17 +976,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WA * W
   }
 }
 
-// dw[o][e] = sum over pieces j (in order) of slab[j][o][e]
+// dw[o][e] = sum over pieces j of slab[j][o][e]: block = 64 elements x 4
+// contiguous piece segments; the segment sums are added in segment order
+// (fixed order, deterministic).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int64_t n_pieces,
                                                            int K, int64_t cc, float* __restrict__ dw) {
+  __shared__ float part[4][64];
   const int o = blockIdx.y;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= cc) return;
-  const float* p = slab + (int64_t)o * cc + e;
-  const int64_t stride = (int64_t)K * cc;
+  const int el = threadIdx.x & 63, seg = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + el;
+  const int64_t j0 = n_pieces * seg / 4, j1 = n_pieces * (seg + 1) / 4;
   float s = 0.f;
-  for (int64_t j = 0; j < n_pieces; ++j) s += p[j * stride];
-  dw[(int64_t)o * cc + e] = s;
+  if (e < cc) {
+    const float* p = slab + (int64_t)o * cc + e;
+    const int64_t stride = (int64_t)K * cc;
+    for (int64_t j = j0; j < j1; ++j) s += p[j * stride];
+  }
+  part[seg][el] = s;
+  __syncthreads();
+  if (seg == 0 && e < cc) dw[(int64_t)o * cc + e] = ((part[0][el] + part[1][el]) + part[2][el]) + part[3][el];
 }
 
 inline int pick_tile(int n16) {
@@ -1067,14 +1075,14 @@ int launch_tile7(int nt, int tile_rows, int split, const float* x, int c_in, con
 int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out) {
   (void)n_rows;
   (void)c_in;
-  // narrow outputs: per-wave 64-row tiles (no barriers); otherwise shared
-  // 128-row tiles
-  return c_out <= 32 ? 64 : 128;
+  (void)c_out;
+  // 128-row tiles everywhere: per-wave pipelined tiles for narrow outputs,
+  // shared tiles (with the offset split on small grids) otherwise
+  return 128;
 }
 
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int c_in, int c_out, int tile_rows) {
-  (void)c_in;
-  if (tile_rows != 128 || n_rows <= 0 || c_out <= 0) return 0;
+  if (tile_rows != 128 || n_rows <= 0 || c_out <= 0 || (c_out <= 32 && c_in <= 64)) return 0;
   const Plan7 p = plan7(ceil_div(n_rows, tile_rows), c_out);
   return p.split > 1 ? (size_t)p.split * (size_t)n_rows * (size_t)c_out * sizeof(float) : 0;
 }
@@ -1118,6 +1126,18 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
     const int rc = launch_tile7((c_out / 16) % 4 == 0 ? 4 : 2, 256, 1, x, c_in, wt, K, flip, c_out, tile_start,
                                 chunk_off, chunk_src, chunk_row, n_rows, out, nullptr, s);
     return rc ? rc : check_launch("msp_conv_tile");
+  }
+  if (c_out <= 32 && c_in <= 64) {
+    // narrow outputs: pipelined per-wave form, one 128-row tile per wave, no barriers
+    const int NT = c_out / 16;
+    const unsigned grid = (unsigned)ceil_div(n_tiles, kWaves);
+#define LP(N, C)                                                                                              \
+  if (NT == N && c_in == 16 * C)                                                                              \
+    conv_tilep_kernel<N, C, 128><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off,     \
+                                                           chunk_src, chunk_row, n_rows, n_tiles, 1, out);
+    LP(1, 1) LP(1, 2) LP(1, 3) LP(1, 4) LP(2, 1) LP(2, 2) LP(2, 3) LP(2, 4)
+#undef LP
+    return check_launch("msp_conv_tile");
   }
   const Plan7 p = plan7(n_tiles, c_out);
   const size_t need = msp_conv_tile_workspace_size(n_rows, c_in, c_out, tile_rows);
@@ -1218,7 +1238,9 @@ int64_t msp_wgrad_pieces(int64_t total_pairs, int K) {
   // about 512 pairs per piece and at most ~3072 pieces x offsets per launch
   if (K < 1) return 1;
   int64_t n = total_pairs / ((int64_t)K * 512);
-  const int64_t cap = 3072 / K > 1 ? 3072 / K : 1;
+  // one-offset contractions (network-in-network weight gradients) get longer
+  // pieces: fewer partial tiles to reduce
+  const int64_t cap = K == 1 ? 768 : (3072 / K > 1 ? 3072 / K : 1);
   if (n > cap) n = cap;
   return n < 1 ? 1 : n;
 }
@@ -1245,7 +1267,7 @@ int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const i
 #undef LAUNCH_ROW
 #undef LAUNCH
   const int64_t cc = (int64_t)c_in * c_out;
-  dim3 g2((unsigned)ceil_div(cc, 256), (unsigned)K);
+  dim3 g2((unsigned)ceil_div(cc, 64), (unsigned)K);
   wgrad_reduce_kernel<<<g2, 256, 0, s>>>(slab, n_pieces, K, cc, dw);
   return check_launch("msp_conv_wgrad");
 }

@@ -165,7 +165,8 @@ class Deconvolution(_ConvBase):
 
 
 class NetworkInNetwork(nn.Module):
-    """Per-site dense linear map (a plain GEMM, rocBLAS/hipBLASLt via torch)."""
+    """Per-site dense linear map: GEMMs on hipBLASLt via torch, weight gradient
+    on msp_conv_wgrad (ops.NetworkInNetworkFunction)."""
 
     def __init__(self, nIn, nOut, bias=False):
         super().__init__()
@@ -174,8 +175,7 @@ class NetworkInNetwork(nn.Module):
         self.bias = nn.Parameter(torch.zeros(nOut)) if bias else None
 
     def forward(self, input):
-        ops._check_feats(input.features)
-        f = input.features @ self.weight
+        f = ops.NetworkInNetworkFunction.apply(input.features, self.weight)
         if self.bias is not None:
             f = f + self.bias
         _count(input.features.size(0) * self.nIn * self.nOut, f)

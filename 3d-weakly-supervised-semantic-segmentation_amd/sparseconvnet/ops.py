@@ -195,6 +195,44 @@ class DeconvolutionFunction(torch.autograd.Function):
         return dx, dw, None, None
 
 
+# ------------------------------------------------------------------ network-in-network
+class _IdentityPairs:
+    """Pair lists of the per-site linear map: row i -> row i (one 'offset')."""
+
+    def __init__(self, n, device):
+        self.total = int(n)
+        self.off_start = torch.tensor([0, n], dtype=torch.int64, device=device)
+        self.pair = torch.arange(max(n, 1), dtype=torch.int32, device=device)
+
+
+class NetworkInNetworkFunction(torch.autograd.Function):
+    """out = x W (§8(a) a11).  Forward and backward-data are dense GEMMs on
+    hipBLASLt through torch; the weight gradient x^T dy (contraction over all
+    V rows, where the library GEMMs pick skinny split-free tiles) runs on
+    msp_conv_wgrad as a one-offset convolution with identity pairs."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        _check_feats(x)
+        x = x.contiguous()
+        ctx.save_for_backward(x, weight)
+        return x @ weight
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, weight = ctx.saved_tensors
+        g = gout.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = g @ weight.t()
+        if ctx.needs_input_grad[1]:
+            cin, cout = weight.shape
+            cin_p, cout_p = _pad16(cin), _pad16(cout)
+            p = _IdentityPairs(x.size(0), x.device)
+            dw = conv_wgrad(_pad_cols(x, cin_p), _pad_cols(g, cout_p), p, p.pair, p.pair, 1)[0, :cin, :cout]
+        return dx, dw
+
+
 # ------------------------------------------------------------------ batch norm
 class BatchNormFunction(torch.autograd.Function):
     """BatchNormalization + (leaky) ReLU; stats[5][C] as in include/mi3dsparse.h."""

@@ -45,7 +45,7 @@ def test_queries_and_validation_without_gpu():
     assert _lib.query("msp_hash_capacity", 10) == 1024
     assert _lib.query("msp_scan_workspace_size", 5000) > 0
     assert _lib.query("msp_bn_partials", 10 ** 7, 32) == 1024
-    assert _lib.query("msp_conv_tile_rows", 10 ** 6, 32, 32) == 64
+    assert _lib.query("msp_conv_tile_rows", 10 ** 6, 32, 32) == 128
     assert _lib.query("msp_conv_tile_rows", 10 ** 6, 64, 64) == 128
     assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 64, 64, 128) == 0  # big grid: no offset split
     assert _lib.query("msp_conv_tile_workspace_size", 2000, 192, 192, 128) > 0  # small grid: split partials

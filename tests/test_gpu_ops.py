@@ -196,6 +196,26 @@ def test_nin_join_add():
     torch.testing.assert_close(a.features, 2 * y.features)
 
 
+@pytest.mark.parametrize("n,cin,cout", [(5000, 64, 32), (3001, 40, 24), (70000, 96, 48)])
+def test_nin_grads(n, cin, cout):
+    """NetworkInNetwork backward: dx on hipBLASLt, dW on msp_conv_wgrad with
+    identity pairs (any channel counts: padded to 16), against fp64 torch."""
+    torch.manual_seed(n)
+    coords, feats = _inputs(n, 30, n_feat=cin)
+    g, _ = _pair(coords, feats)
+    nin = scn.NetworkInNetwork(cin, cout, False).to(DEV)
+    x = g.features.detach().requires_grad_(True)
+    g.features = x
+    y = nin(g).features
+    w = torch.randn(cout, device=DEV)
+    (y * w).square().sum().backward()
+    xd, wd = x.detach().double(), nin.weight.detach().double()
+    yd = xd @ wd
+    gy = 2 * yd * w.double().square()
+    close(x.grad, gy @ wd.t(), 1e-5, "nin dx")
+    close(nin.weight.grad, xd.t() @ gy, 1e-5, "nin dW")
+
+
 def test_empty_and_single_point():
     c = torch.tensor([[5, 6, 7, 0]])
     f = torch.randn(1, 3)
