@@ -43,13 +43,14 @@ def _pad_weight(w, cin_p, cout_p):
     return F.pad(w, (0, cout_p - cout, 0, cin_p - cin))
 
 
-def _record(kind, flops, fn):
+def _record(kind, flops, fn, nbytes=0):
     """Run fn(); when bench.py installed a recorder, bracket it with HIP
-    events on the current stream and account its algorithmic FLOPs."""
+    events on the current stream and account its algorithmic FLOPs and
+    compulsory bytes."""
     rec = _lib.recorder()
     if rec is None:
         return fn()
-    return rec.run(kind, flops, fn)
+    return rec.run(kind, flops, fn, nbytes)
 
 
 # ------------------------------------------------------------------ convolution helpers
@@ -64,10 +65,14 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     if n_rows:
         wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(n_rows), c_in, c_out, tr))
         ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
+        # compulsory bytes: input rows, output rows, weights, rulebook (chunk
+        # offsets, 16 x (int32 src + uint16 row) per chunk, tile starts)
+        nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
+            tiles["n_chunks"] * (1 + 16 * 6) + 8 * (tiles["tile_start"].numel())
         _record(kind, flops, lambda: call(
             "msp_conv_tile", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tr, ptr(tiles["tile_start"]),
             ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), n_rows, ptr(out),
-            ptr(ws), wsb, _stream(x)))
+            ptr(ws), wsb, _stream(x)), nbytes)
     return out[:n_rows]
 
 

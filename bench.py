@@ -44,7 +44,7 @@ class KernelRecorder:
         self.events = []
         self.active = False
 
-    def run(self, kind, flops, fn):
+    def run(self, kind, flops, fn, nbytes=0):
         if not self.active:
             return fn()
         s = torch.cuda.Event(enable_timing=True)
@@ -52,23 +52,35 @@ class KernelRecorder:
         s.record()
         r = fn()
         e.record()
-        self.events.append((kind, flops, s, e))
+        self.events.append((kind, flops, nbytes, s, e))
         return r
 
     def summary(self):
         torch.cuda.synchronize()
-        tot_f, tot_ms, n = 0.0, 0.0, 0
+        tot_f, tot_b, tot_ms, n = 0.0, 0.0, 0.0, 0
         per = {}
-        for kind, f, s, e in self.events:
+        for kind, f, nb, s, e in self.events:
             ms = s.elapsed_time(e)
             tot_f += f
+            tot_b += nb
             tot_ms += ms
             n += 1
             k = per.setdefault(kind, [0, 0.0, 0.0])
             k[0] += 1
             k[1] += f
             k[2] += ms
-        return tot_f, tot_ms, n, per
+        return tot_f, tot_b, tot_ms, n, per
+
+
+def pmc_traffic():
+    """HBM bytes per msp_conv_tile call measured with rocprofv3 PMC counters on
+    this workload (scripts/pmc_traffic.sh; committed under profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    if not os.path.isfile(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_call"), os.path.relpath(path, ROOT)
 
 
 def level_stats(meta):
@@ -178,7 +190,7 @@ def main():
     vox = sum(batches[i % len(batches)][2] for i in range(args.steps))
     dt_max, vox_all = dp.max_over_ranks(dt), dp.sum_over_ranks(float(vox))
 
-    flops, kms, nlaunch, per = rec.summary()
+    flops, abytes, kms, nlaunch, per = rec.summary()
     _lib.set_recorder(None)
 
     # one untimed forward for the per-level statistics and the MAC counter
@@ -196,6 +208,7 @@ def main():
 
     if rank == 0:
         achieved = flops / (kms * 1e-3) / 1e12 if kms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic()
         res = {
             "metric": "active-voxels/sec fwd+bwd, SparseConvUNet m=32 2cm voxels",
             "value": vox_all / dt_max,
@@ -228,7 +241,11 @@ def main():
                 "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per msp_conv_tile call (PMC 2*FETCH_SIZE + WRITE_SIZE)",
+                "traffic_source": traffic_src,
+                "alg_bytes_per_call": abytes / max(nlaunch, 1),
+                "alg_bytes_gbs": abytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0,
                 "launches": nlaunch,
                 "avg_launch_us": kms / max(nlaunch, 1) * 1e3,
                 "per_kind": {k: {"launches": v[0], "tflops": v[1] / (v[2] * 1e-3) / 1e12 if v[2] else 0.0,
