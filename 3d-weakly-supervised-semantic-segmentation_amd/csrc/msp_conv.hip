@@ -1234,14 +1234,17 @@ int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, 
   return check_launch("msp_conv_pairs");
 }
 
-int64_t msp_wgrad_pieces(int64_t total_pairs, int K) {
-  // about 512 pairs per piece and at most ~3072 pieces x offsets per launch
-  if (K < 1) return 1;
-  int64_t n = total_pairs / ((int64_t)K * 512);
-  // one-offset contractions (network-in-network weight gradients) get longer
-  // pieces: fewer partial tiles to reduce
-  const int64_t cap = K == 1 ? 768 : (3072 / K > 1 ? 3072 / K : 1);
-  if (n > cap) n = cap;
+int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out) {
+  // about 4096 blocks per launch (pieces x offsets x dW tiles), at least 256
+  // pairs per piece; one-offset contractions (network-in-network weight
+  // gradients) at most 768 pieces (fewer partial tiles to reduce)
+  if (K < 1 || c_in < 16 || c_out < 16) return 1;
+  auto pick = [](int n16) { return n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1)); };
+  const int64_t n_ty = (int64_t)(c_in / (16 * pick(c_in / 16))) * (c_out / (16 * pick(c_out / 16)));
+  int64_t n = total_pairs / ((int64_t)K * 256);
+  const int64_t by_grid = 4096 / ((int64_t)K * n_ty);
+  if (n > by_grid) n = by_grid;
+  if (K == 1 && n > 768) n = 768;
   return n < 1 ? 1 : n;
 }
 

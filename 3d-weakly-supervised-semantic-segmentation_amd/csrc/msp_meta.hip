@@ -30,14 +30,28 @@ __global__ __launch_bounds__(kThreads) void point_keys_kernel(const int64_t* __r
     keys[i] = bad ? kEmptyKey : make_key(b, x, y, z, log2s);
     vals[i] = (int32_t)i;
   }
-  // one atomic per wave
+  // wave reductions, then one pair of atomics per block (per-wave atomics on
+  // two addresses serialised the kernel at ~25k waves)
+  __shared__ int64_t red_bad[kThreads / 64], red_max[kThreads / 64];
   const unsigned long long badm = ballot64(bad);
   int64_t bmax = (i < n && !bad) ? b : 0;
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) bmax = max(bmax, (int64_t)__shfl_xor(bmax, d, 64));
+  const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    if (badm) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)__popcll(badm));
-    atomicMax((unsigned long long*)&stats[1], (unsigned long long)bmax);
+    red_bad[wave] = __popcll(badm);
+    red_max[wave] = bmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t nb = 0, mx = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+      nb += red_bad[w];
+      mx = max(mx, red_max[w]);
+    }
+    if (nb) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)nb);
+    if (mx) atomicMax((unsigned long long*)&stats[1], (unsigned long long)mx);
   }
 }
 
@@ -215,30 +229,35 @@ __global__ __launch_bounds__(kThreads) void pair_fill_kernel(const int32_t* __re
 // mbcnt) into 16-row chunks that share the offset.
 constexpr int kChunk = MSP_CHUNK;
 
+// Phase 1 (both kernels): every wave ballots its 64 rows for all K offsets
+// and leaves the per-offset popcounts (and first present input row) in LDS;
+// one barrier; then per-tile sums over the TW waves.  K <= 255.
 template <int TW>
 __global__ __launch_bounds__(kThreads) void tile_count_kernel(const int32_t* __restrict__ map, int K, int64_t n,
                                                               int64_t n_tiles, int64_t* __restrict__ cnt,
                                                               int64_t* __restrict__ max_cnt) {
-  __shared__ int pc_s[kThreads / 64];
+  __shared__ uint8_t pc_s[kThreads / 64][256];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = wave % TW;
   const int64_t t = (int64_t)blockIdx.x * (kThreads / 64 / TW) + wave / TW;
   const int64_t r = t * (64 * TW) + sub * 64 + lane;
   const bool live = t < n_tiles && r < n;
-  int64_t nch = 0;
+
   for (int o = 0; o < K; ++o) {
     const int pc = __popcll(ballot64(live && map[(int64_t)o * n + r] >= 0));
-    int tot = pc;
-    if (TW > 1) {
-      if (lane == 0) pc_s[wave] = pc;
-      __syncthreads();
-      tot = 0;
+    if (lane == 0) pc_s[wave][o] = (uint8_t)pc;
+  }
+  if (TW > 1) __syncthreads();
+  if (sub != 0 || t >= n_tiles) return;
+  int64_t nch = 0;
+  for (int o = lane; o < K; o += 64) {
+    int tot = 0;
 #pragma unroll
-      for (int w = 0; w < TW; ++w) tot += pc_s[wave - sub + w];
-      __syncthreads();
-    }
+    for (int w = 0; w < TW; ++w) tot += pc_s[wave + w][o];
     nch += (tot + kChunk - 1) / kChunk;
   }
-  if (sub == 0 && lane == 0 && t < n_tiles) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) nch += __shfl_xor(nch, d, 64);
+  if (lane == 0) {
     cnt[t] = nch;
     atomicMax(reinterpret_cast<unsigned long long*>(max_cnt), (unsigned long long)nch);
   }
@@ -252,56 +271,82 @@ __global__ __launch_bounds__(kThreads) void tile_fill_kernel(const int32_t* __re
                                                              int32_t* __restrict__ chunk_src,
                                                              uint16_t* __restrict__ chunk_row) {
   constexpr int TR = 64 * TW;
-  __shared__ int pc_s[kThreads / 64];
-  __shared__ int32_t first_s[kThreads / 64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = wave % TW;
-  const int64_t t = (int64_t)blockIdx.x * (kThreads / 64 / TW) + wave / TW;
+  constexpr int TPB = kThreads / 64 / TW;  // tiles per block
+  __shared__ uint8_t pc_s[kThreads / 64][256];
+  __shared__ int32_t first_s[kThreads / 64][256];
+  __shared__ int32_t cst_s[TPB][256];  // first chunk of each offset (relative to the tile)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = wave % TW, tb = wave / TW;
+  const int64_t t = (int64_t)blockIdx.x * TPB + tb;
   const int slot = sub * 64 + lane;  // row inside the tile
   const int64_t r = t * TR + slot;
   const bool live = t < n_tiles && r < n;
-  int64_t c = t < n_tiles ? tile_start[t] : 0;
+
   for (int o = 0; o < K; ++o) {
     const int32_t v = live ? map[(int64_t)o * n + r] : -1;
     const unsigned long long m = ballot64(v >= 0);
-    const int pc = __popcll(m);
-    // first present input row of this wave (padding slots repeat the tile's
-    // first present row of this offset: in bounds and nearby for the gather)
     const int32_t vf = m ? __shfl(v, __ffsll((long long)m) - 1) : -1;
-    int before = 0, tot = pc;
-    int32_t vfirst = vf;
-    if (TW > 1) {
-      if (lane == 0) {
-        pc_s[wave] = pc;
-        first_s[wave] = vf;
-      }
-      __syncthreads();
-      tot = 0;
-      vfirst = -1;
+    if (lane == 0) {
+      pc_s[wave][o] = (uint8_t)__popcll(m);
+      first_s[wave][o] = vf;
+    }
+  }
+  __syncthreads();
+  if (sub == 0) {
+    // per offset: chunk count, exclusive prefix over offsets (64 at a time),
+    // and the tile's first present input row (padding slots repeat it)
+    int carry = 0;
+    for (int o0 = 0; o0 < K; o0 += 64) {
+      const int o = o0 + lane;
+      int nchk = 0;
+      int32_t vfirst = -1;
+      if (o < K) {
+        int tot = 0;
 #pragma unroll
-      for (int w = 0; w < TW; ++w) {
-        const int p = pc_s[wave - sub + w];
-        if (w < sub) before += p;
-        tot += p;
-        const int32_t f = first_s[wave - sub + w];
-        if (vfirst < 0) vfirst = f;
+        for (int w = 0; w < TW; ++w) {
+          tot += pc_s[wave + w][o];
+          const int32_t f = first_s[wave + w][o];
+          if (vfirst < 0) vfirst = f;
+        }
+        nchk = (tot + kChunk - 1) / kChunk;
       }
-      __syncthreads();
+      const int incl = wave_incl_scan(nchk);
+      if (o < K) {
+        cst_s[tb][o] = carry + incl - nchk;
+        first_s[wave][o] = vfirst;
+      }
+      carry += __shfl(incl, 63, 64);
+    }
+  }
+  __syncthreads();
+  if (t >= n_tiles) return;
+  const int64_t c0 = tile_start[t];
+  const int w0 = wave - sub;
+
+  for (int o = 0; o < K; ++o) {
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < TW; ++w) {
+      const int p = pc_s[w0 + w][o];
+      if (w < sub) before += p;
+      tot += p;
     }
     if (tot == 0) continue;  // uniform over the tile
+    const int64_t c = c0 + cst_s[tb][o];
     const int nch = (tot + kChunk - 1) / kChunk;
+    const int32_t v = live ? map[(int64_t)o * n + r] : -1;
     if (v >= 0) {
+      const unsigned long long m = ballot64(true);  // lanes with a neighbour (exec = v >= 0)
       const int pos = before + mbcnt64(m);
       const int64_t e = (c + pos / kChunk) * kChunk + (pos % kChunk);
       chunk_src[e] = v;
       chunk_row[e] = (uint16_t)slot;
     }
-    if (t < n_tiles && slot >= tot && slot < nch * kChunk) {  // padding slots of the last chunk
+    if (slot >= tot && slot < nch * kChunk) {  // padding slots of the last chunk
       const int64_t e = (c + slot / kChunk) * kChunk + (slot % kChunk);
-      chunk_src[e] = vfirst;
+      chunk_src[e] = first_s[w0][o];
       chunk_row[e] = (uint16_t)TR;
     }
-    if (t < n_tiles && slot < nch) chunk_off[c + slot] = (uint8_t)o;
-    c += nch;
+    if (slot < nch) chunk_off[c + slot] = (uint8_t)o;
   }
 }
 
@@ -430,11 +475,12 @@ int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32
   int64_t* total = offs + m;
   void* sws = total + 1;
   dim3 grid((unsigned)nrb, (unsigned)K);
-  pair_count_kernel<<<grid, kThreads, 0, s>>>(map, n, nrb, counts);
-  int rc = scan_exclusive_i64(counts, offs, m, total, sws, scan_ws_bytes(m), s);
-  if (rc) return rc;
-  pair_starts_kernel<<<(unsigned)ceil_div(K + 1, 256), 256, 0, s>>>(offs, K, nrb, total, off_start);
-  if (cap > 0) {
+  if (cap <= 0) {  // counting call; the filling call reuses its workspace (block offsets)
+    pair_count_kernel<<<grid, kThreads, 0, s>>>(map, n, nrb, counts);
+    int rc = scan_exclusive_i64(counts, offs, m, total, sws, scan_ws_bytes(m), s);
+    if (rc) return rc;
+    pair_starts_kernel<<<(unsigned)ceil_div(K + 1, 256), 256, 0, s>>>(offs, K, nrb, total, off_start);
+  } else {
     pair_fill_kernel<<<grid, kThreads, 0, s>>>(map, n, nrb, offs, pair_in, pair_out);
   }
   return check_launch("msp_pair_lists");
@@ -457,24 +503,30 @@ int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64
   int64_t* cnt = reinterpret_cast<int64_t*>(ws);
   void* sws = cnt + n_tiles + 1;
   const int tw = tile_rows / 64;
-  MSP_HIP(hipMemsetAsync(tile_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_tile_rulebook");
   const unsigned g = (unsigned)ceil_div(n_tiles, kThreads / 64 / tw);
-#define TW_CASE(W)                                                                              \
-  case W:                                                                                       \
-    tile_count_kernel<W><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, tile_start + n_tiles + 1);                      \
-    break;
-  switch (tw) { TW_CASE(1) TW_CASE(2) TW_CASE(4) }
-#undef TW_CASE
-  int rc = scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
-  if (rc) return rc;
-  if (chunk_cap > 0) {
-#define TW_CASE(W)                                                                                     \
-  case W:                                                                                              \
-    tile_fill_kernel<W><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, tile_start, chunk_off, chunk_src,  \
-                                               chunk_row);                                            \
-    break;
-    switch (tw) { TW_CASE(1) TW_CASE(2) TW_CASE(4) }
-#undef TW_CASE
+  if (chunk_cap <= 0) {  // counting call; the filling call reuses its tile_start
+    MSP_HIP(hipMemsetAsync(tile_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_tile_rulebook");
+    int64_t* mx = tile_start + n_tiles + 1;
+    switch (tw) {
+      case 1: tile_count_kernel<1><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, mx); break;
+      case 2: tile_count_kernel<2><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, mx); break;
+      default: tile_count_kernel<4><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, mx); break;
+    }
+    const int rc =
+        scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
+    if (rc) return rc;
+  } else {
+    switch (tw) {
+      case 1:
+        tile_fill_kernel<1><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, tile_start, chunk_off, chunk_src, chunk_row);
+        break;
+      case 2:
+        tile_fill_kernel<2><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, tile_start, chunk_off, chunk_src, chunk_row);
+        break;
+      default:
+        tile_fill_kernel<4><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, tile_start, chunk_off, chunk_src, chunk_row);
+        break;
+    }
   }
   return check_launch("msp_tile_rulebook");
 }

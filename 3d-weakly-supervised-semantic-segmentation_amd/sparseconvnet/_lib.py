@@ -37,7 +37,7 @@ PROTOTYPES = {
     "msp_conv_tile_workspace_size": (SZ, [I64, I, I, I]),
     "msp_conv_tile": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_pairs": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
-    "msp_wgrad_pieces": (I64, [I64, I]),
+    "msp_wgrad_pieces": (I64, [I64, I, I, I]),
     "msp_conv_wgrad": (I, [P, I, P, I, P, P, P, I, I64, P, P, P]),
     "msp_bn_partials": (I64, [I64, I]),
     "msp_bn_stats": (I, [P, I64, I, P, P]),

@@ -87,7 +87,7 @@ def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out):
 def conv_wgrad(x, dy, pairs, pin, pout, K):
     c_in, c_out = x.size(1), dy.size(1)
     dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
-    n_pieces = int(_lib.query("msp_wgrad_pieces", _lib.I64(pairs.total), K))
+    n_pieces = int(_lib.query("msp_wgrad_pieces", _lib.I64(pairs.total), K, c_in, c_out))
     slab = torch.empty((n_pieces, K, c_in, c_out), dtype=torch.float32, device=x.device)
     call("msp_conv_wgrad", ptr(x), c_in, ptr(dy), c_out, ptr(pin), ptr(pout), ptr(pairs.off_start), K,
          n_pieces, ptr(slab), ptr(dw), _stream(x))

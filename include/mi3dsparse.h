@@ -89,7 +89,9 @@ int msp_down_map(const uint64_t* fine_keys, int64_t n_fine, const int32_t* paren
 /* Per-offset pair lists of an offset-major map: for o in [0,K), for every row
  * r with map[o][r] >= 0 (ascending r): (pair_in, pair_out) = (map[o][r], r).
  * off_start[K+1] (device int64) gets the list starts.  Pass cap = 0 to only
- * count (off_start[K] = total), then call again with cap >= total. */
+ * count (off_start[K] = total), then call again with cap >= total and the same
+ * off_start and workspace (the filling call reuses the counting call's block
+ * offsets instead of recounting). */
 int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32_t* pair_out, int64_t cap,
                    int64_t* off_start, void* ws, size_t ws_bytes, msp_stream_t stream);
 /* Output-tile rulebook for msp_conv_tile: rows are cut into tiles of
@@ -101,7 +103,8 @@ int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32
  * = input row, chunk_row[c*16+j] = row inside the tile.  Padding slots of a
  * chunk have chunk_row = tile_rows and repeat a present input row of the same
  * tile and offset (so every gather stays in bounds).
- * Count-then-fill like msp_pair_lists (total chunks = tile_start[n_tiles]). */
+ * Count-then-fill like msp_pair_lists (total chunks = tile_start[n_tiles]); the
+ * filling call reuses tile_start from the counting call. */
 int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64_t* tile_start,
                       uint8_t* chunk_off, int32_t* chunk_src, uint16_t* chunk_row, int64_t chunk_cap, void* ws,
                       size_t ws_bytes, msp_stream_t stream);
@@ -141,10 +144,10 @@ int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, 
  * row) is cut into n_pieces equal pieces; piece j of every offset covers
  * about the same row band, and the K pieces of a band run together so the
  * band's rows are read from L2 once.  Piece (j, o) writes its partial tile to
- * slab[n_pieces][K][c_in][c_out]; a second kernel reduces the pieces in order
- * j = 0, 1, ... (deterministic) into dw[K][c_in][c_out].  msp_wgrad_pieces
- * gives the piece count the library is tuned for. */
-int64_t msp_wgrad_pieces(int64_t total_pairs, int K);
+ * slab[n_pieces][K][c_in][c_out]; a second kernel reduces the pieces in a
+ * fixed order (deterministic) into dw[K][c_in][c_out].  msp_wgrad_pieces
+ * gives the piece count the library is tuned for (about 4096 blocks). */
+int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out);
 int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
                    const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
                    float* dw, msp_stream_t stream);

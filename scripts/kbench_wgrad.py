@@ -37,5 +37,5 @@ for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 128])):
         ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
         err = max(err, ((dw[o].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
     flops = 2.0 * rules.n_rules * c * c
-    print(f"L{L} V={V} R={rules.n_rules} pieces={_lib.query('msp_wgrad_pieces', _lib.I64(p.total), 27)}: {ms:.3f} ms "
+    print(f"L{L} V={V} R={rules.n_rules} pieces={_lib.query('msp_wgrad_pieces', _lib.I64(p.total), 27, c, c)}: {ms:.3f} ms "
           f"{flops / ms / 1e9:.1f} TF  max rel err {err:.2e}", flush=True)
