@@ -30,10 +30,14 @@ __global__ __launch_bounds__(kThreads) void point_keys_kernel(const int64_t* __r
     keys[i] = bad ? kEmptyKey : make_key(b, x, y, z, log2s);
     vals[i] = (int32_t)i;
   }
+  // batch column non-decreasing along the points? (the fused encoder tail
+  // relies on scene b being the point range of batch id b)
+  const bool desc = i > 0 && i < n && b < coords[(i - 1) * stride + 3];
   // wave reductions, then one pair of atomics per block (per-wave atomics on
   // two addresses serialised the kernel at ~25k waves)
-  __shared__ int64_t red_bad[kThreads / 64], red_max[kThreads / 64];
+  __shared__ int64_t red_bad[kThreads / 64], red_max[kThreads / 64], red_desc[kThreads / 64];
   const unsigned long long badm = ballot64(bad);
+  const unsigned long long descm = ballot64(desc);
   int64_t bmax = (i < n && !bad) ? b : 0;
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) bmax = max(bmax, (int64_t)__shfl_xor(bmax, d, 64));
@@ -41,17 +45,20 @@ __global__ __launch_bounds__(kThreads) void point_keys_kernel(const int64_t* __r
   if ((threadIdx.x & 63) == 0) {
     red_bad[wave] = __popcll(badm);
     red_max[wave] = bmax;
+    red_desc[wave] = __popcll(descm);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int64_t nb = 0, mx = 0;
+    int64_t nb = 0, mx = 0, nd = 0;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; ++w) {
       nb += red_bad[w];
       mx = max(mx, red_max[w]);
+      nd += red_desc[w];
     }
     if (nb) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)nb);
     if (mx) atomicMax((unsigned long long*)&stats[1], (unsigned long long)mx);
+    if (nd) atomicAdd((unsigned long long*)&stats[2], (unsigned long long)nd);
   }
 }
 

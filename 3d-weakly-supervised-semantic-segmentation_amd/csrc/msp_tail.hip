@@ -1,0 +1,169 @@
+// Fused encoder tail for training:
+//
+//   OutputLayer -> SparseConvBase_.postProcessing
+//   (models/SparseConvNet.py:20-26: per-scene torch.mean over the point rows
+//    [batch_offsets[b], batch_offsets[b+1]) of the per-point features)
+//
+// computed straight from the level-0 voxel rows, without materialising the
+// (N, C) per-point tensor:
+//
+//   out[b] = (1 / n_b) * sum over voxels v of scene b of cnt_v * feat[v]
+//
+// where cnt_v = vstart[v+1] - vstart[v] is the number of points in voxel v
+// (every point of v carries feat[v] after the OutputLayer) and n_b the points
+// of scene b.  Voxel rows are sorted by Morton key with the batch index in
+// the high bits, so each scene is one contiguous voxel range.  The reduction
+// is two-stage and fixed-order (pieces of kPiece rows inside one scene, then
+// the pieces of a scene in order): bitwise reproducible.
+//
+// Backward: dfeat[v] = cnt_v / n_b(v) * dout[b(v)].
+#include "msp_common.h"
+
+namespace msp {
+
+constexpr int kTT = 256;
+constexpr int kPiece = 1024;  // voxel rows per stage-1 block
+
+// vscene[b] = first voxel row of scene b (b in [0, B]), from the sorted keys
+__global__ __launch_bounds__(kTT) void scene_ranges_kernel(const uint64_t* __restrict__ keys, int64_t V, int shift,
+                                                           int B, int64_t* __restrict__ vscene) {
+  const int64_t v = (int64_t)blockIdx.x * kTT + threadIdx.x;
+  if (v > V) return;
+  const int64_t bv = v < V ? (int64_t)(keys[v] >> shift) : (int64_t)B;
+  const int64_t bp = v > 0 ? (int64_t)(keys[v - 1] >> shift) : -1;
+  const int64_t hi = bv < B ? bv : B;
+  for (int64_t b = bp + 1; b <= hi; ++b) vscene[b] = v;
+}
+
+// pstart[b] = first stage-1 piece of scene b (pstart[B] = number of pieces);
+// npts[b] = points of scene b (from the voxel point runs)
+__global__ __launch_bounds__(kTT) void scene_pieces_kernel(const int64_t* __restrict__ vscene,
+                                                           const int32_t* __restrict__ vstart, int B,
+                                                           int64_t* __restrict__ pstart, int64_t* __restrict__ npts) {
+  if (threadIdx.x != 0) return;
+  int64_t acc = 0;
+  for (int b = 0; b < B; ++b) {
+    pstart[b] = acc;
+    const int64_t v0 = vscene[b], v1 = vscene[b + 1];
+    acc += (v1 - v0 + kPiece - 1) / kPiece;
+    npts[b] = (int64_t)vstart[v1] - (int64_t)vstart[v0];
+  }
+  pstart[B] = acc;
+}
+
+// stage 1: block p sums cnt_v * feat[v] over its piece's rows; thread layout
+// rows-in-parallel x channels (C <= 256), or all threads on channels with the
+// rows sequential (C > 256, up to 4 channels per thread)
+__global__ __launch_bounds__(kTT) void scene_partial_kernel(const float* __restrict__ f, int C,
+                                                            const int32_t* __restrict__ vstart,
+                                                            const int64_t* __restrict__ vscene,
+                                                            const int64_t* __restrict__ pstart, int B,
+                                                            float* __restrict__ partial) {
+  __shared__ float red[kTT];
+  const int64_t p = blockIdx.x;
+  if (p >= pstart[B]) return;  // the grid is sized for the worst case
+  int lo = 0, hi = B;          // scene b with pstart[b] <= p < pstart[b+1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pstart[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  const int b = lo;
+  const int64_t r0 = vscene[b] + (p - pstart[b]) * kPiece;
+  const int64_t r1 = min(r0 + kPiece, vscene[b + 1]);
+  const int t = threadIdx.x;
+  float* dst = partial + p * (int64_t)C;
+  if (C <= kTT) {
+    const int RG = kTT / C, g = t / C, c = t % C;
+    float s = 0.f;
+    if (g < RG) {
+      for (int64_t v = r0 + g; v < r1; v += RG) s += (float)(vstart[v + 1] - vstart[v]) * f[v * C + c];
+    }
+    red[t] = s;
+    __syncthreads();
+    if (t < C) {
+      float acc = 0.f;
+      for (int k = 0; k < RG; ++k) acc += red[k * C + t];
+      dst[t] = acc;
+    }
+  } else {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t v = r0; v < r1; ++v) {
+      const float w = (float)(vstart[v + 1] - vstart[v]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (t + k * kTT < C) s[k] += w * f[v * C + t + k * kTT];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (t + k * kTT < C) dst[t + k * kTT] = s[k];
+  }
+}
+
+// stage 2: out[b][c] = (sum of scene b's pieces, in order) / n_b
+__global__ __launch_bounds__(kTT) void scene_final_kernel(const float* __restrict__ partial, int C,
+                                                          const int64_t* __restrict__ pstart,
+                                                          const int64_t* __restrict__ npts, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * kTT + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int64_t p = pstart[b]; p < pstart[b + 1]; ++p) s += partial[p * C + c];
+  const int64_t n = npts[b];
+  out[(int64_t)b * C + c] = n > 0 ? s / (float)n : 0.f;
+}
+
+__global__ __launch_bounds__(kTT) void scene_mean_bwd_kernel(const float* __restrict__ dout, int C,
+                                                             const uint64_t* __restrict__ keys, int64_t V, int shift,
+                                                             const int32_t* __restrict__ vstart,
+                                                             const int64_t* __restrict__ npts,
+                                                             float* __restrict__ df) {
+  const int64_t n = V * C;
+  for (int64_t e = (int64_t)blockIdx.x * kTT + threadIdx.x; e < n; e += (int64_t)gridDim.x * kTT) {
+    const int64_t v = e / C;
+    const int c = (int)(e % C);
+    const int64_t b = (int64_t)(keys[v] >> shift);
+    const float w = (float)(vstart[v + 1] - vstart[v]) / (float)npts[b];
+    df[e] = w * dout[b * C + c];
+  }
+}
+
+inline int64_t n_pieces_bound(int64_t V, int B) { return (V + kPiece - 1) / kPiece + B; }
+
+}  // namespace msp
+
+using namespace msp;
+
+extern "C" {
+
+size_t msp_scene_mean_workspace_size(int64_t V, int B, int C) {
+  return (size_t)(B + 1) * sizeof(int64_t) + (size_t)n_pieces_bound(V, B) * (size_t)C * sizeof(float);
+}
+
+int msp_scene_mean_fwd(const float* feats, int C, const uint64_t* keys, int64_t V, int shift,
+                       const int32_t* vstart, int B, int64_t* vscene, int64_t* npts, float* out, void* ws,
+                       size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && C <= 4 * kTT && B >= 1 && V >= 0 && shift >= 0 && shift < 64,
+              "msp_scene_mean_fwd: bad arguments (C=%d B=%d V=%lld)", C, B, (long long)V);
+  MSP_REQUIRE(ws_bytes >= msp_scene_mean_workspace_size(V, B, C), "msp_scene_mean_fwd: workspace too small");
+  hipStream_t s = as_stream(stream);
+  int64_t* pstart = static_cast<int64_t*>(ws);
+  float* partial = reinterpret_cast<float*>(pstart + B + 1);
+  scene_ranges_kernel<<<(unsigned)ceil_div(V + 1, kTT), kTT, 0, s>>>(keys, V, shift, B, vscene);
+  scene_pieces_kernel<<<1, 64, 0, s>>>(vscene, vstart, B, pstart, npts);
+  scene_partial_kernel<<<(unsigned)n_pieces_bound(V, B), kTT, 0, s>>>(feats, C, vstart, vscene, pstart, B, partial);
+  scene_final_kernel<<<dim3((unsigned)ceil_div(C, kTT), (unsigned)B), kTT, 0, s>>>(partial, C, pstart, npts, out);
+  return check_launch("msp_scene_mean_fwd");
+}
+
+int msp_scene_mean_bwd(const float* dout, int C, const uint64_t* keys, int64_t V, int shift, const int32_t* vstart,
+                       const int64_t* npts, float* dfeats, msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && V >= 0, "msp_scene_mean_bwd: bad arguments");
+  if (V == 0) return MSP_OK;
+  int64_t g = ceil_div(V * C, kTT);
+  if (g > 65535 * 16) g = 65535 * 16;
+  scene_mean_bwd_kernel<<<(unsigned)g, kTT, 0, as_stream(stream)>>>(dout, C, keys, V, shift, vstart, npts, dfeats);
+  return check_launch("msp_scene_mean_bwd");
+}
+
+}  // extern "C"

@@ -53,6 +53,9 @@ PROTOTYPES = {
     "msp_unpool_bwd": (I, [P, I, P, I64, P, P]),
     "msp_maxpool_fwd": (I, [P, I, P, I64, P, P, P]),
     "msp_maxpool_bwd": (I, [P, I, P, I64, P, P]),
+    "msp_scene_mean_workspace_size": (SZ, [I64, I, I]),
+    "msp_scene_mean_fwd": (I, [P, I, P, I64, I, P, I, P, P, P, P, SZ, P]),
+    "msp_scene_mean_bwd": (I, [P, I, P, I64, I, P, P, P, P]),
 }
 
 _lib = None

@@ -160,6 +160,7 @@ class InputRules:
 
     def __init__(self, n_points, perm, p2v, vstart, batch_size):
         self.n_points, self.perm, self.p2v, self.vstart, self.batch_size = n_points, perm, p2v, vstart, batch_size
+        self.batch_monotonic = False  # batch column non-decreasing along the points
 
 
 class Metadata:
@@ -180,10 +181,10 @@ class Metadata:
         n = coords.size(0)
         keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         vals = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        stats = torch.zeros(2, dtype=torch.int64, device=dev)
+        stats = torch.zeros(3, dtype=torch.int64, device=dev)
         if n:
             call("msp_point_keys", ptr(coords), n, 4, log2, size, ptr(keys), ptr(vals), ptr(stats), s)
-        n_bad, max_b = stats.tolist()
+        n_bad, max_b, n_desc = stats.tolist()
         if n_bad:
             raise ValueError(f"InputLayer: {n_bad} points outside [0, {size})^3 or with a negative batch index")
         end_bit = min(64, 3 * log2 + max(1, int(max_b).bit_length()))
@@ -207,6 +208,7 @@ class Metadata:
         lvl = Level(size, log2, uniq[:max(V, 1)], V, dev)
         self.levels[size] = lvl
         self.input = InputRules(n, perm[:n], p2v[:n], vstart[:V + 1], int(max_b) + 1 if n else 0)
+        self.input.batch_monotonic = n_desc == 0
         return lvl
 
     def level(self, size):

@@ -337,6 +337,41 @@ class OutputLayerFunction(torch.autograd.Function):
         return din[:ctx.V], None
 
 
+class SceneMeanFunction(torch.autograd.Function):
+    """Fused OutputLayer + per-scene mean over the points (SURVEY.md §8(f)
+    rank 2; models/SparseConvNet.py:20-26) from the level-0 voxel rows:
+    out[b] = sum_v cnt_v feat[v] / n_b without the (N, C) per-point tensor."""
+
+    @staticmethod
+    def forward(ctx, x, level, rules, B):
+        _check_feats(x)
+        x = x.contiguous()
+        V, C = x.shape
+        dev = x.device
+        vscene = torch.empty(B + 1, dtype=torch.int64, device=dev)
+        npts = torch.empty(B, dtype=torch.int64, device=dev)
+        out = torch.empty((B, C), dtype=torch.float32, device=dev)
+        wsb = int(_lib.query("msp_scene_mean_workspace_size", _lib.I64(V), B, C))
+        ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=dev)
+        shift = 3 * level.log2
+        call("msp_scene_mean_fwd", ptr(x), C, ptr(level.keys), V, shift, ptr(rules.vstart), B, ptr(vscene),
+             ptr(npts), ptr(out), ptr(ws), wsb, _stream(x))
+        ctx.level, ctx.rules, ctx.V, ctx.shift = level, rules, V, shift
+        ctx.save_for_backward(npts)
+        ctx.mark_non_differentiable(npts)
+        return out, npts
+
+    @staticmethod
+    def backward(ctx, g, _gn):
+        (npts,) = ctx.saved_tensors
+        g = g.contiguous()
+        C = g.size(1)
+        dx = torch.empty((max(ctx.V, 1), C), dtype=torch.float32, device=g.device)
+        call("msp_scene_mean_bwd", ptr(g), C, ptr(ctx.level.keys), ctx.V, ctx.shift, ptr(ctx.rules.vstart),
+             ptr(npts), ptr(dx), _stream(g))
+        return dx[:ctx.V], None, None, None
+
+
 class UnPoolingFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, rules, n_fine):

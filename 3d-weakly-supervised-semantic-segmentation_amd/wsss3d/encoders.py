@@ -16,6 +16,7 @@ import torch
 from torch import nn
 
 import sparseconvnet as scn
+from sparseconvnet.ops import SceneMeanFunction
 
 from .registry import MODEL_REGISTRY
 
@@ -55,8 +56,45 @@ class SparseConvBase_(nn.Module):
         if coords.size(0) != feats.size(0):
             raise AssertionError(f"Coords and feats not aligned! coords's batchsize is {coords.size(0)} "
                                  f"while feats' is {feats.size(0)}. ")
+        if istrain and self._fusable():
+            return self._encode_scene_means(coords, feats, x["batch_offsets"])
         out = self.encode([coords, feats])
         return self.postProcessing(out, x["batch_offsets"]) if istrain else out
+
+    # ---------------------------------------------------------------- fused tail
+    def _fusable(self):
+        """The default encode/postProcessing over a Sequential ending in an
+        OutputLayer (every registered encoder): the training output can skip
+        the (N, C) per-point tensor."""
+        enc = self.encoder
+        return (type(self).encode is SparseConvBase_.encode
+                and type(self).postProcessing is SparseConvBase_.postProcessing
+                and isinstance(enc, scn.Sequential) and len(enc) > 1 and isinstance(enc[-1], scn.OutputLayer))
+
+    def _encode_scene_means(self, coords, feats, batch_offsets):
+        """Per-scene means straight from the level-0 voxel rows
+        (ops.SceneMeanFunction).  Valid when scene b is exactly the points of
+        batch id b: batch column non-decreasing and the first/last point of
+        every range carrying its index; otherwise the per-point path runs."""
+        off = [int(o) for o in batch_offsets]
+        B = len(off) - 1
+        t = self.encoder[:-1]([coords, feats])
+        rules = t.metadata.input
+        ok = B >= 1 and rules.batch_monotonic and rules.batch_size <= B and off[0] == 0 and off[-1] == coords.size(0)
+        if ok:
+            idx, want = [], []
+            for b in range(B):
+                if off[b + 1] > off[b]:
+                    idx += [off[b], off[b + 1] - 1]
+                    want += [b, b]
+            if idx:
+                got = coords[torch.tensor(idx, device=coords.device), -1].tolist()
+                ok = [int(v) for v in got] == want
+        if not ok:
+            return self.postProcessing(self.encoder[-1](t), batch_offsets)
+        lvl = t.metadata.level(int(t.spatial_size[0]))
+        out, _ = SceneMeanFunction.apply(t.features, lvl, rules, B)
+        return out
 
 
 def _wrap(dimension, full_scale, m, make_body, out_planes):

@@ -55,7 +55,9 @@ const char* msp_last_error(void);
 /* coords: n rows of `row_stride` int64, [x, y, z, batch] (batch column last,
  * dataset/data.py:198).  Writes Morton keys and vals[i] = i.  stats[0] =
  * number of rows outside [0, spatial_size)^3 or with negative batch id,
- * stats[1] = max batch id.  stats must be zeroed by the caller. */
+ * stats[1] = max batch id, stats[2] = number of rows whose batch id is below
+ * the previous row's (0: batch column non-decreasing).  stats[3] must be
+ * zeroed by the caller. */
 int msp_point_keys(const int64_t* coords, int64_t n, int64_t row_stride, int log2_size, int64_t spatial_size,
                    uint64_t* keys, int32_t* vals, int64_t* stats, msp_stream_t stream);
 
@@ -192,6 +194,22 @@ int msp_maxpool_fwd(const float* in, int C, const int32_t* child_start, int64_t 
 /* din must be zeroed by the caller */
 int msp_maxpool_bwd(const float* dout, int C, const int32_t* argmax, int64_t n_coarse, float* din,
                     msp_stream_t stream);
+
+/* ---------------- fused encoder tail (training): OutputLayer + per-scene
+ * mean of the per-point features, SparseConvBase_.postProcessing
+ * (models/SparseConvNet.py:20-26), from the level-0 voxel rows without the
+ * (N, C) per-point tensor.  keys: the level's sorted keys, shift = 3*log2 of
+ * its spatial size (batch = key >> shift), vstart[V+1]: point runs of the
+ * voxels (InputLayer).  Writes vscene[B+1] (voxel range of each scene),
+ * npts[B] (points per scene) and out[B][C] = mean over the scene's points;
+ * 1 <= C <= 1024.  Fixed-order two-stage reduction (deterministic). */
+size_t msp_scene_mean_workspace_size(int64_t V, int B, int C);
+int msp_scene_mean_fwd(const float* feats, int C, const uint64_t* keys, int64_t V, int shift,
+                       const int32_t* vstart, int B, int64_t* vscene, int64_t* npts, float* out, void* ws,
+                       size_t ws_bytes, msp_stream_t stream);
+/* dfeats[v] = (cnt_v / npts[b(v)]) * dout[b(v)] */
+int msp_scene_mean_bwd(const float* dout, int C, const uint64_t* keys, int64_t V, int shift, const int32_t* vstart,
+                       const int64_t* npts, float* dfeats, msp_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -114,3 +114,45 @@ def test_counters_match_oracle():
     ref(xo)
     assert scn.forward_pass_multiplyAdd_count == O.forward_pass_multiplyAdd_count > 0
     assert scn.forward_pass_hidden_states == O.forward_pass_hidden_states > 0
+
+
+@pytest.mark.parametrize("name,m", [("SparseConvUNet", 16), ("SparseConvFCNet", 8)])
+def test_fused_scene_mean_matches_per_point_path(name, m):
+    """istrain=True runs the fused tail (scene means from the voxel rows, no
+    (N, C) per-point tensor); it must equal OutputLayer + per-scene torch.mean
+    (models/SparseConvNet.py:20-26) in value and in every parameter gradient,
+    and a batch whose ranges do not match the batch column falls back to the
+    per-point path."""
+    torch.manual_seed(3)
+    batch = make_batch(3, 10, seed=5, spacing=0.05)
+    cfg = dict(m=m, dimension=3, full_scale=4096, block_reps=1, residual_blocks=False)
+    cls, _ = MODEL_REGISTRY.get(name)
+    model = cls(name, **cfg).to(DEV)
+    assert model._fusable()
+    x = EasyDict(coords=torch.from_numpy(batch["coords"]).to(DEV), feature=torch.from_numpy(batch["feats"]).to(DEV),
+                 batch_offsets=batch["batch_offsets"])
+    w = torch.randn(3, model(x).size(1), device=DEV)
+
+    def run(fused):
+        model.zero_grad()
+        if fused:
+            out = model(x, istrain=True)
+        else:
+            from wsss3d.encoders import segment_mean
+            out = segment_mean(model(x), x.batch_offsets)
+        (out * w).square().sum().backward()
+        return out.detach(), {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+
+    of, gf = run(True)
+    op, gp = run(False)
+    _close(of, op, 1e-5, "scene means")
+    for k in gp:
+        _close(gf[k], gp[k], 1e-4, "grad " + k)
+    # batch column not matching the ranges: the fused path must not be taken
+    xb = EasyDict(coords=x.coords.clone(), feature=x.feature, batch_offsets=x.batch_offsets)
+    xb.coords[0, -1] = 2
+    with torch.no_grad():
+        outb = model(xb, istrain=True)
+        from wsss3d.encoders import segment_mean
+        refb = segment_mean(model(xb), xb.batch_offsets)
+    _close(outb, refb, 1e-6, "fallback")
