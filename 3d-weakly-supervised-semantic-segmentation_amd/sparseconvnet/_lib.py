@@ -56,6 +56,8 @@ PROTOTYPES = {
     "msp_scene_mean_workspace_size": (SZ, [I64, I, I]),
     "msp_scene_mean_fwd": (I, [P, I, P, I64, I, P, I, P, P, P, P, SZ, P]),
     "msp_scene_mean_bwd": (I, [P, I, P, I64, I, P, P, P, P]),
+    "msp_merge_workspace_size": (SZ, [I, I64]),
+    "msp_merge": (I, [P, P, P, P, I, I64, I, D, P, P, P, P, P, P, I, P, P, P, P, I64, P, P, P, SZ, P]),
 }
 
 _lib = None

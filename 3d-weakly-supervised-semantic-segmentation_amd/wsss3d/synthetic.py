@@ -71,6 +71,61 @@ def make_room(seed: int, spacing: float = 0.02, jitter: float = 0.005):
     return coords.astype(np.float32), colours.astype(np.float32), labels
 
 
+def train_params(scale: float, seed: int, idx: int):
+    """The random draws of `trainMerge` for scene idx (`dataset/data.py:165-178, 200`),
+    in the reference's order: jitter matrix, flip, rotation angle, the two
+    rand(3) of the offset, the colour shift.  They do not depend on the data,
+    so the device batch assembly (wsss3d/merge.py) uses the same draws.
+    Returns (rot (3,3) f64, c1 (3,), c2 (3,), u1 (3,), u2 (3,), shift (3,) f32)."""
+    rng = np.random.RandomState(1000 + seed * 997 + idx)
+    m = np.eye(3) + rng.randn(3, 3) * 0.1  # data.py:165
+    m[0][0] *= rng.randint(0, 2) * 2 - 1
+    m *= scale
+    theta = rng.rand() * 2 * np.pi
+    rot = np.matmul(m, [[np.cos(theta), np.sin(theta), 0], [-np.sin(theta), np.cos(theta), 0], [0, 0, 1]])
+    u1, u2 = rng.rand(3), rng.rand(3)  # data.py:178, left to right
+    shift = rng.randn(3).astype(np.float32) * 0.1  # data.py:200
+    return rot, np.zeros(3), np.zeros(3), u1, u2, shift
+
+
+def val_params(scale: float, seed: int, idx: int):
+    """The random draws of `valMerge` (`dataset/data.py:263-275`): flip,
+    rotation, the centring jitter U(-2, 2)^3, the two rand(3) of the offset."""
+    rng = np.random.RandomState(2000 + seed * 997 + idx)
+    m = np.eye(3)
+    m[0][0] *= rng.randint(0, 2) * 2 - 1
+    m *= scale
+    theta = rng.rand() * 2 * np.pi
+    m = np.matmul(m, [[np.cos(theta), np.sin(theta), 0], [-np.sin(theta), np.cos(theta), 0], [0, 0, 1]])
+    c2 = rng.uniform(-2, 2, 3)
+    u1, u2 = rng.rand(3), rng.rand(3)
+    return m, None, c2, u1, u2, np.zeros(3, np.float32)
+
+
+def transform(a, rot, c1, c2):
+    """a . rot + c1 + c2 in fp64, each product and sum rounded in a fixed order
+    ((a0 r0j + a1 r1j) + a2 r2j) + c1j + c2j -- the reference's np.matmul in
+    float64 up to BLAS summation order; the device path uses the same order."""
+    a = a.astype(np.float64)
+    t = (a[:, 0:1] * rot[0][None, :] + a[:, 1:2] * rot[1][None, :]) + a[:, 2:3] * rot[2][None, :]
+    return (t + c1[None, :]) + c2[None, :]
+
+
+def _place(t, u1, u2, full_scale, mode):
+    """Random offset into [0, full_scale)^3 and the crop (data.py:174-182 train,
+    :271-277 val; each formula in its own evaluation order)."""
+    lo, hi = t.min(0), t.max(0)
+    if mode == "train":
+        length = hi - lo
+        q1, q2 = full_scale - length - 0.001, full_scale - length + 0.001
+    else:
+        q1, q2 = full_scale - hi + lo - 0.001, full_scale - hi + lo + 0.001
+    offset = -lo + np.clip(q1, 0, None) * u1 + np.clip(q2, None, 0) * u2
+    p = t + offset
+    keep = (p.min(1) >= 0) * (p.max(1) < full_scale)
+    return p, keep
+
+
 def train_merge(scenes, scale: float, full_scale: int = 4096, seed: int = 0):
     """Restates `trainMerge` (`dataset/data.py:135-238`) for the point-cloud part.
 
@@ -80,27 +135,15 @@ def train_merge(scenes, scale: float, full_scale: int = 4096, seed: int = 0):
     locs, feats, labels, scene_labels = [], [], [], []
     batch_offsets = [0]
     for idx, (a, b, c) in enumerate(scenes):
-        rng = np.random.RandomState(1000 + seed * 997 + idx)
-        m = np.eye(3) + rng.randn(3, 3) * 0.1  # data.py:165
-        m[0][0] *= rng.randint(0, 2) * 2 - 1
-        m *= scale
-        theta = rng.rand() * 2 * np.pi
-        rot = np.matmul(m, [[np.cos(theta), np.sin(theta), 0],
-                            [-np.sin(theta), np.cos(theta), 0], [0, 0, 1]])
-        a = np.matmul(a.astype(np.float64), rot)
-        lo, hi = a.min(0), a.max(0)
-        length = hi - lo
-        offset = (-lo + np.clip(full_scale - length - 0.001, 0, None) * rng.rand(3)
-                  + np.clip(full_scale - length + 0.001, None, 0) * rng.rand(3))  # data.py:178
-        a = a + offset
-        keep = (a.min(1) >= 0) * (a.max(1) < full_scale)  # data.py:181
-        a, bb, cc = a[keep], b[keep], c[keep]
+        rot, c1, c2, u1, u2, shift = train_params(scale, seed, idx)
+        p, keep = _place(transform(a, rot, c1, c2), u1, u2, full_scale, "train")
+        a, bb, cc = p[keep], b[keep], c[keep]
         a = a.astype(np.int64)  # torch.from_numpy(a).long() truncates toward zero
         sl = np.zeros(NUM_CLASSES, np.float32)
         u = np.unique(cc)
         sl[u[u >= 0]] = 1.0
         locs.append(np.concatenate([a, np.full((len(a), 1), idx, np.int64)], 1))
-        feats.append(bb + rng.randn(3).astype(np.float32) * 0.1)  # data.py:200
+        feats.append(bb + shift)  # data.py:200
         labels.append(cc)
         scene_labels.append(sl)
         batch_offsets.append(batch_offsets[-1] + int(keep.sum()))
@@ -115,19 +158,9 @@ def val_merge(scenes, scale: float, full_scale: int = 4096, seed: int = 0):
     locs, feats, labels, point_ids = [], [], [], []
     base = 0
     for idx, (a, b, c) in enumerate(scenes):
-        rng = np.random.RandomState(2000 + seed * 997 + idx)
-        m = np.eye(3)
-        m[0][0] *= rng.randint(0, 2) * 2 - 1
-        m *= scale
-        theta = rng.rand() * 2 * np.pi
-        m = np.matmul(m, [[np.cos(theta), np.sin(theta), 0], [-np.sin(theta), np.cos(theta), 0], [0, 0, 1]])
-        a = np.matmul(a.astype(np.float64), m) + full_scale / 2 + rng.uniform(-2, 2, 3)
-        lo, hi = a.min(0), a.max(0)
-        offset = (-lo + np.clip(full_scale - hi + lo - 0.001, 0, None) * rng.rand(3)
-                  + np.clip(full_scale - hi + lo + 0.001, None, 0) * rng.rand(3))
-        a = a + offset
-        keep = (a.min(1) >= 0) * (a.max(1) < full_scale)
-        a = a[keep].astype(np.int64)
+        m, _, c2, u1, u2, _ = val_params(scale, seed, idx)
+        p, keep = _place(transform(a, m, np.full(3, full_scale / 2), c2), u1, u2, full_scale, "val")
+        a = p[keep].astype(np.int64)
         locs.append(np.concatenate([a, np.full((len(a), 1), idx, np.int64)], 1))
         feats.append(b[keep])
         labels.append(c[keep])

@@ -211,6 +211,27 @@ int msp_scene_mean_fwd(const float* feats, int C, const uint64_t* keys, int64_t 
 int msp_scene_mean_bwd(const float* dout, int C, const uint64_t* keys, int64_t V, int shift, const int32_t* vstart,
                        const int64_t* npts, float* dfeats, msp_stream_t stream);
 
+/* ---------------- batch assembly on the device:
+ * the per-point part of trainMerge (mode 0, dataset/data.py:135-238) and
+ * valMerge (mode 1, :256-310) for B scenes already in HBM.  Scene b is points
+ * [scene_start[b], scene_start[b+1]) of xyz/rgb (f32, 3 per point) and labels
+ * (int64).  Per scene (device arrays, the host's random draws): rot[b][9]
+ * (t = a . rot), c1[b][3], c2[b][3] (added to t in that order), u1/u2[b][3]
+ * (the offset's two rand(3)), shift[b][3] (f32 colour shift).  fp64
+ * arithmetic in a fixed order without FMA contraction; then the mode's
+ * offset formula, the crop to [0, full_scale)^3 and trunc() -> coords
+ * (N,4) int64 [x,y,z,b] in point order, feats = rgb + shift, labels_out,
+ * point_ids (mode 1, may be NULL) = point_id_base + input index,
+ * batch_offsets[B+1] (device) and scene_labels[B][n_classes] (1 where a kept
+ * point has that label; n_classes <= 32).  Outputs are sized for all points
+ * (capacity scene_start[B]); the kept count is batch_offsets[B]. */
+size_t msp_merge_workspace_size(int B, int64_t max_scene_points);
+int msp_merge(const float* xyz, const float* rgb, const int64_t* labels, const int64_t* scene_start, int B,
+              int64_t max_scene_points, int mode, double full_scale, const double* rot, const double* c1,
+              const double* c2, const double* u1, const double* u2, const float* shift, int n_classes,
+              int64_t* coords, float* feats, int64_t* labels_out, int64_t* point_ids, int64_t point_id_base,
+              int64_t* batch_offsets, float* scene_labels, void* ws, size_t ws_bytes, msp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
