@@ -5,7 +5,7 @@ registry (`utils/registry.py`), encoder plugin surface
 producer (`dataset/data.py` transforms) and the data-parallel driver."""
 from .edict import EasyDict
 from .registry import LOSS_REGISTRY, MODEL_REGISTRY, Registry
-from . import encoders, heads  # noqa: F401  (registers the classes)
+from . import encoders, heads, text  # noqa: F401  (registers the classes)
 from .encoders import SparseConvBase_, segment_mean
 
 __all__ = ["EasyDict", "Registry", "MODEL_REGISTRY", "LOSS_REGISTRY", "SparseConvBase_", "segment_mean"]

@@ -2,9 +2,11 @@
 `utils/loss.py:5-33`).
 
 The training call is `model((x, text), istrain=True)` (train.py:69) and the
-eval call `model(x)` -> per-point logits (N, 20) (train.py:106).  The
-TextTransformer branch of MultiLabelContrastive is out of scope for this
-round: a text model must be supplied by the caller.
+eval call `model(x)` -> per-point logits (N, 20) (train.py:106).  The text
+model of MultiLabelContrastive is looked up in the registry: TextTransformer
+(wsss3d/text.py) is registered; CLIPTransformer needs pretrained CLIP weights
+that are not available offline.  Scene features in training come from the
+encoder's fused tail (per-scene means without the (N, C) tensor).
 """
 from __future__ import annotations
 
@@ -58,9 +60,9 @@ class FullySupervised(nn.Module):
 
 @MODEL_REGISTRY.register()
 class MultiLabelContrastive(nn.Module):
-    """Point + text heads (models/MultiLabelContrastive.py:7-47).  The text
-    encoder class is looked up in the registry; none is registered by this
-    package yet."""
+    """Point + text heads (models/MultiLabelContrastive.py:7-47).  The scene
+    features are the encoder's training output (per-scene means, the
+    reference's loop at :34-39, through the fused tail)."""
 
     def __init__(self, pc_config, text_config):
         super().__init__()
@@ -80,7 +82,7 @@ class MultiLabelContrastive(nn.Module):
             text_feats = self.text_linear(tf)
         else:
             text_feats = -1
-        global_feats = segment_mean(self.pc_encoder(pc_input), pc_input.batch_offsets)
+        global_feats = self.pc_encoder(pc_input, istrain=True)
         return self.linear(global_feats), (global_feats, text_feats, has_text)
 
 

@@ -132,7 +132,16 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--residual", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--workload", choices=["unet", "contrastive"], default="unet",
+                    help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
+                         "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
+                         "(CLIP text-tower shape: width 512, 12 layers, context 120, vocab 49408), 10 texts per "
+                         "scene, Classification + TextContrastive losses")
     args = ap.parse_args()
+    if args.workload == "contrastive":
+        if args.scale == 50:
+            args.scale = 20
+        args.reps, args.residual = 1, 0
 
     from wsss3d import dp
 
@@ -146,27 +155,47 @@ def main():
     _lib.load()
     # two distinct batches per rank, alternated step to step
     host_batches = [make_batch(args.batch, args.scale, seed=1000 * rank + k) for k in range(2)]
+    contrastive = args.workload == "contrastive"
+    n_text, seq_len, vocab = 10, 120, 49408
     batches = []
-    for b in host_batches:
+    for k, b in enumerate(host_batches):
         x = EasyDict(coords=torch.from_numpy(b["coords"]).to(dev), feature=torch.from_numpy(b["feats"]).to(dev),
                      batch_offsets=b["batch_offsets"])
         y = torch.from_numpy(b["scene_labels"]).to(dev)
         v0 = len(np.unique(b["coords"], axis=0))
-        batches.append((x, y, v0))
+        text = None
+        if contrastive:  # every scene has texts: random ids, end-of-text = the largest id
+            g = torch.Generator().manual_seed(1000 * rank + k)
+            tok = torch.randint(1, vocab - 1, (args.batch, n_text, seq_len), generator=g)
+            eot = torch.randint(8, seq_len, (args.batch, n_text), generator=g)
+            tok.scatter_(2, eot[..., None], vocab - 1)
+            tok = torch.where(torch.arange(seq_len)[None, None] > eot[..., None], torch.zeros_like(tok), tok)
+            text = (tok.to(dev), torch.arange(args.batch, device=dev))
+        batches.append((x, y, v0, text))
 
     torch.manual_seed(0)
-    pc = EasyDict(name="SparseConvUNet", m=args.m, dimension=3, full_scale=4096, block_reps=args.reps,
-                  residual_blocks=bool(args.residual))
-    cls, _ = MODEL_REGISTRY.get("MultiLabel")
-    model = dp.wrap(cls(pc).to(dev), dev)
+    if contrastive:
+        pc = EasyDict(name="SparseConvFCNet", m=args.m, dimension=3, full_scale=4096, block_reps=args.reps,
+                      residual_blocks=bool(args.residual))
+        tc = EasyDict(name="TextTransformer", context_length=seq_len, width=512, layers=12, vocab_size=vocab)
+        cls, _ = MODEL_REGISTRY.get("MultiLabelContrastive")
+        model = dp.wrap(cls(pc, tc).to(dev), dev)
+    else:
+        pc = EasyDict(name="SparseConvUNet", m=args.m, dimension=3, full_scale=4096, block_reps=args.reps,
+                      residual_blocks=bool(args.residual))
+        cls, _ = MODEL_REGISTRY.get("MultiLabel")
+        model = dp.wrap(cls(pc).to(dev), dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     cls_loss, _ = LOSS_REGISTRY.get("Classification")
+    con_loss, _ = LOSS_REGISTRY.get("TextContrastive")
 
     def step(i):
-        x, y, _ = batches[i % len(batches)]
+        x, y, _, text = batches[i % len(batches)]
         opt.zero_grad(set_to_none=True)
-        logits, _ = model((x, None), istrain=True)
+        logits, meta = model((x, text), istrain=True)
         loss = cls_loss(logits, y)
+        if contrastive:
+            loss = loss + con_loss(*meta)
         loss.backward()
         opt.step()
         return loss
@@ -209,8 +238,18 @@ def main():
     if rank == 0:
         achieved = flops / (kms * 1e-3) / 1e12 if kms > 0 else 0.0
         traffic, traffic_src = pmc_traffic()
+        if contrastive:
+            workload = (f"MultiLabelContrastive: SparseConvFCNet m={args.m} block_reps={args.reps} scale="
+                        f"{args.scale:g} ({100 / args.scale:g} cm voxels) + TextTransformer (512 wide, 12 layers, "
+                        f"{n_text} texts x {seq_len} tokens per scene), {args.batch} scenes/GPU, Classification + "
+                        "TextContrastive, Adam step")
+        else:
+            workload = (f"SparseConvUNet m={args.m} block_reps={args.reps} residual={bool(args.residual)} "
+                        f"scale={args.scale:g} ({100 / args.scale:g} cm voxels), {args.batch} scenes/GPU, "
+                        "MultiLabel head, Adam step")
         res = {
-            "metric": "active-voxels/sec fwd+bwd, SparseConvUNet m=32 2cm voxels",
+            "metric": "active-voxels/sec fwd+bwd, SparseConvUNet m=32 2cm voxels" if not contrastive else
+                      "active-voxels/sec fwd+bwd, MultiLabelContrastive (SparseConvFCNet m=32 + TextTransformer)",
             "value": vox_all / dt_max,
             "unit": "active-voxels/s",
             "n_gpus": world,
@@ -224,9 +263,7 @@ def main():
             "data": "synthetic ScanNet-shaped procedural rooms (wsss3d/synthetic.py), trainMerge transform, "
                     "random-init weights",
             "config": {
-                "workload": f"SparseConvUNet m={args.m} block_reps={args.reps} residual={bool(args.residual)} "
-                            f"scale={args.scale:g} ({100 / args.scale:g} cm voxels), {args.batch} scenes/GPU, "
-                            "MultiLabel head, Adam step",
+                "workload": workload,
                 "scenes_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world}",
@@ -252,7 +289,7 @@ def main():
                                  "ms": v[2]} for k, v in per.items()},
             },
         }
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and not contrastive:
             res["cpu_baseline"] = cpu_baseline(args, host_batches[0])
         print(json.dumps(res), flush=True)
     if world > 1:
