@@ -160,16 +160,17 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
   struct St {
     int o, src, row;
   };
+  // Branch-free loads: chunk positions past the tile's last chunk are clamped
+  // to it (loads stay in range, the work is skipped by a uniform branch), so
+  // the compiler's wait counts stay exact and a prefetch is never waited for
+  // before it is consumed (conditional loads made it drain every load at the
+  // MFMAs).
+  const int64_t clast = ce > cb ? ce - 1 : cb;
   auto ld_idx = [&](int64_t c, St& d) {
-    if (c < ce) {
-      d.o = chunk_off[c];
-      d.src = chunk_src[c * MSP_CHUNK + r];
-      d.row = chunk_row[c * MSP_CHUNK + r];
-    } else {
-      d.o = 0;
-      d.src = -1;
-      d.row = TR;
-    }
+    const int64_t cc = c < clast ? c : clast;
+    d.o = chunk_off[cc];
+    d.src = chunk_src[cc * MSP_CHUNK + r];
+    d.row = chunk_row[cc * MSP_CHUNK + r];
   };
   auto ld_val = [&](const St& d, floatx4 (&av)[KC], floatx4 (&bv)[NT][KC]) {
     // padding slots hold a present row (see the header); their result column
@@ -184,40 +185,55 @@ __global__ __launch_bounds__(kThreads) void conv_tilep_kernel(
       for (int t = 0; t < NT; ++t) bv[t][kc] = *reinterpret_cast<const floatx4*>(wb + t * 16 * C_IN + kc * 16);
     }
   };
-  auto run = [&](const floatx4 (&av)[KC], const floatx4 (&bv)[NT][KC], int row) {
-    floatx4 acc[NT];
+  auto run = [&](const floatx4 (&av)[KC], const floatx4 (&bv)[NT][KC], int row, bool live) {
+    if (live) {
+      floatx4 acc[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
+      for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma4(bv[t][kc][s], av[kc][s], acc[t]);
-    if (row < TR) {
+          for (int t = 0; t < NT; ++t) acc[t] = mfma4(bv[t][kc][s], av[kc][s], acc[t]);
+      if (row < TR) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
+        for (int t = 0; t < NT; ++t)
+          *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
+      }
+    }
+    // mark the set read on every path (see conv_tile7_kernel)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      asm volatile("" ::"v"(av[kc]));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) asm volatile("" ::"v"(bv[t][kc]));
     }
   };
-  // Two register sets used in turn (no copies of loaded registers, which
-  // would make the wave wait for them early): while chunk c computes from one
-  // set, chunk c+1's rows and weights load into the other and chunk c+2's
-  // indices into c's index slot.
-  St iA, iB;
-  floatx4 aA[KC], bA[NT][KC], aB[KC], bB[NT][KC];
-  ld_idx(cb, iA);
-  ld_idx(cb + 1, iB);
-  if (cb < ce) ld_val(iA, aA, bA);
-  for (int64_t c = cb; c < ce; c += 2) {
-    int row = iA.row;
-    if (c + 1 < ce) ld_val(iB, aB, bB);
-    ld_idx(c + 2, iA);
-    run(aA, bA, row);
-    if (c + 1 >= ce) break;
-    row = iB.row;
-    if (c + 2 < ce) ld_val(iA, aA, bA);
-    ld_idx(c + 3, iB);
-    run(aB, bB, row);
+  // D register sets used in turn (no copies of loaded values): chunk c+k
+  // computes from set k while the other sets' loads (chunks up to c+k+D-1)
+  // are in flight; a chunk's indices are loaded D chunks before its values.
+  // Trip count a multiple of D; chunk positions past the end compute nothing.
+  constexpr int D = 2;  // 4 was measured: no gain at level 0 (35.8 vs 36.4 TF/s)
+  St J[D];
+  int rowR[D];
+  floatx4 S_a[D][KC], S_b[D][NT][KC];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    ld_idx(cb + k, J[k]);
+    rowR[k] = J[k].row;
+    ld_val(J[k], S_a[k], S_b[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) ld_idx(cb + D + k, J[k]);
+  for (int64_t c = cb; c < ce; c += D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      run(S_a[k], S_b[k], rowR[k], c + k < ce);
+      ld_val(J[k], S_a[k], S_b[k]);  // chunk c+k+D
+      rowR[k] = J[k].row;
+      ld_idx(c + k + 2 * D, J[k]);
+    }
   }
   const int64_t row0 = tile * TR;
   const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
