@@ -941,33 +941,39 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WA * W
       }
   };
 
-  // two register sets used in turn (no copies), so a set's loads are only
-  // waited for when that set is computed, one super-step later
+  // D register sets used in turn (no copies of loaded values): super-step
+  // g+k computes from set k while the loads of the next D-1 super-steps are
+  // in flight; indices are loaded D super-steps before their values.  Loads
+  // are never conditional (positions past the piece are clamped and masked
+  // by `ok`), so the compiler's wait counts stay exact.  Small dW tiles do
+  // little MFMA work per super-step and get the deeper pipeline.
+  constexpr int D = (WA * WB <= 4) ? 4 : 2;  // measured: 6 (L0) and 3 (L2) are slower
   constexpr int64_t kStride = 16 * kWaves;
-  int64_t g = p0 + 16 * wave;
-  if (g < p1) {
-    Ix ia, ib;
-    Vals va, vb;
-    ld_idx(g, ia);
-    ld_val(ia, va);
-    ld_idx(g + kStride, ib);
-    for (;;) {
-      const bool n1 = g + kStride < p1;
-      if (n1) {
-        ld_val(ib, vb);
-        ld_idx(g + 2 * kStride, ia);
+  const int64_t g0 = p0 + 16 * wave;
+  if (g0 < p1) {  // wave-uniform
+    Ix X[D];
+    Vals V[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      ld_idx(g0 + k * kStride, X[k]);
+      ld_val(X[k], V[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) ld_idx(g0 + (D + k) * kStride, X[k]);
+    for (int64_t g = g0; g < p1; g += D * kStride) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        if (g + k * kStride < p1) compute(V[k]);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {  // mark the set read on every path
+#pragma unroll
+          for (int i = 0; i < WA; ++i) asm volatile("" ::"v"(V[k].a[kk][i]));
+#pragma unroll
+          for (int t = 0; t < WB; ++t) asm volatile("" ::"v"(V[k].b[kk][t]));
+        }
+        ld_val(X[k], V[k]);
+        ld_idx(g + (2 * D + k) * kStride, X[k]);
       }
-      compute(va);
-      g += kStride;
-      if (!n1) break;
-      const bool n2 = g + kStride < p1;
-      if (n2) {
-        ld_val(ia, va);
-        ld_idx(g + 2 * kStride, ib);
-      }
-      compute(vb);
-      g += kStride;
-      if (!n2) break;
     }
   }
   // deterministic cross-wave sum: wave 0 stores, waves 1..3 add in order
