@@ -102,13 +102,13 @@ __host__ __device__ inline uint64_t hash_key(uint64_t k) {
   return k;
 }
 
-__device__ inline int32_t hash_find(const uint64_t* __restrict__ tkeys, const int32_t* __restrict__ tvals,
-                                    uint64_t mask, uint64_t key) {
+// Table slots are 16 bytes {key, value}: a probe is one load of one line.
+__device__ inline int32_t hash_find(const uint64_t* __restrict__ table, uint64_t mask, uint64_t key) {
   uint64_t h = hash_key(key) & mask;
   for (;;) {
-    const uint64_t t = tkeys[h];
-    if (t == key) return tvals[h];
-    if (t == kEmptyKey) return -1;
+    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * h);
+    if (e.x == key) return (int32_t)e.y;
+    if (e.x == kEmptyKey) return -1;
     h = (h + 1) & mask;
   }
 }

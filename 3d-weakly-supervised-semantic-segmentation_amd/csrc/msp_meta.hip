@@ -116,17 +116,16 @@ __global__ __launch_bounds__(kThreads) void seg_apply_kernel(
 
 // ---------------------------------------------------------------- hash grid
 __global__ __launch_bounds__(kThreads) void hash_build_kernel(const uint64_t* __restrict__ keys, int64_t n,
-                                                              uint64_t* __restrict__ tkeys,
-                                                              int32_t* __restrict__ tvals, uint64_t mask) {
+                                                              uint64_t* __restrict__ table, uint64_t mask) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint64_t key = keys[i];
   uint64_t h = hash_key(key) & mask;
   for (;;) {
     const unsigned long long prev =
-        atomicCAS((unsigned long long*)&tkeys[h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+        atomicCAS((unsigned long long*)&table[2 * h], (unsigned long long)kEmptyKey, (unsigned long long)key);
     if (prev == kEmptyKey) {
-      tvals[h] = (int32_t)i;
+      table[2 * h + 1] = (uint64_t)i;
       return;
     }
     h = (h + 1) & mask;
@@ -135,8 +134,7 @@ __global__ __launch_bounds__(kThreads) void hash_build_kernel(const uint64_t* __
 
 __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                             int log2s, int64_t size, int f,
-                                                            const uint64_t* __restrict__ tkeys,
-                                                            const int32_t* __restrict__ tvals, uint64_t mask,
+                                                            const uint64_t* __restrict__ table, uint64_t mask,
                                                             int32_t* __restrict__ nbr) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
@@ -154,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __re
         if (dx == 0 && dy == 0 && dz == 0) {
           v = (int32_t)i;
         } else if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size) {
-          v = hash_find(tkeys, tvals, mask, make_key(b, xx, yy, zz, log2s));
+          v = hash_find(table, mask, make_key(b, xx, yy, zz, log2s));
         }
         nbr[(int64_t)o * n + i] = v;
       }
@@ -437,22 +435,21 @@ int64_t msp_hash_capacity(int64_t n) {
   return cap;
 }
 
-int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* tkeys, int32_t* tvals, int64_t cap,
-                   msp_stream_t stream) {
+int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap, msp_stream_t stream) {
   MSP_REQUIRE(cap >= 2 * n && (cap & (cap - 1)) == 0, "msp_hash_build: capacity must be a power of 2 >= 2n");
   if (n == 0) return MSP_OK;
-  hash_build_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, tkeys, tvals, (uint64_t)(cap - 1));
+  hash_build_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, table, (uint64_t)(cap - 1));
   return check_launch("msp_hash_build");
 }
 
 int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
-                 const uint64_t* tkeys, const int32_t* tvals, int64_t cap, int32_t* nbr, msp_stream_t stream) {
+                 const uint64_t* table, int64_t cap, int32_t* nbr, msp_stream_t stream) {
   MSP_REQUIRE(filter_size >= 1 && (filter_size & 1) == 1 && filter_size <= 5,
               "msp_subm_map: filter_size must be odd and <= 5 (got %d)", filter_size);
   MSP_REQUIRE((cap & (cap - 1)) == 0, "msp_subm_map: bad capacity");
   if (n == 0) return MSP_OK;
   subm_map_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, log2_size, spatial_size, filter_size,
-                                                                tkeys, tvals, (uint64_t)(cap - 1), nbr);
+                                                                table, (uint64_t)(cap - 1), nbr);
   return check_launch("msp_subm_map");
 }
 

@@ -91,11 +91,11 @@ class SubmRules:
         K = filter_size ** 3
         self.K, self.filter_size = K, filter_size
         V = level.n
-        tkeys, tvals, cap = level.hash()
+        table, cap = level.hash()
         self.nbr = torch.empty((K, max(V, 1)), dtype=torch.int32, device=dev)
         if V:
-            call("msp_subm_map", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(tkeys), ptr(tvals),
-                 cap, ptr(self.nbr), s)
+            call("msp_subm_map", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(table), cap,
+                 ptr(self.nbr), s)
         self._tiles = {}
         self._map, self._n = self.nbr, V
         self.pairs = PairLists(self.nbr, K, V, dev, s)
@@ -140,12 +140,10 @@ class Level:
     def hash(self):
         if self._hash is None:
             cap = int(query("msp_hash_capacity", I64(self.n)))
-            tkeys = torch.full((cap,), -1, dtype=torch.int64, device=self.device)
-            tvals = torch.empty(cap, dtype=torch.int32, device=self.device)
+            table = torch.full((2 * cap,), -1, dtype=torch.int64, device=self.device)  # {key, value} slots
             if self.n:
-                call("msp_hash_build", ptr(self.keys), self.n, ptr(tkeys), ptr(tvals), cap,
-                     _lib.stream(self.device))
-            self._hash = (tkeys, tvals, cap)
+                call("msp_hash_build", ptr(self.keys), self.n, ptr(table), cap, _lib.stream(self.device))
+            self._hash = (table, cap)
         return self._hash
 
     def subm_rules(self, filter_size):

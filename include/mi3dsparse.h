@@ -78,12 +78,13 @@ int msp_segment(const uint64_t* sorted_keys, int64_t n, int shift, const int32_t
 /* ---------------- metadata: hash grid + rulebooks (replaces SCN Metadata's
  * submanifold / strided rulebooks) ----------------- */
 int64_t msp_hash_capacity(int64_t n);
-/* tkeys must be pre-filled with 0xFF bytes (empty); keys unique. */
-int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* tkeys, int32_t* tvals, int64_t cap,
-                   msp_stream_t stream);
+/* Open-addressing table of cap 16-byte slots {uint64 key, uint64 value}
+ * (table = 2*cap uint64, one probe = one load); it must be pre-filled with
+ * 0xFF bytes (empty); keys unique. */
+int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap, msp_stream_t stream);
 /* Submanifold neighbour map nbr[K][n], K = filter_size^3 (odd filter_size). */
 int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
-                 const uint64_t* tkeys, const int32_t* tvals, int64_t cap, int32_t* nbr, msp_stream_t stream);
+                 const uint64_t* table, int64_t cap, int32_t* nbr, msp_stream_t stream);
 /* Strided (size == stride == 2^log2_stride) child map: down[K][n_coarse],
  * K = 8^log2_stride, down[o][parent_of[i]] = i for every fine row i. */
 int msp_down_map(const uint64_t* fine_keys, int64_t n_fine, const int32_t* parent_of, int log2_size_fine,

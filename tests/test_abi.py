@@ -56,7 +56,7 @@ def test_queries_and_validation_without_gpu():
     assert rc == -1 and b"tile_rows" in lib.msp_last_error()
     rc = lib.msp_conv_tile(None, 3, None, 27, 0, 16, 64, None, None, None, None, 100, None, None, 0, None)
     assert rc == -1 and b"multiples of 16" in lib.msp_last_error()
-    rc = lib.msp_subm_map(None, 10, 12, 4096, 4, None, None, 1024, None, None)
+    rc = lib.msp_subm_map(None, 10, 12, 4096, 4, None, 1024, None, None)
     assert rc == -1 and b"odd" in lib.msp_last_error()
     rc = lib.msp_down_map(None, 10, None, 12, 3, None, 5, None)
     assert rc == -1
