@@ -132,31 +132,33 @@ __global__ __launch_bounds__(kThreads) void hash_build_kernel(const uint64_t* __
   }
 }
 
+// One thread per (site, offset) of the first half of the filter box plus the
+// centre: the neighbour relation is symmetric (j = nbr[o][i] <=> i =
+// nbr[K-1-o][j]), so each found pair also fills its mirror entry and only
+// half the hash probes are made.  nbr must be pre-filled with -1; every
+// entry is written at most once (no races, deterministic).
 __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                             int log2s, int64_t size, int f,
                                                             const uint64_t* __restrict__ table, uint64_t mask,
                                                             int32_t* __restrict__ nbr) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
+  const int K = f * f * f, centre = (K - 1) / 2;
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= n * (centre + 1)) return;
+  const int o = (int)(e / n);
+  const int64_t i = e - (int64_t)o * n;
+  if (o == centre) {
+    nbr[(int64_t)o * n + i] = (int32_t)i;
+    return;
+  }
   int64_t b, x, y, z;
   split_key(keys[i], log2s, b, x, y, z);
   const int h = f / 2;
-  int o = 0;
-  for (int dx = -h; dx <= h; ++dx) {
-    const int64_t xx = x + dx;
-    for (int dy = -h; dy <= h; ++dy) {
-      const int64_t yy = y + dy;
-      for (int dz = -h; dz <= h; ++dz, ++o) {
-        const int64_t zz = z + dz;
-        int32_t v = -1;
-        if (dx == 0 && dy == 0 && dz == 0) {
-          v = (int32_t)i;
-        } else if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size) {
-          v = hash_find(table, mask, make_key(b, xx, yy, zz, log2s));
-        }
-        nbr[(int64_t)o * n + i] = v;
-      }
-    }
+  const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
+  if (xx < 0 || yy < 0 || zz < 0 || xx >= size || yy >= size || zz >= size) return;
+  const int32_t j = hash_find(table, mask, make_key(b, xx, yy, zz, log2s));
+  if (j >= 0) {
+    nbr[(int64_t)o * n + i] = j;
+    nbr[(int64_t)(K - 1 - o) * n + j] = (int32_t)i;
   }
 }
 
@@ -448,8 +450,11 @@ int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial
               "msp_subm_map: filter_size must be odd and <= 5 (got %d)", filter_size);
   MSP_REQUIRE((cap & (cap - 1)) == 0, "msp_subm_map: bad capacity");
   if (n == 0) return MSP_OK;
-  subm_map_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, log2_size, spatial_size, filter_size,
-                                                                table, (uint64_t)(cap - 1), nbr);
+  hipStream_t s = as_stream(stream);
+  const int K = filter_size * filter_size * filter_size;
+  MSP_HIP(hipMemsetAsync(nbr, 0xFF, (size_t)K * n * sizeof(int32_t), s), "msp_subm_map");
+  subm_map_kernel<<<grid1(n * ((K - 1) / 2 + 1)), kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size,
+                                                                     table, (uint64_t)(cap - 1), nbr);
   return check_launch("msp_subm_map");
 }
 
