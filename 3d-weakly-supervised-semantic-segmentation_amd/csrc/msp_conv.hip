@@ -17,39 +17,12 @@
 // B[l>>4][l&15]; D[row=(l>>4)*4+j][col=l&15] in register j.  Inside a 16-wide
 // channel chunk the 4 k-steps s of lane group q cover channel 4q+s, so each
 // lane reads its A row and its B (weight) row as one float4.
-#include "msp_common.h"
+#include "msp_conv_common.h"
 
 namespace msp {
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
 __device__ inline floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-constexpr int kWaves = 4;
-constexpr int kThreads = 64 * kWaves;
-
-// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each
-// with its own L2.  Neighbouring tiles gather the same input rows, so give
-// every XCD a contiguous range of logical blocks (bijective for any count).
-__device__ inline int64_t xcd_linear(int64_t bid, int64_t nb) {
-  const int64_t q = nb >> 3, rem = nb & 7, x = bid & 7;
-  return (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + (bid >> 3);
-}
-
-// LDS tile accumulator [64 rows][NC] with the 16-byte column groups XOR-
-// swizzled by row: 16 distinct consecutive rows at one column group land on
-// 16 distinct bank quads (ds_read/write_b128 are served per 16 lanes).
-template <int NC>
-__device__ inline int acc_pos(int row, int g) {
-  constexpr int G = NC / 4;
-  if constexpr ((G & (G - 1)) == 0) {
-    constexpr int RP = NC >= 64 ? 1 : 64 / NC;
-    return row * NC + 4 * (g ^ ((row / RP) & (G - 1)));
-  } else {
-    return row * NC + 4 * ((g + row) % G);
-  }
 }
 
 // ---------------------------------------------------------------- conv_tile
@@ -778,16 +751,6 @@ __global__ __launch_bounds__(kThreads) void conv_tile7_kernel(
   }
 }
 
-// out[i] = sum over splits sp = 0, 1, ... (in order) of part[sp][i]
-__global__ __launch_bounds__(256) void split_reduce_kernel(const floatx4* __restrict__ part, int n_split, int64_t n4,
-                                                           floatx4* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n4) return;
-  floatx4 s = part[i];
-  for (int k = 1; k < n_split; ++k) s += part[(int64_t)k * n4 + i];
-  out[i] = s;
-}
-
 // Largest o with starts[o] <= v (starts non-decreasing, starts[0] = 0).
 __device__ inline int find_offset(const int64_t* __restrict__ starts, int K, int64_t v) {
   int lo = 0, hi = K;
@@ -1034,36 +997,6 @@ extern "C" {
 
 namespace {
 
-// Shared-tile plan: NT (16-channel groups per block) and the offset split.
-// NT is the largest of 4, 3, 2 dividing the output groups that still gives
-// >= 2048 blocks, else the smallest of them (more blocks); small grids split
-// each tile's offsets over up to 8 blocks (partials reduced in split order).
-struct Plan7 {
-  int nt, n_y, split;
-};
-
-Plan7 plan7(int64_t n_tiles, int c_out) {
-  const int n16 = c_out / 16;
-  Plan7 p{1, n16, 1};
-  int smallest = 0;
-  for (int nt : {2, 3, 4})
-    if (n16 % nt == 0 && !smallest) smallest = nt;
-  for (int nt : {4, 3, 2}) {
-    if (n16 % nt == 0 && n_tiles * (n16 / nt) >= 2048) {
-      p.nt = nt;
-      break;
-    }
-  }
-  if (p.nt == 1 && smallest) p.nt = smallest;
-  p.n_y = n16 / p.nt;
-  const int64_t blocks = n_tiles * p.n_y;
-  if (blocks < 1024) {
-    const int64_t sp = (1024 + blocks - 1) / blocks;
-    p.split = (int)(sp > 8 ? 8 : sp);
-  }
-  return p;
-}
-
 int launch_tile7(int nt, int tile_rows, int split, const float* x, int c_in, const float* wt, int K, int flip,
                  int c_out, const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                  const uint16_t* chunk_row, int64_t n_rows, float* out, float* part, hipStream_t s) {
@@ -1103,10 +1036,9 @@ int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out) {
   return 128;
 }
 
-size_t msp_conv_tile_workspace_size(int64_t n_rows, int c_in, int c_out, int tile_rows) {
-  if (tile_rows != 128 || n_rows <= 0 || c_out <= 0 || (c_out <= 32 && c_in <= 64)) return 0;
-  const Plan7 p = plan7(ceil_div(n_rows, tile_rows), c_out);
-  return p.split > 1 ? (size_t)p.split * (size_t)n_rows * (size_t)c_out * sizeof(float) : 0;
+size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows) {
+  if (tile_rows != 128 || n_rows <= 0 || c_out <= 0 || K <= 0 || (c_out <= 32 && c_in <= 64)) return 0;
+  return x6_ws_bytes(n_rows, K, c_in, c_out, plan_x6(n_rows, c_out, 0, 0));
 }
 
 int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
@@ -1161,11 +1093,12 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
 #undef LP
     return check_launch("msp_conv_tile");
   }
-  const Plan7 p = plan7(n_tiles, c_out);
-  const size_t need = msp_conv_tile_workspace_size(n_rows, c_in, c_out, tile_rows);
-  MSP_REQUIRE(ws_bytes >= need, "msp_conv_tile: workspace too small (%zu < %zu)", ws_bytes, need);
-  const int rc = launch_tile7(p.nt, tile_rows, p.split, x, c_in, wt, K, flip, c_out, tile_start, chunk_off,
-                              chunk_src, chunk_row, n_rows, out, static_cast<float*>(ws), s);
+  // shared 128-row tiles on bf16 MFMA with exact operand splits (msp_conv_x6.hip)
+  const PlanX6 p = plan_x6(n_rows, c_out, 0, 0);
+  const size_t need = x6_ws_bytes(n_rows, K, c_in, c_out, p);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_tile: workspace too small (%zu < %zu)", ws_bytes, need);
+  const int rc = launch_x6(p, x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows, out,
+                           ws, s);
   return rc ? rc : check_launch("msp_conv_tile");
 }
 

@@ -124,13 +124,16 @@ int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coo
  * wt[K-1-o] (submanifold backward-data with the forward weight layout).
  * c_in % 16 == 0, c_out % 16 == 0.  Every output row is written.
  * tile_rows 64: per-wave tiles; 128 / 256: one tile shared by the 4 waves of
- * a block; with 128-row tiles small grids split each tile's offsets over
- * several blocks, whose partial sums go to the workspace (ws_bytes >=
- * msp_conv_tile_workspace_size(n_rows, c_in, c_out, tile_rows)) and are
- * added in a fixed order.  msp_conv_tile_rows gives the tile height the
- * library is tuned for. */
+ * a block.  With 128-row tiles and c_out > 32 (or c_in > 64) the contraction
+ * runs on bf16 MFMA over exact three-piece bf16 splits of both fp32 operands
+ * (six piece products, fp32 accumulation: fp32-class error, checked against
+ * fp64 in tests/test_gpu_ops.py); the split weights and, on small grids, the
+ * partial sums of an offset split (added in a fixed order) live in the
+ * workspace: ws_bytes >= msp_conv_tile_workspace_size(n_rows, K, c_in,
+ * c_out, tile_rows).  msp_conv_tile_rows gives the tile height the library
+ * is tuned for. */
 int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out);
-size_t msp_conv_tile_workspace_size(int64_t n_rows, int c_in, int c_out, int tile_rows);
+size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows);
 int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                   const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,

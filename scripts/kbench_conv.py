@@ -69,7 +69,7 @@ for L, size in enumerate(sizes):
             tl = books[tr]
             out = torch.empty(V, cout, device="cuda")
             if abl is None:
-                wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(V), cin, cout, tr))
+                wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(V), 27, cin, cout, tr))
                 ws = torch.empty(max(wsb // 4, 1), device="cuda")
                 f = lambda: _lib.call("msp_conv_tile", ptr(x), cin, ptr(wt), 27, 0, cout, tr, ptr(tl["tile_start"]),
                                       ptr(tl["chunk_off"]), ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out),

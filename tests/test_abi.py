@@ -40,15 +40,17 @@ def test_prototypes_match_header():
 
 def test_queries_and_validation_without_gpu():
     lib = _lib.load()
-    assert lib.msp_abi_version() == 2
+    assert lib.msp_abi_version() == 3
     assert _lib.query("msp_hash_capacity", 1000) == 2048
     assert _lib.query("msp_hash_capacity", 10) == 1024
     assert _lib.query("msp_scan_workspace_size", 5000) > 0
     assert _lib.query("msp_bn_partials", 10 ** 7, 32) == 1024
     assert _lib.query("msp_conv_tile_rows", 10 ** 6, 32, 32) == 128
     assert _lib.query("msp_conv_tile_rows", 10 ** 6, 64, 64) == 128
-    assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 64, 64, 128) == 0  # big grid: no offset split
-    assert _lib.query("msp_conv_tile_workspace_size", 2000, 192, 192, 128) > 0  # small grid: split partials
+    # x6 form: split weights (K x 3 x c_out x c_pad bf16) + offset-split partials on small grids
+    assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 27, 64, 64, 128) == 27 * 3 * 64 * 64 * 2
+    assert _lib.query("msp_conv_tile_workspace_size", 2000, 27, 192, 192, 128) > 27 * 3 * 192 * 192 * 2
+    assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 27, 32, 32, 128) == 0  # per-wave f32 form
     # invalid arguments are rejected before any HIP call
     rc = lib.msp_conv_tile(None, 3, None, 27, 0, 16, 64, None, None, None, None, 100, None, None, 0, None)
     assert rc == -1 and b"multiples of 16" in lib.msp_last_error()

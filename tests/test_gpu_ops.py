@@ -283,3 +283,47 @@ def test_residual_block_grads(n, cin):
     pg = dict(bg.named_parameters())
     for k, p in bo.named_parameters():
         close(pg[k].grad, p.grad, 1e-4, "grad " + k)
+
+
+@pytest.mark.parametrize("cin,cout,flip", [(64, 64, 0), (96, 96, 1), (48, 96, 0), (256, 128, 0), (224, 32, 1)])
+def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
+    """msp_conv_tile on 128-row tiles runs the contraction as six bf16 MFMA
+    products of exact three-piece splits (msp_conv_x6.hip).  Its error against
+    an fp64 evaluation must be fp32-class: at most 2x that of the f32-input
+    MFMA kernel (one fmaf chain, exact fp32) on the same rulebook, and below
+    1e-6 of the output scale."""
+    import ctypes
+    from sparseconvnet import _lib, ops
+    from sparseconvnet._lib import ptr
+    torch.manual_seed(cin + cout)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    lvl = t.metadata.level(64)
+    rules = lvl.subm_rules(3)
+    V = lvl.n
+    x = torch.randn(V, cin, device=DEV)
+    wt = torch.randn(27, cout, cin, device=DEV) / (27 * cin) ** 0.5
+    y = ops.conv_tile(x, wt, 27, flip, cout, rules, V)
+    # f32-MFMA shared-tile kernel on the same rulebook (debug hook; split 1)
+    lib = _lib.load()
+    fn = lib.msp_debug_conv_tile
+    P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    fn.restype = I
+    fn.argtypes = [I, I, P, I, P, I, I, I, I, P, P, P, P, I64, P, P, P]
+    tl = rules.tiles_for(128)
+    nt = 2 if (cout // 16) % 2 == 0 else 1
+    y32 = torch.empty(V, cout, device=DEV)
+    rc = fn(81, nt, ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
+            ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(y32), None, _lib.stream(x.device))
+    assert rc == 0, lib.msp_last_error()
+    # fp64 reference from the neighbour map
+    nb = rules.nbr.long()
+    x64 = torch.cat([x.double(), torch.zeros(1, cin, dtype=torch.float64, device=DEV)])
+    w64 = wt.double().flip(0) if flip else wt.double()
+    ref = torch.zeros(V, cout, dtype=torch.float64, device=DEV)
+    for o in range(27):
+        ref += x64[torch.where(nb[o] >= 0, nb[o], V)] @ w64[o].t()
+    scale = ref.abs().max().item()
+    e_x6 = (y.double() - ref).abs().max().item() / scale
+    e_f32 = (y32.double() - ref).abs().max().item() / scale
+    assert e_x6 <= max(2.0 * e_f32, 1e-7) and e_x6 < 1e-6, (e_x6, e_f32)
