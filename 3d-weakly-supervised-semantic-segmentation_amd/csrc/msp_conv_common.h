@@ -44,9 +44,9 @@ static __global__ __launch_bounds__(256) void split_reduce_kernel(const floatx4*
 // Shared-tile convolution on bf16 MFMA with exact three-piece operand splits
 // (msp_conv_x6.hip), used by msp_conv_tile for 128-row tiles.
 struct PlanX6 {
-  int nt, ks, n_y, split, depth;
+  int nt, ks, n_y, split, depth, abl, tr, nb;  // abl: timing experiments only (msp_debug_conv_x6)
 };
-PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks);
+PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks, int tile_rows = 128);
 size_t x6_ws_bytes(int64_t n_rows, int K, int c_in, int c_out, const PlanX6& p);
 int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,

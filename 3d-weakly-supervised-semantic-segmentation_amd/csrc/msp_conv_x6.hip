@@ -14,10 +14,12 @@
 // matrix-core cycles at fp32-class accuracy (tests/test_gpu_ops.py checks the
 // error against an fp64 reference next to the f32-MFMA path's).
 //
-// Weights are split once per call into a [K][3][c_out][c_pad] bf16 image
-// (c_pad = c_in rounded up to the k-slice, zero padded) by split_weights_
-// kernel; the gathered input rows are split in registers (4.5 VALU per value:
-// v_cvt_pk_bf16_f32, shift/and back to fp32, v_pk_add_f32).
+// Weights are split once per call by split_weights_kernel into the exact
+// LDS images of the steps, [K][c_out / NC][k-slices][3][KS/8][NC] 16-byte
+// units of 8 k (XOR swizzle applied, zero padded past c_in), so a step's
+// staging is a straight coalesced copy; the gathered input rows are split in
+// registers (4.5 VALU per value: v_cvt_pk_bf16_f32, shift/and back to fp32,
+// v_pk_add_f32).
 //
 // Structure as conv_tile7 (msp_conv.hip): block = 4 waves sharing one
 // 128-row output tile accumulated in LDS, steps over (offset, KS-deep k-slice)
@@ -66,26 +68,34 @@ __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, u32x4
   }
 }
 
-// wt [rows = K*c_out][c_in] fp32 -> ws [K][3][c_out][c_pad] bf16 (16-byte
-// units of 8 k); k >= c_in is zero.  One thread per unit.
-__global__ __launch_bounds__(256) void split_weights_kernel(const float* __restrict__ wt, int64_t rows, int c_out,
-                                                            int c_in, int c_pad, u32x4* __restrict__ ws) {
-  const int upr = c_pad >> 3;
-  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (u >= rows * upr) return;
-  const int64_t row = u / upr;
-  const int k8 = (int)(u - row * upr);
-  const int64_t o = row / c_out, n = row - o * c_out;
-  u32x4 p[3];
-  if (8 * k8 < c_in) {  // c_in % 16 == 0: a unit is all data or all padding
-    const floatx4* src = reinterpret_cast<const floatx4*>(wt + row * c_in + 8 * k8);
-    split8(src[0], src[1], p);
-  } else {
-#pragma unroll
-    for (int s = 0; s < 3; ++s) p[s] = u32x4{0u, 0u, 0u, 0u};
+// wt [K][c_out][c_in] fp32 -> the per-step LDS images of conv_x6d_kernel:
+// unit u = (p * K8 + k8) * NC + n of image (o, cy, ks) holds piece p of
+// wt[o][cy * NC + n][ks * KS + 8 k8 .. + 7] (zero past c_in).  Unswizzled:
+// the staging copy is linear, and the fragment reads (lane (r, q) reads unit
+// row k8 = 4kk + q, column 16t + r) put the 16 lanes of each ds_read_b128 lane
+// group ({0-3,12-15,20-27}, ... -- MI355X_MICROARCH.md LDS table) on 16
+// distinct bank quads (r of q covers 0-3 and 12-15, r of q+1 covers 4-11).
+// One thread per unit.
+__global__ __launch_bounds__(256) void split_weights_kernel(const float* __restrict__ wt, int K, int c_out, int c_in,
+                                                            int NC, int KS, u32x4* __restrict__ img) {
+  const int K8 = KS / 8, WU = 3 * K8 * NC;
+  const int n_y = c_out / NC, nks = (c_in + KS - 1) / KS;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (int64_t)K * n_y * nks * WU) return;
+  const int u = (int)(g % WU);
+  const int64_t rest = g / WU;
+  const int ks = (int)(rest % nks);
+  const int64_t r2 = rest / nks;
+  const int cy = (int)(r2 % n_y);
+  const int64_t o = r2 / n_y;
+  const int p = u / (K8 * NC), rem = u % (K8 * NC), k8 = rem / NC, n = rem % NC;
+  const int k = ks * KS + 8 * k8;
+  u32x4 pc[3] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+  if (k < c_in) {  // c_in % 16 == 0: a unit is all data or all padding
+    const floatx4* src = reinterpret_cast<const floatx4*>(wt + ((o * c_out) + cy * NC + n) * c_in + k);
+    split8(src[0], src[1], pc);
   }
-#pragma unroll
-  for (int s = 0; s < 3; ++s) ws[((o * 3 + s) * c_out + n) * upr + k8] = p[s];
+  img[g] = p == 0 ? pc[0] : (p == 1 ? pc[1] : pc[2]);
 }
 
 // D-deep pipelined form.  A step is one (offset, KS-deep k-slice); with the
@@ -98,9 +108,13 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float* __restr
 //   weights(s+1+D) load | rows + gathers(s+D) | sources(s+2D)
 // so every load has D steps to land.  Step descriptors come from a packed
 // per-offset table in LDS (one read per step, for step s + 2D).
-template <int NT, int KS, int D, int TR>
+// ABL (timing experiments only, wrong results): bit 1 no barrier, 2 no
+// gathers, 4 no LDS accumulation, 8 no weight staging, 16 no split, 32 no MFMA.
+// NB = weight slice buffers: 2 (one barrier per step) or 1 (a second barrier
+// before the slice is overwritten; 12 KiB less LDS -> 3 blocks per CU).
+template <int NT, int KS, int D, int TR, int ABL = 0, int NB = 2>
 __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
-    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wsp, int c_pad, int K, int flip, int c_out,
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows, int n_y,
     int n_split, float* __restrict__ out) {
@@ -108,12 +122,11 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
   constexpr int NC = 16 * NT;
   constexpr int K8 = KS / 8;
   constexpr int NKK = KS / 32;
-  constexpr int SWZ = 16 / K8;
   constexpr int WU = 3 * K8 * NC;
   constexpr int SPT = (WU + kThreads - 1) / kThreads;
   constexpr int MJ = TR / (16 * kWaves);
   __shared__ floatx4 acc4[TR * NC / 4];
-  __shared__ u32x4 wbuf[2][WU];
+  __shared__ u32x4 wbuf[NB][WU];
   __shared__ unsigned long long need[2];
   __shared__ int gfirst[128];
   __shared__ int gcount[128];
@@ -220,30 +233,20 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
 #pragma unroll
     for (int j = 0; j < MJ; ++j) d.v[j] = (crow_t + chunk_idx(sd, j))[r];
   };
-  // weight staging: per-thread unit offsets are loop constants; a step adds
-  // a uniform base (offset, channel slice, k-slice)
-  const int upr = c_pad >> 3;
-  uint32_t woff[SPT];
-#pragma unroll
-  for (int i = 0; i < SPT; ++i) {
-    const int f = (tid + kThreads * i) < WU ? tid + kThreads * i : WU - 1;
-    const int k8 = f % K8, pn = f / K8, n = pn % NC, p = pn / NC;
-    woff[i] = (uint32_t)((p * c_out + n) * upr + k8);
-  }
-  const u32x4* wsp_c = wsp + (int64_t)c0 * upr;
+  // weight staging: a step's slice is one contiguous image (split_weights_
+  // kernel), copied unit for unit (coalesced loads, linear LDS stores)
+  const int n_y_w = c_out / NC;
+  const u32x4* wimg_c = wimg + (int64_t)(c0 / NC) * nks * WU;
   auto ld_w = [&](const Step& sd, WSt& w) {
     const int ow = flip ? (K - 1 - sd.o) : sd.o;
-    const u32x4* wb = wsp_c + ((int64_t)ow * 3 * c_out * upr + sd.ks * K8);
+    const u32x4* wb = wimg_c + ((int64_t)ow * n_y_w * nks + sd.ks) * WU;
 #pragma unroll
-    for (int i = 0; i < SPT; ++i) w.u[i] = wb[woff[i]];
+    for (int i = 0; i < SPT; ++i) w.u[i] = wb[(tid + kThreads * i) < WU ? tid + kThreads * i : WU - 1];
   };
   auto st_w = [&](const WSt& w, int buf) {
 #pragma unroll
-    for (int i = 0; i < SPT; ++i) {
-      const int f = tid + kThreads * i;
-      const int k8 = f % K8, pn = f / K8, n = pn % NC, p = pn / NC;
-      if (f < WU) wbuf[buf][(p * K8 + k8) * NC + (n ^ (SWZ * k8))] = w.u[i];
-    }
+    for (int i = 0; i < SPT; ++i)
+      if (tid + kThreads * i < WU) wbuf[buf][tid + kThreads * i] = w.u[i];
   };
   const char* xb = reinterpret_cast<const char*>(x);
   const uint32_t row_bytes = (uint32_t)c_in * 4u;
@@ -255,8 +258,13 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
       for (int kk = 0; kk < NKK; ++kk) {
         const int k = min(sd.ks * KS + kk * 32 + 8 * q, c_in - 8);
         const floatx4* pv = reinterpret_cast<const floatx4*>(xb + (ro + 4u * (uint32_t)k));
-        v.a[j][kk][0] = pv[0];
-        v.a[j][kk][1] = pv[1];
+        if (ABL & 2) {
+          v.a[j][kk][0] = floatx4{(float)sv.v[j], (float)k, 1.f, 2.f};
+          v.a[j][kk][1] = floatx4{(float)k, (float)sv.v[j], 3.f, 4.f};
+        } else {
+          v.a[j][kk][0] = pv[0];
+          v.a[j][kk][1] = pv[1];
+        }
       }
     }
   };
@@ -275,17 +283,28 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
         u32x4 xp[MJ][3];
 #pragma unroll
         for (int j = 0; j < MJ; ++j)
-          if (j < sd.gn) split8(v.a[j][kk][0], v.a[j][kk][1], xp[j]);
+          if (j < sd.gn) {
+            if (ABL & 16) {
+#pragma unroll
+              for (int pp = 0; pp < 3; ++pp)
+                xp[j][pp] = u32x4{__float_as_uint(v.a[j][kk][0][pp]), __float_as_uint(v.a[j][kk][0][pp + 1]),
+                                  __float_as_uint(v.a[j][kk][1][pp]), __float_as_uint(v.a[j][kk][1][pp + 1])};
+            } else {
+              split8(v.a[j][kk][0], v.a[j][kk][1], xp[j]);
+            }
+          }
         const int k8 = kk * 4 + q;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const int un = (16 * t + r) ^ (SWZ * k8);
+          const int un = 16 * t + r;
           const u32x4 w0 = wb[(0 * K8 + k8) * NC + un];
           const u32x4 w1 = wb[(1 * K8 + k8) * NC + un];
           const u32x4 w2 = wb[(2 * K8 + k8) * NC + un];
 #pragma unroll
           for (int j = 0; j < MJ; ++j) {
-            if (j < sd.gn) {
+            if (j < sd.gn && (ABL & 32)) {
+              acc[j][t] += __builtin_bit_cast(floatx4, w0 ^ w1 ^ w2 ^ xp[j][0] ^ xp[j][1] ^ xp[j][2]);
+            } else if (j < sd.gn) {
               floatx4 a = acc[j][t];
               a = mfma_bf16(w2, xp[j][0], a);
               a = mfma_bf16(w1, xp[j][1], a);
@@ -349,13 +368,25 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
     for (int k = 0; k < D; ++k) {
       const int s = base + k;
       const int k1 = (k + 1) % D;
-      __syncthreads();  // wbuf[s & 1] holds step s's slice; step s-1's LDS updates are done
-      mma(Vd[k], s & 1, V[k]);
+      if (!(ABL & 1)) __syncthreads();  // wbuf[s & 1] holds step s's slice; step s-1's LDS updates are done
+      mma(Vd[k], (s & 1) % NB, V[k]);
       consume_val(V[k]);
-      rmw(Vd[k], R[k]);
+      if (!(ABL & 4)) {
+        rmw(Vd[k], R[k]);
+      } else if (Vd[k].gn > 0) {
+        floatx4 z = acc[0][0];
+#pragma unroll
+        for (int j = 0; j < MJ; ++j)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) z += acc[j][t];
+        acc4[lane] += z;
+      }
       consume_row(R[k]);
-      st_w(Wr[k1], (s + 1) & 1);  // step s+1's slice (loaded D steps ago)
-      ld_w(Sd[k1], Wr[k1]);       // step s+1+D
+      if (!(ABL & 8)) {
+        if (NB == 1) __syncthreads();  // every wave is done with step s's slice
+        st_w(Wr[k1], ((s + 1) & 1) % NB);  // step s+1's slice (loaded D steps ago)
+        ld_w(Sd[k1], Wr[k1]);       // step s+1+D
+      }
       Vd[k] = Sd[k];
       ld_row(Vd[k], R[k]);  // step s+D
       gather(Vd[k], S[k], V[k]);
@@ -380,27 +411,34 @@ using namespace msp;
 
 namespace msp {
 
-// NT: the widest of 4, 3, 2 dividing the 16-channel output groups (most
-// reuse of each gathered and split input row); k-slice 32 for NT = 4 (LDS:
-// a 32 KiB accumulator + 2 x 24 KiB weight slices at 64 would not leave room
-// for two blocks per CU), 64 otherwise.  Small grids split each tile's
-// offsets over up to 8 blocks (partials reduced in split order).  Measured
-// on the headline batch (scripts/kbench_x6.py): pipeline depth 2 is as fast
-// as 3 or 4.
-PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks) {
+// Plan (measured on the headline batch's rulebooks, scripts/kbench_x6.py,
+// profiles/r01/kbench_x6_*.log): 32-deep k-slices everywhere (fewer
+// registers per pipeline slot -> 3 waves per SIMD); NT = 4 output groups per
+// block with a single weight buffer (46 KiB of LDS -> 3 blocks per CU) when
+// the grid has >= 256 tile x slice blocks, else NT = 3, 4, 2, 1 (first that
+// divides) with double-buffered weights.  Small grids split each tile's
+// offsets over up to 8 blocks (partials reduced in split order).  Pipeline
+// depth 2 (3 and 4 measured no faster).
+PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks, int tile_rows) {
   const int n16 = c_out / 16;
-  PlanX6 p{1, 64, 1, 1, 2};  // NT = 1 when no wider group count divides (5, 7, ... groups)
-  for (int nt : {4, 3, 2}) {
-    if (n16 % nt == 0) {
-      p.nt = nt;
-      break;
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
+  PlanX6 p{1, 32, 1, 1, 2, 0, tile_rows, 2};
+  if (n16 % 4 == 0 && n_tiles * (n16 / 4) >= 256) {
+    p.nt = 4;
+    p.nb = 1;
+  } else {
+    for (int nt : {3, 4, 2}) {
+      if (n16 % nt == 0) {
+        p.nt = nt;
+        break;
+      }
     }
   }
   if (force_nt > 0) p.nt = force_nt;
-  p.ks = p.nt == 4 ? 32 : 64;
   if (force_ks > 0) p.ks = force_ks;
+  if (p.nt != 4) p.nb = 2;
   p.n_y = n16 / p.nt;
-  const int64_t blocks = ceil_div(n_rows, 128) * p.n_y;
+  const int64_t blocks = n_tiles * p.n_y;
   if (blocks < 1024) {
     const int64_t sp = (1024 + blocks - 1) / blocks;
     p.split = (int)(sp > 8 ? 8 : sp);
@@ -425,24 +463,35 @@ size_t x6_ws_bytes(int64_t n_rows, int K, int c_in, int c_out, const PlanX6& p) 
 int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s) {
-  const int64_t n_tiles = ceil_div(n_rows, 128);
-  const int c_pad = (int)(ceil_div(c_in, p.ks) * p.ks);
+  const int64_t n_tiles = ceil_div(n_rows, p.tr);
   u32x4* wsp = static_cast<u32x4*>(ws);
-  const int64_t units = (int64_t)K * c_out * (c_pad / 8);
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, (int64_t)K * c_out, c_out, c_in, c_pad,
-                                                                      wsp);
+  const int64_t units = (int64_t)x6_weight_bytes(K, c_in, c_out, p.ks) / 16;
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * p.nt, p.ks, wsp);
   float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + round256(x6_weight_bytes(K, c_in, c_out, p.ks)));
   float* dst = p.split > 1 ? part : out;
   const unsigned grid = (unsigned)(n_tiles * p.n_y * p.split);
   bool launched = false;
-#define LD(N, S, DD)                                                                                          \
-  if (!launched && p.nt == N && p.ks == S && p.depth == DD) {                                                 \
-    conv_x6d_kernel<N, S, DD, 128><<<grid, kThreads, 0, s>>>(x, c_in, wsp, c_pad, K, flip, c_out, tile_start, \
-                                                             chunk_off, chunk_src, chunk_row, n_rows, p.n_y,  \
-                                                             p.split, dst);                                   \
+#define LD(N, S, DD, B)                                                                                       \
+  if (!launched && p.nt == N && p.ks == S && p.depth == DD && p.nb == B && !p.abl && p.tr == 128) {          \
+    conv_x6d_kernel<N, S, DD, 128, 0, B><<<grid, kThreads, 0, s>>>(x, c_in, wsp, K, flip, c_out, tile_start,  \
+                                                                   chunk_off, chunk_src, chunk_row, n_rows,  \
+                                                                   p.n_y, p.split, dst);                     \
     launched = true;                                                                                          \
   }
-  LD(1, 64, 2) LD(2, 64, 2) LD(3, 64, 2) LD(4, 32, 2) LD(4, 32, 3) LD(3, 64, 3) LD(2, 64, 3)
+#define LA(A)                                                                                                 \
+  if (!launched && p.nt == 4 && p.ks == 32 && p.depth == 2 && p.abl == A) {                                  \
+    conv_x6d_kernel<4, 32, 2, 128, A><<<grid, kThreads, 0, s>>>(x, c_in, wsp, K, flip, c_out, tile_start,    \
+                                                                chunk_off, chunk_src, chunk_row, n_rows,     \
+                                                                p.n_y, p.split, dst);                        \
+    launched = true;                                                                                          \
+  }
+  if (p.abl) {
+    LA(1) LA(2) LA(4) LA(8) LA(16) LA(32) LA(48) LA(63)
+  }
+#undef LA
+  // production (plan_x6) and the variants scripts/kbench_x6.py compares
+  LD(4, 32, 2, 1) LD(4, 32, 2, 2) LD(3, 32, 2, 2) LD(2, 32, 2, 2) LD(1, 32, 2, 2)
+  LD(3, 64, 2, 2) LD(2, 64, 2, 2) LD(4, 32, 3, 1)
 #undef LD
   if (!launched) {
     set_error("msp_conv_tile: no x6 kernel for nt=%d ks=%d depth=%d", p.nt, p.ks, p.depth);
@@ -463,12 +512,17 @@ extern "C" {
 // Experiment hook (not part of the public ABI; scripts/kbench_conv.py): the
 // x6 shared-tile form with NT / KS forced (0 = the plan's choice).  With
 // ws == nullptr returns the workspace bytes needed.
-int64_t msp_debug_conv_x6(int nt, int ks, int depth, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+int64_t msp_debug_conv_x6(int nt, int ks, int depth, int abl, int tile_rows, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
                           const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                           const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
                           msp_stream_t stream) {
-  PlanX6 p = plan_x6(n_rows, c_out, nt, ks);
+  PlanX6 p = plan_x6(n_rows, c_out, nt, ks, tile_rows > 0 ? tile_rows : 128);
   if (depth > 0) p.depth = depth;
+  if (abl >= 256) {  // 256 + nb: weight buffer count forced
+    p.nb = abl - 256;
+  } else {
+    p.abl = abl;
+  }
   MSP_REQUIRE((c_out / 16) % p.nt == 0, "msp_debug_conv_x6: nt %d does not divide c_out/16", p.nt);
   const size_t need = x6_ws_bytes(n_rows, K, c_in, c_out, p);
   if (!ws) return (int64_t)need;

@@ -16,17 +16,19 @@ lib = _lib.load()
 P, I, I64, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
 fx6 = lib.msp_debug_conv_x6
 fx6.restype = I64
-fx6.argtypes = [I, I, I, P, I, P, I, I, I, P, P, P, P, I64, P, P, SZ, P]
+fx6.argtypes = [I, I, I, I, I, P, I, P, I, I, I, P, P, P, P, I64, P, P, SZ, P]
 b = make_batch(8, 50, seed=1)
 t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
 meta = t.metadata
 n_lv = int(os.environ.get("LEVELS", "7"))
+first = int(os.environ.get("FIRST_LEVEL", "0"))
 sizes = [4096 >> i for i in range(n_lv)]
 for s_ in sizes[:-1]:
     meta.downsample(s_, 2)
 s = _lib.stream()
-X6 = [tuple(int(v) for v in e.split(":")) for e in
-      os.environ.get("X6", "0:0:1,4:32:2,4:32:3,4:32:4,3:64:2,2:64:2,2:64:3").split(",")]
+# nt:ks:depth[:abl[:tile_rows]]  (abl: msp_conv_x6.hip ablation bits, timing only)
+X6 = [tuple([int(v) for v in e.split(":")] + [0, 0, 0, 0, 128][len(e.split(":")):]) for e in
+      os.environ.get("X6", "0:0:0,4:32:2,4:32:3,3:64:2,2:64:2").split(",")]
 NSUB = 4096
 
 
@@ -44,16 +46,18 @@ def timeit(f, n=10):
 
 
 for L, size in enumerate(sizes):
+    if L < first:
+        continue
     lvl = meta.level(size)
     rules = lvl.subm_rules(3)
     V = lvl.n
-    c = 32 * (L + 1)
+    c = int(os.environ.get("M", "32")) * (L + 1)
     tl = metadata.tile_rulebook(rules.nbr, 27, V, "cuda", s, tile_rows=128)
     print(f"L{L} V={V} R={rules.n_rules}", flush=True)
     rows = torch.arange(min(NSUB, V), device="cuda")
     nb = rules.nbr[:, :len(rows)].long()  # [27][n]
     for cin, cout in ((c, c), (2 * c, c)):
-        if cout <= 32 and cin <= 64:
+        if cout <= 32 and cin <= 64 and not os.environ.get("NARROW"):
             continue  # per-wave f32 form territory
         torch.manual_seed(L)
         x = torch.randn(V, cin, device="cuda")
@@ -74,17 +78,18 @@ for L, size in enumerate(sizes):
         prod = out.clone()
         err = (out[:len(rows)].double() - ref).abs().max().item() / scale
         print(f"   {cin:3d}->{cout:3d} f32 tile7      {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF  err {err:.2e}", flush=True)
-        for nt, ks, dp in X6:
+        for nt, ks, dp, abl, trx in X6:
             if nt and (cout // 16) % nt:
                 continue
-            args = [nt, ks, dp, ptr(x), cin, ptr(wt), 27, 0, cout, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
-                    ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), None, 0, s]
+            tlx = tl if trx == 128 else metadata.tile_rulebook(rules.nbr, 27, V, "cuda", s, tile_rows=trx)
+            args = [nt, ks, dp, abl, trx, ptr(x), cin, ptr(wt), 27, 0, cout, ptr(tlx["tile_start"]), ptr(tlx["chunk_off"]),
+                    ptr(tlx["chunk_src"]), ptr(tlx["chunk_row"]), V, ptr(out), None, 0, s]
             need = fx6(*args)
             if need < 0:
                 print(f"   {cin}->{cout} x6 nt{nt} ks{ks} d{dp}: {lib.msp_last_error()}")
                 continue
             wsx = torch.empty(need // 4 + 1, device="cuda")
-            args[15], args[16] = ptr(wsx), int(need)
+            args[17], args[18] = ptr(wsx), int(need)
 
             def fx(args=args):
                 rc = fx6(*args)
@@ -93,5 +98,5 @@ for L, size in enumerate(sizes):
             ms = timeit(fx)
             err = (out[:len(rows)].double() - ref).abs().max().item() / scale
             dprod = ((out - prod).abs().max() / prod.abs().max()).item()
-            print(f"   {cin:3d}->{cout:3d} x6 nt{nt} ks{ks:2d} d{dp} {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF  err {err:.2e}"
+            print(f"   {cin:3d}->{cout:3d} x6 nt{nt} ks{ks:2d} d{dp} a{abl:2d} t{trx} {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF  err {err:.2e}"
                   f"  vs f32 {dprod:.1e}", flush=True)
