@@ -818,21 +818,6 @@ __global__ __launch_bounds__(kThreads) void conv_pairs_kernel(
 // Indices run two 16-pair super-steps ahead, values one.  Waves take
 // super-steps round-robin;
 // their tiles are summed in fixed order into the block's slab (deterministic).
-template <int W>
-__device__ inline void load_vec(const float* p, float (&v)[W]) {
-  if (W == 4) {
-    const floatx4 t = *reinterpret_cast<const floatx4*>(p);
-#pragma unroll
-    for (int i = 0; i < W; ++i) v[i] = t[i];
-  } else if (W == 2) {
-    const float2 t = *reinterpret_cast<const float2*>(p);
-    v[0] = t.x;
-    v[W - 1] = t.y;
-  } else {
-#pragma unroll
-    for (int i = 0; i < W; ++i) v[i] = p[i];
-  }
-}
 
 template <int WA, int WB>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WA * WB > 9 ? 2 : 3))) void conv_wgrad4_kernel(
@@ -1189,13 +1174,23 @@ int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, 
   return check_launch("msp_conv_pairs");
 }
 
+// Experiment hook (not part of the public ABI): 1 = weight gradients on the
+// f32-MFMA kernel (conv_wgrad4_kernel) instead of the x6 one; the piece count
+// stays the x6 plan's (callers size the slab from msp_wgrad_pieces).
+static int g_wgrad_f32 = 0;
+int msp_debug_wgrad_f32(int on) {
+  g_wgrad_f32 = on;
+  return MSP_OK;
+}
+
 int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out) {
   // about 4096 blocks per launch (pieces x offsets x dW tiles), at least 256
   // pairs per piece; one-offset contractions (network-in-network weight
   // gradients) at most 768 pieces (fewer partial tiles to reduce)
   if (K < 1 || c_in < 16 || c_out < 16) return 1;
-  auto pick = [](int n16) { return n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1)); };
-  const int64_t n_ty = (int64_t)(c_in / (16 * pick(c_in / 16))) * (c_out / (16 * pick(c_out / 16)));
+  int wa, wb;
+  wgrad_x6_tile(c_in, c_out, wa, wb);
+  const int64_t n_ty = (int64_t)(c_in / (16 * wa)) * (c_out / (16 * wb));
   int64_t n = total_pairs / ((int64_t)K * 256);
   const int64_t by_grid = 4096 / ((int64_t)K * n_ty);
   if (n > by_grid) n = by_grid;
@@ -1210,8 +1205,16 @@ int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const i
               "msp_conv_wgrad: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && n_pieces >= 1, "msp_conv_wgrad: K=%d n_pieces=%lld", K, (long long)n_pieces);
   hipStream_t s = as_stream(stream);
-  // dW tiles of up to 64 x 64 per block: the largest divisor <= 4 of the
-  // 16-channel group counts
+  const int64_t cc = (int64_t)c_in * c_out;
+  dim3 g2((unsigned)ceil_div(cc, 64), (unsigned)K);
+  if (!g_wgrad_f32) {  // bf16 MFMA on exact operand splits (msp_conv_x6.hip)
+    MSP_REQUIRE(launch_wgrad_x6(x, c_in, dy, c_out, pair_in, pair_out, off_start, K, n_pieces, slab, s) == MSP_OK,
+                "msp_conv_wgrad: no x6 kernel for c_in=%d c_out=%d", c_in, c_out);
+    wgrad_reduce_kernel<<<g2, 256, 0, s>>>(slab, n_pieces, K, cc, dw);
+    return check_launch("msp_conv_wgrad");
+  }
+  // f32-MFMA form (msp_debug_wgrad_f32): dW tiles of up to 64 x 64 per
+  // block, the largest divisor <= 4 of the 16-channel group counts
   auto pick = [](int n16) { return n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1)); };
   const int WA = pick(c_in / 16), WB = pick(c_out / 16);
   const int n_ty = (c_in / (16 * WA)) * (c_out / (16 * WB));
@@ -1224,8 +1227,6 @@ int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const i
   LAUNCH_ROW(1) LAUNCH_ROW(2) LAUNCH_ROW(3) LAUNCH_ROW(4)
 #undef LAUNCH_ROW
 #undef LAUNCH
-  const int64_t cc = (int64_t)c_in * c_out;
-  dim3 g2((unsigned)ceil_div(cc, 64), (unsigned)K);
   wgrad_reduce_kernel<<<g2, 256, 0, s>>>(slab, n_pieces, K, cc, dw);
   return check_launch("msp_conv_wgrad");
 }

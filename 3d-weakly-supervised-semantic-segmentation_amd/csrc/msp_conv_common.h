@@ -31,6 +31,23 @@ __device__ inline int acc_pos(int row, int g) {
   }
 }
 
+// W consecutive floats (W = 4: one 16-byte load, 2: 8-byte, else scalar)
+template <int W>
+__device__ inline void load_vec(const float* p, float (&v)[W]) {
+  if (W == 4) {
+    const floatx4 t = *reinterpret_cast<const floatx4*>(p);
+#pragma unroll
+    for (int i = 0; i < W; ++i) v[i] = t[i];
+  } else if (W == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x;
+    v[W - 1] = t.y;
+  } else {
+#pragma unroll
+    for (int i = 0; i < W; ++i) v[i] = p[i];
+  }
+}
+
 // out[i] = sum over splits sp = 0, 1, ... (in order) of part[sp][i]
 static __global__ __launch_bounds__(256) void split_reduce_kernel(const floatx4* __restrict__ part, int n_split,
                                                                   int64_t n4, floatx4* __restrict__ out) {
@@ -51,5 +68,11 @@ size_t x6_ws_bytes(int64_t n_rows, int K, int c_in, int c_out, const PlanX6& p);
 int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s);
+
+// bf16-split weight gradient (msp_conv_x6.hip), used by msp_conv_wgrad.
+int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
+                    const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
+                    hipStream_t s);
+void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb);
 
 }  // namespace msp

@@ -405,6 +405,185 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------- weight gradient
+// dW[o] = sum over the pairs (i, j) of offset o of x[i]^T dy[j], on bf16 MFMA
+// over exact three-piece splits of both operands (six products per fp32
+// multiply-add, as the convolution above).  Block = piece of one offset's
+// pair list and one (16 WA x 16 WB) dW tile, as conv_wgrad4_kernel
+// (msp_conv.hip), whose slab and reduction it shares.  MFMA k = 32 pairs:
+// lane (r, q) takes pairs 8q .. 8q+7 of a super-step and loads WA
+// consecutive input channels m0 + WA r .. and WB output channels n0 + WB r ..
+// of each (16 lanes read 16 WA contiguous floats of one row), so component
+// sa of its 8 x vectors is the lane's A fragment for channel m0 + WA r + sa
+// and component sb of its dy vectors its B fragment: accumulator (sa, sb)
+// register j holds dW[m0 + WA (4q + j) + sa][n0 + WB r + sb].  Waves take
+// super-steps round-robin, two register sets deep; positions past the piece
+// are clamped to its last pair and their x values zeroed (uniform branch:
+// only the last super-step of a wave in a piece can be partial).
+template <int WA, int WB>
+__global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
+    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
+    int K, int64_t n_pieces, int n_ty, float* __restrict__ slab) {
+  constexpr int TM = 16 * WA, TN = 16 * WB;
+  constexpr int D = 2;
+  __shared__ float red[TM * TN];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t b = lb / n_ty;
+  const int ty = (int)(lb % n_ty);
+  const int n_tj = c_out / TN;
+  const int m0 = (ty / n_tj) * TM, n0 = (ty % n_tj) * TN;
+  const int o = (int)(b % K);
+  const int64_t j = b / K;
+  const int64_t os = off_start[o], cnt = off_start[o + 1] - os;
+  const int64_t p0 = os + cnt * j / n_pieces;
+  const int64_t p1 = os + cnt * (j + 1) / n_pieces;
+
+  floatx4 acc[WA][WB];
+#pragma unroll
+  for (int i = 0; i < WA; ++i)
+#pragma unroll
+    for (int t = 0; t < WB; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  struct Ix {
+    int32_t i[8], o[8];
+  };
+  struct Vals {
+    float a[8][WA], b[8][WB];
+  };
+  auto ld_idx = [&](int64_t g, Ix& d) {
+    const int64_t pp = g + 8 * q;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t pc = min(pp + k, p1 - 1);
+      d.i[k] = pin[pc];
+      d.o[k] = pout[pc];
+    }
+  };
+  const float* xm = x + m0 + WA * r;
+  const float* dyn = dy + n0 + WB * r;
+  auto ld_val = [&](const Ix& d, Vals& v) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      load_vec<WA>(xm + (int64_t)d.i[k] * c_in, v.a[k]);
+      load_vec<WB>(dyn + (int64_t)d.o[k] * c_out, v.b[k]);
+    }
+  };
+  auto compute = [&](int64_t g, const Vals& v) {
+    float a[8][WA];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int i = 0; i < WA; ++i) a[k][i] = v.a[k][i];
+    if (g + 32 > p1) {  // uniform: partial super-step, zero the x values of pairs past the piece
+      const int64_t pp = g + 8 * q;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int i = 0; i < WA; ++i) a[k][i] = pp + k < p1 ? a[k][i] : 0.f;
+    }
+    u32x4 bp[WB][3];
+#pragma unroll
+    for (int t = 0; t < WB; ++t)
+      split8(floatx4{v.b[0][t], v.b[1][t], v.b[2][t], v.b[3][t]},
+             floatx4{v.b[4][t], v.b[5][t], v.b[6][t], v.b[7][t]}, bp[t]);
+#pragma unroll
+    for (int i = 0; i < WA; ++i) {
+      u32x4 ap[3];
+      split8(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]}, ap);
+#pragma unroll
+      for (int t = 0; t < WB; ++t) {
+        floatx4 c = acc[i][t];
+        c = mfma_bf16(ap[2], bp[t][0], c);
+        c = mfma_bf16(ap[1], bp[t][1], c);
+        c = mfma_bf16(ap[0], bp[t][2], c);
+        c = mfma_bf16(ap[1], bp[t][0], c);
+        c = mfma_bf16(ap[0], bp[t][1], c);
+        acc[i][t] = mfma_bf16(ap[0], bp[t][0], c);
+      }
+    }
+  };
+  constexpr int64_t kStride = 32 * kWaves;
+  const int64_t g0 = p0 + 32 * wave;
+  if (g0 < p1) {  // wave-uniform
+    Ix X[D];
+    Vals V[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      ld_idx(g0 + k * kStride, X[k]);
+      ld_val(X[k], V[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) ld_idx(g0 + (D + k) * kStride, X[k]);
+    for (int64_t g = g0; g < p1; g += D * kStride) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        if (g + k * kStride < p1) compute(g + k * kStride, V[k]);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {  // mark the set read on every path
+#pragma unroll
+          for (int i = 0; i < WA; ++i) asm volatile("" ::"v"(V[k].a[kk][i]));
+#pragma unroll
+          for (int t = 0; t < WB; ++t) asm volatile("" ::"v"(V[k].b[kk][t]));
+        }
+        ld_val(X[k], V[k]);
+        ld_idx(g + (2 * D + k) * kStride, X[k]);
+      }
+    }
+  }
+  // deterministic cross-wave sum: wave 0 stores, waves 1..3 add in order
+  for (int w = 0; w < kWaves; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < WA; ++i)
+#pragma unroll
+        for (int t = 0; t < WB; ++t)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            float* d = red + (WA * (4 * q + jj) + i) * TN + WB * r + t;
+            *d = (w == 0) ? acc[i][t][jj] : (*d + acc[i][t][jj]);
+          }
+    }
+    __syncthreads();
+  }
+  float* sb = slab + b * (int64_t)c_in * c_out;
+  for (int e = threadIdx.x; e < TM * TN; e += kThreads) {
+    const int i = e / TN, jn = e % TN;
+    sb[(int64_t)(m0 + i) * c_out + n0 + jn] = red[e];
+  }
+}
+
+// dW tile of the x6 weight gradient: WA in {4, 3, 2, 1} (largest dividing
+// c_in / 16), WB in {2, 1} (registers: two value sets of 8 pairs each).
+void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb) {
+  const int a = c_in / 16, bb = c_out / 16;
+  wa = a % 4 == 0 ? 4 : (a % 3 == 0 ? 3 : (a % 2 == 0 ? 2 : 1));
+  wb = bb % 2 == 0 ? 2 : 1;
+}
+
+int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
+                    const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
+                    hipStream_t s) {
+  int WA, WB;
+  wgrad_x6_tile(c_in, c_out, WA, WB);
+  const int n_ty = (c_in / (16 * WA)) * (c_out / (16 * WB));
+  const unsigned grid = (unsigned)(n_pieces * K * n_ty);
+  bool launched = false;
+#define LW(A, B)                                                                                          \
+  if (!launched && WA == A && WB == B) {                                                                  \
+    wgrad_x6_kernel<A, B><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, K, \
+                                                    n_pieces, n_ty, slab);                               \
+    launched = true;                                                                                      \
+  }
+  LW(1, 1) LW(2, 1) LW(3, 1) LW(4, 1) LW(1, 2) LW(2, 2) LW(3, 2) LW(4, 2)
+#undef LW
+  return launched ? MSP_OK : MSP_EINVAL;
+}
+
+
 }  // namespace msp
 
 using namespace msp;

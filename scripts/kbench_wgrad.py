@@ -1,5 +1,6 @@
 """Micro-benchmark of msp_conv_wgrad on the headline batch's real submanifold
-pair lists (levels 0-2), checked against a torch fp64 reference."""
+pair lists (levels 0-3, c -> c and 2c -> c), x6 (bf16 split) form against the
+f32-MFMA form (msp_debug_wgrad_f32), each checked against torch fp64."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
 import __graft_entry__ as g; g.add_path()
@@ -13,11 +14,15 @@ meta = t.metadata
 sizes = [4096, 2048, 1024, 512]
 for s_ in sizes[:-1]:
     meta.downsample(s_, 2)
-for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 128])):
+lib = _lib.load()
+cases = [(L, size, ci, c) for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 128])) for ci in (c, 2 * c)]
+for (L, size, ci, c), mode in [(cs, m) for cs in cases for m in (0, 1)]:
+    lib.msp_debug_wgrad_f32(mode)
     rules = meta.level(size).subm_rules(3)
     p = rules.pairs
     V = meta.level(size).n
-    x = torch.randn(V, c, device="cuda")
+    torch.manual_seed(L)
+    x = torch.randn(V, ci, device="cuda")
     dy = torch.randn(V, c, device="cuda")
     for _ in range(2):
         dw = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
@@ -36,6 +41,7 @@ for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 128])):
         s0, s1 = offs[o], offs[o + 1]
         ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
         err = max(err, ((dw[o].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
-    flops = 2.0 * rules.n_rules * c * c
-    print(f"L{L} V={V} R={rules.n_rules} pieces={_lib.query('msp_wgrad_pieces', _lib.I64(p.total), 27, c, c)}: {ms:.3f} ms "
+    flops = 2.0 * rules.n_rules * ci * c
+    print(f"L{L} {ci:3d}->{c:3d} {'f32' if mode else 'x6 '} V={V} R={rules.n_rules} "
+          f"pieces={_lib.query('msp_wgrad_pieces', _lib.I64(p.total), 27, ci, c)}: {ms:.3f} ms "
           f"{flops / ms / 1e9:.1f} TF  max rel err {err:.2e}", flush=True)
