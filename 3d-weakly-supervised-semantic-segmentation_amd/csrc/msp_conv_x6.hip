@@ -670,7 +670,7 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
 #undef LA
   // production (plan_x6) and the variants scripts/kbench_x6.py compares
   LD(4, 32, 2, 1) LD(4, 32, 2, 2) LD(3, 32, 2, 2) LD(2, 32, 2, 2) LD(1, 32, 2, 2)
-  LD(3, 64, 2, 2) LD(2, 64, 2, 2) LD(4, 32, 3, 1)
+  LD(3, 64, 2, 2) LD(2, 64, 2, 2) LD(4, 32, 3, 1) LD(4, 64, 2, 1) LD(3, 64, 2, 1) LD(3, 32, 2, 1)
 #undef LD
   if (!launched) {
     set_error("msp_conv_tile: no x6 kernel for nt=%d ks=%d depth=%d", p.nt, p.ks, p.depth);
