@@ -1022,7 +1022,8 @@ int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out) {
 }
 
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows) {
-  if (tile_rows != 128 || n_rows <= 0 || c_out <= 0 || K <= 0 || (c_out <= 32 && c_in <= 64)) return 0;
+  if (tile_rows != 128 || n_rows <= 0 || c_out <= 0 || K <= 0) return 0;
+  if (c_out <= 32 && c_in <= 64) return x6p_ws_bytes(K, c_in, c_out);
   return x6_ws_bytes(n_rows, K, c_in, c_out, plan_x6(n_rows, c_out, 0, 0));
 }
 
@@ -1067,16 +1068,12 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
     return rc ? rc : check_launch("msp_conv_tile");
   }
   if (c_out <= 32 && c_in <= 64) {
-    // narrow outputs: pipelined per-wave form, one 128-row tile per wave, no barriers
-    const int NT = c_out / 16;
-    const unsigned grid = (unsigned)ceil_div(n_tiles, kWaves);
-#define LP(N, C)                                                                                              \
-  if (NT == N && c_in == 16 * C)                                                                              \
-    conv_tilep_kernel<N, C, 128><<<grid, kThreads, 0, s>>>(x, wt, K, flip, c_out, tile_start, chunk_off,     \
-                                                           chunk_src, chunk_row, n_rows, n_tiles, 1, out);
-    LP(1, 1) LP(1, 2) LP(1, 3) LP(1, 4) LP(2, 1) LP(2, 2) LP(2, 3) LP(2, 4)
-#undef LP
-    return check_launch("msp_conv_tile");
+    // narrow outputs: per-wave 128-row tiles, no barriers (msp_conv_x6.hip)
+    const size_t need = x6p_ws_bytes(K, c_in, c_out);
+    MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_tile: workspace too small (%zu < %zu)", ws_bytes, need);
+    const int rc = launch_x6p(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows,
+                              out, ws, s);
+    return rc ? rc : check_launch("msp_conv_tile");
   }
   // shared 128-row tiles on bf16 MFMA with exact operand splits (msp_conv_x6.hip)
   const PlanX6 p = plan_x6(n_rows, c_out, 0, 0);

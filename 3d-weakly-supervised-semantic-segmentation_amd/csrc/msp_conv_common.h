@@ -69,6 +69,12 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s);
 
+// Per-wave split-bf16 form for narrow outputs (c_out <= 32, c_in <= 64).
+int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
+               const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
+               float* out, void* ws, hipStream_t s);
+size_t x6p_ws_bytes(int K, int c_in, int c_out);
+
 // bf16-split weight gradient (msp_conv_x6.hip), used by msp_conv_wgrad.
 int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
                     const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,

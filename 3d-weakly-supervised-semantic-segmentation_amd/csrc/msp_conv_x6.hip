@@ -406,6 +406,166 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
 }
 
 
+// ---------------------------------------------------------------- per-wave tiles
+// Narrow outputs (c_out <= 32, level 0 of m=32 nets): one wave owns one
+// 128-row output tile and all 16 NT output channels, no block barrier (the
+// f32 conv_tilep_kernel structure, msp_conv.hip).  With few chunks per offset
+// and tile there is nothing to share between waves; the f32 form was bound
+// by the f32 MFMA dependency chain (SQ_WAIT_INST_ANY 57-70 % of wave cycles,
+// profiles/r01/pmc_tilep_r01t.txt), which the bf16 split form shortens
+// 2.7x.  Per chunk the lane loads its row fragment X[src_r][32 kk + 8q .. +7]
+// and its weight fragments (three pieces, NT column groups, NKK k-steps) from
+// the per-step weight images of split_weights_kernel (KS = 32, NC = 16 NT:
+// one coalesced 1 KiB wave-load per fragment).  Chunk indices run two chunks
+// ahead of the values, values one; loads are branch-free (positions past the
+// tile's last chunk are clamped to it, their work skipped uniformly).
+template <int NT, int NKK>
+__global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
+    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
+    const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
+    int64_t n_tiles, int n_y, float* __restrict__ out) {
+  constexpr int NC = 16 * NT, TR = 128;
+  constexpr int WU = 3 * 4 * NC;  // 16-byte units of one (offset, k-slice) image
+  __shared__ floatx4 lds4[kWaves][TR * NC / 4];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t tile = (lb / n_y) * kWaves + wave;
+  if (tile >= n_tiles) return;  // wave-uniform; the kernel has no block barrier
+  float* acc_s = reinterpret_cast<float*>(lds4[wave]);
+  for (int i = lane; i < TR * NC / 4; i += 64) lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int cy = (int)(lb % n_y);
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
+  const int64_t clast = ce > cb ? ce - 1 : cb;
+  const u32x4* wim_c = wimg + (int64_t)cy * NKK * WU + q * NC + r;  // lane's unit in image (o, cy, 0), piece 0
+
+  struct St {
+    int o, src, row;
+  };
+  struct Val {
+    floatx4 a[NKK][2];
+    u32x4 w[NKK][NT][3];
+  };
+  auto ld_idx = [&](int64_t c, St& d) {
+    const int64_t cc = c < clast ? c : clast;
+    d.o = chunk_off[cc];
+    d.src = chunk_src[cc * MSP_CHUNK + r];
+    d.row = chunk_row[cc * MSP_CHUNK + r];
+  };
+  auto ld_val = [&](const St& d, Val& v) {
+    const char* xs = reinterpret_cast<const char*>(x) + (uint32_t)d.src * (uint32_t)c_in * 4u;
+    const int ow = flip ? (K - 1 - d.o) : d.o;
+    const u32x4* wo = wim_c + (int64_t)ow * n_y * NKK * WU;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int k = min(32 * kk + 8 * q, c_in - 8);  // k past c_in: finite data times zero weights
+      const floatx4* pv = reinterpret_cast<const floatx4*>(xs + 4u * (uint32_t)k);
+      v.a[kk][0] = pv[0];
+      v.a[kk][1] = pv[1];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) v.w[kk][t][p] = wo[kk * WU + p * 4 * NC + 16 * t];
+    }
+  };
+  auto run = [&](const Val& v, int row, bool live) {
+    if (live) {
+      floatx4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        u32x4 xp[3];
+        split8(v.a[kk][0], v.a[kk][1], xp);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          floatx4 c = acc[t];
+          c = mfma_bf16(v.w[kk][t][2], xp[0], c);
+          c = mfma_bf16(v.w[kk][t][1], xp[1], c);
+          c = mfma_bf16(v.w[kk][t][0], xp[2], c);
+          c = mfma_bf16(v.w[kk][t][1], xp[0], c);
+          c = mfma_bf16(v.w[kk][t][0], xp[1], c);
+          acc[t] = mfma_bf16(v.w[kk][t][0], xp[0], c);
+        }
+      }
+      if (row < TR) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {  // mark the set read on every path
+      asm volatile("" ::"v"(v.a[kk][0]), "v"(v.a[kk][1]));
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(v.w[kk][t][p]));
+    }
+  };
+  constexpr int D = 2;
+  St J[D];
+  int rowR[D];
+  Val S[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    ld_idx(cb + k, J[k]);
+    rowR[k] = J[k].row;
+    ld_val(J[k], S[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) ld_idx(cb + D + k, J[k]);
+  for (int64_t c = cb; c < ce; c += D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      run(S[k], rowR[k], c + k < ce);
+      ld_val(J[k], S[k]);  // chunk c+k+D
+      rowR[k] = J[k].row;
+      ld_idx(c + k + 2 * D, J[k]);
+    }
+  }
+  const int64_t row0 = tile * TR;
+  const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
+  constexpr int V4 = NC / 4;
+  const int c0 = cy * NC;
+  for (int i = lane; i < nr * V4; i += 64) {
+    const int rr = i / V4, g = i % V4;
+    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
+        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
+  }
+}
+
+// Per-wave form for narrow outputs; ws holds the weight images (x6p_ws_bytes).
+int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
+               const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
+               float* out, void* ws, hipStream_t s) {
+  const int NT = c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1;
+  const int NKK = (c_in + 31) / 32;
+  const int n_y = c_out / (16 * NT);
+  const int64_t n_tiles = ceil_div(n_rows, 128);
+  u32x4* wimg = static_cast<u32x4*>(ws);
+  const int64_t units = (int64_t)K * c_out * NKK * 32 * 6 / 16;
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg);
+  const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
+  bool launched = false;
+#define LP(N, C)                                                                                            \
+  if (!launched && NT == N && NKK == C) {                                                                   \
+    conv_x6p_kernel<N, C><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start, chunk_off,  \
+                                                    chunk_src, chunk_row, n_rows, n_tiles, n_y, out);       \
+    launched = true;                                                                                        \
+  }
+  LP(1, 1) LP(1, 2) LP(2, 1) LP(2, 2)
+#undef LP
+  if (!launched) {
+    set_error("msp_conv_tile: no per-wave x6 kernel for c_in=%d c_out=%d", c_in, c_out);
+    return MSP_EINVAL;
+  }
+  return MSP_OK;
+}
+
+size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c_in + 31) / 32) * 32 * 6; }
+
 // ---------------------------------------------------------------- weight gradient
 // dW[o] = sum over the pairs (i, j) of offset o of x[i]^T dy[j], on bf16 MFMA
 // over exact three-piece splits of both operands (six products per fp32

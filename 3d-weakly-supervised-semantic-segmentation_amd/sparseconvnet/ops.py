@@ -63,9 +63,9 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     tiles = rules.tiles_for(tr)
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
     if n_rows:
-        # which contraction the library runs for these channels (msp_conv_tile):
-        # f32 MFMA per-wave tiles for narrow outputs, split-bf16 MFMA otherwise
-        kind += "/f32" if (c_out <= 32 and c_in <= 64) else "/x6"
+        # the contraction msp_conv_tile runs on 128-row tiles: bf16 MFMA over
+        # exact three-piece operand splits (per-wave tiles for narrow outputs)
+        kind += "/x6" if tr == 128 else "/f32"
         wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(n_rows), K, c_in, c_out, tr))
         ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
         # compulsory bytes: input rows, output rows, weights, rulebook (chunk

@@ -9,9 +9,10 @@ value = sum over ranks of level-0 active voxels per step x steps / max-over-
 ranks wall time.  N>1: one process per GPU (torchrun), each rank its own
 scenes (weak scaling), DDP gradient all-reduce over RCCL.
 
-Also reported: roofline of the dominant kernel (msp_conv_tile: f32 MFMA for
-narrow outputs, bf16 MFMA on exact three-piece splits -- six bf16 products per
-fp32 multiply-add -- otherwise; the peak is the time-weighted mix of the two)
+Also reported: roofline of the dominant kernel (msp_conv_tile: bf16 MFMA on
+exact three-piece splits -- six bf16 products per fp32 multiply-add -- so the
+peak is 2500/6 TF/s fp32-equivalent; a call on the f32-MFMA forms would be
+priced at 157.3 and the peak reported is the FLOP-weighted mix)
 timed live with HIP events on its launch stream during the timed steps, and
 the CPU oracle path (fp32, torch threads) on a bounded sample on rank 0.
 """

@@ -50,7 +50,8 @@ def test_queries_and_validation_without_gpu():
     # x6 form: split weights (K x 3 x c_out x c_pad bf16) + offset-split partials on small grids
     assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 27, 64, 64, 128) == 27 * 3 * 64 * 64 * 2
     assert _lib.query("msp_conv_tile_workspace_size", 2000, 27, 192, 192, 128) > 27 * 3 * 192 * 192 * 2
-    assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 27, 32, 32, 128) == 0  # per-wave f32 form
+    # narrow outputs: per-wave x6 form, weight images only (K x c_out x 32-deep k-slices x 3 pieces bf16)
+    assert _lib.query("msp_conv_tile_workspace_size", 10 ** 6, 27, 32, 32, 128) == 27 * 32 * 32 * 6
     # invalid arguments are rejected before any HIP call
     rc = lib.msp_conv_tile(None, 3, None, 27, 0, 16, 64, None, None, None, None, 100, None, None, 0, None)
     assert rc == -1 and b"multiples of 16" in lib.msp_last_error()

@@ -285,13 +285,15 @@ def test_residual_block_grads(n, cin):
         close(pg[k].grad, p.grad, 1e-4, "grad " + k)
 
 
-@pytest.mark.parametrize("cin,cout,flip", [(64, 64, 0), (96, 96, 1), (48, 96, 0), (256, 128, 0), (224, 32, 1)])
+@pytest.mark.parametrize("cin,cout,flip", [(64, 64, 0), (96, 96, 1), (48, 96, 0), (256, 128, 0), (224, 32, 1),
+                                           (32, 32, 0), (64, 32, 1), (48, 16, 0)])
 def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
     """msp_conv_tile on 128-row tiles runs the contraction as six bf16 MFMA
     products of exact three-piece splits (msp_conv_x6.hip).  Its error against
     an fp64 evaluation must be fp32-class: at most 2x that of the f32-input
     MFMA kernel (one fmaf chain, exact fp32) on the same rulebook, and below
-    1e-6 of the output scale."""
+    1e-6 of the output scale.  c_out <= 32 with c_in <= 64 takes the per-wave
+    form (conv_x6p_kernel), the rest the shared-tile form."""
     import ctypes
     from sparseconvnet import _lib, ops
     from sparseconvnet._lib import ptr
