@@ -1180,6 +1180,14 @@ int msp_debug_wgrad_f32(int on) {
   return MSP_OK;
 }
 
+// Experiment hook (not part of the public ABI): target block count of a
+// weight-gradient launch (msp_wgrad_pieces); 0 = the default.
+static int64_t g_wgrad_blocks = 0;
+int msp_debug_wgrad_blocks(int64_t target) {
+  g_wgrad_blocks = target;
+  return MSP_OK;
+}
+
 int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out) {
   // about 4096 blocks per launch (pieces x offsets x dW tiles), at least 256
   // pairs per piece; one-offset contractions (network-in-network weight
@@ -1189,7 +1197,7 @@ int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out) {
   wgrad_x6_tile(c_in, c_out, wa, wb);
   const int64_t n_ty = (int64_t)(c_in / (16 * wa)) * (c_out / (16 * wb));
   int64_t n = total_pairs / ((int64_t)K * 256);
-  const int64_t by_grid = 4096 / ((int64_t)K * n_ty);
+  const int64_t by_grid = (g_wgrad_blocks > 0 ? g_wgrad_blocks : 4096) / ((int64_t)K * n_ty);
   if (n > by_grid) n = by_grid;
   if (K == 1 && n > 768) n = 768;
   return n < 1 ? 1 : n;

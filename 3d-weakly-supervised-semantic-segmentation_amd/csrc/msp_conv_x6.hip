@@ -855,6 +855,13 @@ int64_t msp_debug_conv_x6(int nt, int ks, int depth, int abl, int tile_rows, con
                           const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                           const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
                           msp_stream_t stream) {
+  if (abl == 512) {  // per-wave form regardless of the channel counts (c_in <= 64)
+    const size_t needp = x6p_ws_bytes(K, c_in, c_out);
+    if (!ws) return (int64_t)needp;
+    const int rc = launch_x6p(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows,
+                              out, ws, as_stream(stream));
+    return rc ? rc : check_launch("msp_debug_conv_x6");
+  }
   PlanX6 p = plan_x6(n_rows, c_out, nt, ks, tile_rows > 0 ? tile_rows : 128);
   if (depth > 0) p.depth = depth;
   if (abl >= 256) {  // 256 + nb: weight buffer count forced

@@ -16,8 +16,12 @@ for s_ in sizes[:-1]:
     meta.downsample(s_, 2)
 lib = _lib.load()
 cases = [(L, size, ci, c) for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 128])) for ci in (c, 2 * c)]
-for (L, size, ci, c), mode in [(cs, m) for cs in cases for m in (0, 1)]:
+lib.msp_debug_wgrad_blocks.argtypes = [_lib.I64]
+BLOCKS = [int(v) for v in os.environ.get("BLOCKS", "0").split(",")]
+MODES = [int(v) for v in os.environ.get("MODES", "0,1").split(",")]
+for (L, size, ci, c), mode, nb in [(cs, m, nb) for cs in cases for m in MODES for nb in BLOCKS]:
     lib.msp_debug_wgrad_f32(mode)
+    lib.msp_debug_wgrad_blocks(nb)
     rules = meta.level(size).subm_rules(3)
     p = rules.pairs
     V = meta.level(size).n
@@ -42,6 +46,6 @@ for (L, size, ci, c), mode in [(cs, m) for cs in cases for m in (0, 1)]:
         ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
         err = max(err, ((dw[o].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
     flops = 2.0 * rules.n_rules * ci * c
-    print(f"L{L} {ci:3d}->{c:3d} {'f32' if mode else 'x6 '} V={V} R={rules.n_rules} "
+    print(f"L{L} {ci:3d}->{c:3d} {'f32' if mode else 'x6 '} blocks~{nb or 4096} V={V} R={rules.n_rules} "
           f"pieces={_lib.query('msp_wgrad_pieces', _lib.I64(p.total), 27, ci, c)}: {ms:.3f} ms "
           f"{flops / ms / 1e9:.1f} TF  max rel err {err:.2e}", flush=True)

@@ -28,9 +28,15 @@ for key in order:
         w = c["SQ_WAVE_CYCLES"]
         out.append(f"wait_any={c['SQ_WAIT_ANY'] / w:.2f} wait_inst={c['SQ_WAIT_INST_ANY'] / w:.2f} "
                    f"active={c['SQ_ACTIVE_INST_ANY'] / w:.2f}")
+    if "TCP_TCC_READ_REQ_LATENCY_sum" in c:
+        out.append(f"l2_lat={c['TCP_TCC_READ_REQ_LATENCY_sum'] / max(c['TCP_TCC_READ_REQ_sum'], 1):.0f}cyc")
     if "TCP_TCC_READ_REQ_sum" in c:
-        out.append(f"l2_lat={c['TCP_TCC_READ_REQ_LATENCY_sum'] / max(c['TCP_TCC_READ_REQ_sum'], 1):.0f}cyc "
-                   f"l2_reqs={c['TCP_TCC_READ_REQ_sum']:.3g}")
+        out.append(f"l2_reqs={c['TCP_TCC_READ_REQ_sum']:.3g} "
+                   f"({c['TCP_TCC_READ_REQ_sum'] * 128 / (c['_dur_ns'] * 1e-9) / 1e12:.1f} TB/s at 128 B)")
+    if "SQ_WAVES" in c and "SQ_INSTS_VALU" in c:
+        out.append(f"valu/wave={c['SQ_INSTS_VALU'] / c['SQ_WAVES']:.0f}")
+    if "SQ_WAVES" in c and "SQ_INSTS_VMEM_RD" in c:
+        out.append(f"vmem_rd/wave={c['SQ_INSTS_VMEM_RD'] / c['SQ_WAVES']:.0f}")
     if "TA_BUSY_avr" in c and g:
         out.append(f"ta_busy={c['TA_BUSY_avr'] / g:.2f}")
     if "TCC_HIT_sum" in c:
@@ -38,6 +44,7 @@ for key in order:
     if "FETCH_SIZE" in c:
         out.append(f"fetch={2 * c['FETCH_SIZE'] / 1e3:.0f}MB(x2)")
     if "TCP_PENDING_STALL_CYCLES_sum" in c and g:
-        out.append(f"tcp_pend={c['TCP_PENDING_STALL_CYCLES_sum'] / g / 256:.2f} "
-                   f"tcr_stall={c['TCP_TCR_TCP_STALL_CYCLES_sum'] / g / 256:.2f}")
+        out.append(f"tcp_pend={c['TCP_PENDING_STALL_CYCLES_sum'] / g / 256:.2f}")
+    if "TCP_TCR_TCP_STALL_CYCLES_sum" in c and g:
+        out.append(f"tcr_stall={c['TCP_TCR_TCP_STALL_CYCLES_sum'] / g / 256:.2f}")
     print(" ".join(out))
