@@ -581,7 +581,8 @@ size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c
 // super-steps round-robin, two register sets deep; positions past the piece
 // are clamped to its last pair and their x values zeroed (uniform branch:
 // only the last super-step of a wave in a piece can be partial).
-template <int WA, int WB>
+// ABL (timing only): 1 = no splits (raw bits as the pieces), 2 = no MFMAs.
+template <int WA, int WB, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
     const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
@@ -645,17 +646,31 @@ __global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
 #pragma unroll
         for (int i = 0; i < WA; ++i) a[k][i] = pp + k < p1 ? a[k][i] : 0.f;
     }
+    auto split = [&](const floatx4& lo, const floatx4& hi, u32x4 (&pc)[3]) {
+      if (ABL & 1) {
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+          pc[pp] = u32x4{__float_as_uint(lo[pp]), __float_as_uint(lo[pp + 1]), __float_as_uint(hi[pp]),
+                         __float_as_uint(hi[pp + 1])};
+      } else {
+        split8(lo, hi, pc);
+      }
+    };
     u32x4 bp[WB][3];
 #pragma unroll
     for (int t = 0; t < WB; ++t)
-      split8(floatx4{v.b[0][t], v.b[1][t], v.b[2][t], v.b[3][t]},
-             floatx4{v.b[4][t], v.b[5][t], v.b[6][t], v.b[7][t]}, bp[t]);
+      split(floatx4{v.b[0][t], v.b[1][t], v.b[2][t], v.b[3][t]}, floatx4{v.b[4][t], v.b[5][t], v.b[6][t], v.b[7][t]},
+            bp[t]);
 #pragma unroll
     for (int i = 0; i < WA; ++i) {
       u32x4 ap[3];
-      split8(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]}, ap);
+      split(floatx4{a[0][i], a[1][i], a[2][i], a[3][i]}, floatx4{a[4][i], a[5][i], a[6][i], a[7][i]}, ap);
 #pragma unroll
       for (int t = 0; t < WB; ++t) {
+        if (ABL & 2) {
+          acc[i][t] += __builtin_bit_cast(floatx4, ap[0] ^ ap[1] ^ ap[2] ^ bp[t][0] ^ bp[t][1] ^ bp[t][2]);
+          continue;
+        }
         floatx4 c = acc[i][t];
         c = mfma_bf16(ap[2], bp[t][0], c);
         c = mfma_bf16(ap[1], bp[t][1], c);
@@ -724,6 +739,8 @@ void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb) {
   wb = bb % 2 == 0 ? 2 : 1;
 }
 
+static int g_wgrad_abl = 0;  // msp_debug_wgrad_abl: ablation variants of the x6 weight gradient
+
 int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
                     const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
                     hipStream_t s) {
@@ -738,10 +755,29 @@ int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const 
                                                     n_pieces, n_ty, slab);                               \
     launched = true;                                                                                      \
   }
+#define LWA(A, B, AB)                                                                                     \
+  if (!launched && WA == A && WB == B && g_wgrad_abl == AB) {                                             \
+    wgrad_x6_kernel<A, B, AB><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, \
+                                                        K, n_pieces, n_ty, slab);                         \
+    launched = true;                                                                                      \
+  }
+  if (g_wgrad_abl) {
+    LWA(2, 2, 1) LWA(4, 2, 1) LWA(2, 2, 2) LWA(4, 2, 2) LWA(2, 2, 3) LWA(4, 2, 3)
+  }
+#undef LWA
   LW(1, 1) LW(2, 1) LW(3, 1) LW(4, 1) LW(1, 2) LW(2, 2) LW(3, 2) LW(4, 2)
 #undef LW
   return launched ? MSP_OK : MSP_EINVAL;
 }
+
+}  // namespace msp
+
+extern "C" int msp_debug_wgrad_abl(int abl) {
+  msp::g_wgrad_abl = abl;
+  return MSP_OK;
+}
+
+namespace msp {
 
 
 }  // namespace msp

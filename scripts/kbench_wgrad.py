@@ -19,6 +19,7 @@ cases = [(L, size, ci, c) for L, (size, c) in enumerate(zip(sizes, [32, 64, 96, 
 lib.msp_debug_wgrad_blocks.argtypes = [_lib.I64]
 BLOCKS = [int(v) for v in os.environ.get("BLOCKS", "0").split(",")]
 MODES = [int(v) for v in os.environ.get("MODES", "0,1").split(",")]
+lib.msp_debug_wgrad_abl(int(os.environ.get("ABL", "0")))
 for (L, size, ci, c), mode, nb in [(cs, m, nb) for cs in cases for m in MODES for nb in BLOCKS]:
     lib.msp_debug_wgrad_f32(mode)
     lib.msp_debug_wgrad_blocks(nb)
