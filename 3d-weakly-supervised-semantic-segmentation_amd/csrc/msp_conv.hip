@@ -1071,8 +1071,10 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
     // narrow outputs: per-wave 128-row tiles, no barriers (msp_conv_x6.hip)
     const size_t need = x6p_ws_bytes(K, c_in, c_out);
     MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_tile: workspace too small (%zu < %zu)", ws_bytes, need);
-    const int rc = launch_x6p(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows,
-                              out, ws, s);
+    // weights kept per offset run, chunk values three deep (scripts/kbench_x6.py,
+    // profiles/r01/kbench_x6r_r01u.log)
+    const int rc = launch_x6p(x, c_in, wt, K, flip, c_out, 128, tile_start, chunk_off, chunk_src, chunk_row,
+                              n_rows, out, ws, s, 0, 3, 1);
     return rc ? rc : check_launch("msp_conv_tile");
   }
   // shared 128-row tiles on bf16 MFMA with exact operand splits (msp_conv_x6.hip)

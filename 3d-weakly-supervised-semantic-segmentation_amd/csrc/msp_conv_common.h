@@ -69,10 +69,12 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s);
 
-// Per-wave split-bf16 form for narrow outputs (c_out <= 32, c_in <= 64).
-int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
-               const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
-               float* out, void* ws, hipStream_t s);
+// Per-wave split-bf16 form for narrow outputs (c_out <= 32, c_in <= 64); form 0:
+// weights reloaded per chunk, 1 / 2: per offset run, 2 / 3 register sets.
+int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s, int force_nt = 0,
+               int depth = 0, int form = 0);
 size_t x6p_ws_bytes(int K, int c_in, int c_out);
 
 // bf16-split weight gradient (msp_conv_x6.hip), used by msp_conv_wgrad.

@@ -419,13 +419,13 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
 // one coalesced 1 KiB wave-load per fragment).  Chunk indices run two chunks
 // ahead of the values, values one; loads are branch-free (positions past the
 // tile's last chunk are clamped to it, their work skipped uniformly).
-template <int NT, int NKK>
+template <int NT, int NKK, int TR = 128, int D = 2, int ABL = 0>
 __global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
     int64_t n_tiles, int n_y, float* __restrict__ out) {
-  constexpr int NC = 16 * NT, TR = 128;
+  constexpr int NC = 16 * NT;
   constexpr int WU = 3 * 4 * NC;  // 16-byte units of one (offset, k-slice) image
   __shared__ floatx4 lds4[kWaves][TR * NC / 4];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
     d.src = chunk_src[cc * MSP_CHUNK + r];
     d.row = chunk_row[cc * MSP_CHUNK + r];
   };
-  auto ld_val = [&](const St& d, Val& v) {
+  auto ld_val = [&](const St& d, Val& v, bool first = false) {
     const char* xs = reinterpret_cast<const char*>(x) + (uint32_t)d.src * (uint32_t)c_in * 4u;
     const int ow = flip ? (K - 1 - d.o) : d.o;
     const u32x4* wo = wim_c + (int64_t)ow * n_y * NKK * WU;
@@ -463,10 +463,12 @@ __global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
       const floatx4* pv = reinterpret_cast<const floatx4*>(xs + 4u * (uint32_t)k);
       v.a[kk][0] = pv[0];
       v.a[kk][1] = pv[1];
+      if (!(ABL & 2) || first) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) v.w[kk][t][p] = wo[kk * WU + p * 4 * NC + 16 * t];
+          for (int p = 0; p < 3; ++p) v.w[kk][t][p] = wo[kk * WU + p * 4 * NC + 16 * t];
+      }
     }
   };
   auto run = [&](const Val& v, int row, bool live) {
@@ -504,7 +506,6 @@ __global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
         for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(v.w[kk][t][p]));
     }
   };
-  constexpr int D = 2;
   St J[D];
   int rowR[D];
   Val S[D];
@@ -512,7 +513,7 @@ __global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
   for (int k = 0; k < D; ++k) {
     ld_idx(cb + k, J[k]);
     rowR[k] = J[k].row;
-    ld_val(J[k], S[k]);
+    ld_val(J[k], S[k], true);
   }
 #pragma unroll
   for (int k = 0; k < D; ++k) ld_idx(cb + D + k, J[k]);
@@ -536,29 +537,228 @@ __global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
   }
 }
 
+// Per-wave tiles with weight runs.  conv_x6p_kernel reloads the lane's weight
+// fragments with every chunk (6 of its 8 16-byte loads per chunk at
+// c_in = 32), yet a tile's chunks are sorted by offset, so consecutive chunks
+// mostly share them (about 3 chunks per offset run at level 0); dropping the
+// reloads halved the kernel's time (timing ablation, wrong results).  Here a
+// wave first lists its tile's offset runs (ballot over chunk_off: run start
+// and offset packed per lane, read back with v_readlane), then keeps two
+// weight sets in registers: the current run's and the next run's, loaded at
+// the current run's first chunk (uniform branches; the chunk values keep
+// their D-deep pipeline across runs).
+template <int NT, int NKK, int D, int NW>
+__global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
+    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
+    const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
+    int64_t n_tiles, int n_y, float* __restrict__ out) {
+  constexpr int NC = 16 * NT, TR = 128;
+  constexpr int WU = 3 * 4 * NC;  // 16-byte units of one (offset, k-slice) image
+  __shared__ floatx4 lds4[kWaves][TR * NC / 4];
+  __shared__ int runs_s[kWaves][128];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t tile = (lb / n_y) * kWaves + wave;
+  if (tile >= n_tiles) return;  // wave-uniform; the kernel has no block barrier
+  float* acc_s = reinterpret_cast<float*>(lds4[wave]);
+  for (int i = lane; i < TR * NC / 4; i += 64) lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int cy = (int)(lb % n_y);
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
+  const int n = (int)(ce - cb);
+  const int64_t clast = ce > cb ? ce - 1 : cb;
+  const u32x4* wim_c = wimg + (int64_t)cy * NKK * WU + q * NC + r;  // lane's unit in image (o, cy, 0), piece 0
+
+  // offset runs of the tile: packed (first chunk << 8 | offset), at most
+  // min(K, n) <= 128 of them
+  int n_runs = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const int ic = i < n ? i : n - 1;
+    const int o = chunk_off[cb + ic];
+    const int op = chunk_off[cb + (ic > 0 ? ic - 1 : 0)];
+    const bool st = i < n && (i == 0 || o != op);
+    const unsigned long long m = ballot64(st);
+    const int pos = n_runs + mbcnt64(m);
+    if (st && pos < 128) runs_s[wave][pos] = (i << 8) | o;
+    n_runs += __popcll(m);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nr_c = n_runs > 0 ? n_runs : 1;
+  const int run_lo = n_runs > 0 ? runs_s[wave][lane < n_runs ? lane : n_runs - 1] : 0;
+  const int run_hi = n_runs > 64 ? runs_s[wave][64 + lane < n_runs ? 64 + lane : n_runs - 1] : run_lo;
+  auto run_at = [&](int j) -> int {  // packed run j (clamped to the last), j uniform
+    const int jc = j < nr_c ? j : nr_c - 1;
+    return jc < 64 ? __builtin_amdgcn_readlane(run_lo, jc) : __builtin_amdgcn_readlane(run_hi, jc - 64);
+  };
+  auto start_of = [&](int j) -> int { return j < n_runs ? (run_at(j) >> 8) : (1 << 22); };
+
+  struct Wt {
+    u32x4 w[NKK][NT][3];
+  };
+  auto ld_w = [&](int j, Wt& w) {
+    const int o = run_at(j) & 255;
+    const int ow = flip ? (K - 1 - o) : o;
+    const u32x4* wo = wim_c + (int64_t)ow * n_y * NKK * WU;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) w.w[kk][t][p] = wo[kk * WU + p * 4 * NC + 16 * t];
+  };
+  struct St {
+    int src, row;
+  };
+  struct Val {
+    floatx4 a[NKK][2];
+  };
+  auto ld_idx = [&](int64_t c, St& d) {
+    const int64_t cc = c < clast ? c : clast;
+    d.src = chunk_src[cc * MSP_CHUNK + r];
+    d.row = chunk_row[cc * MSP_CHUNK + r];
+  };
+  auto ld_val = [&](const St& d, Val& v) {
+    const char* xs = reinterpret_cast<const char*>(x) + (uint32_t)d.src * (uint32_t)c_in * 4u;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int k = min(32 * kk + 8 * q, c_in - 8);  // k past c_in: finite data times zero weights
+      const floatx4* pv = reinterpret_cast<const floatx4*>(xs + 4u * (uint32_t)k);
+      v.a[kk][0] = pv[0];
+      v.a[kk][1] = pv[1];
+    }
+  };
+  auto run = [&](const Val& v, const Wt& w, int row) {
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      u32x4 xp[3];
+      split8(v.a[kk][0], v.a[kk][1], xp);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        floatx4 c = acc[t];
+        c = mfma_bf16(w.w[kk][t][2], xp[0], c);
+        c = mfma_bf16(w.w[kk][t][1], xp[1], c);
+        c = mfma_bf16(w.w[kk][t][0], xp[2], c);
+        c = mfma_bf16(w.w[kk][t][1], xp[0], c);
+        c = mfma_bf16(w.w[kk][t][0], xp[1], c);
+        acc[t] = mfma_bf16(w.w[kk][t][0], xp[0], c);
+      }
+    }
+    if (row < TR) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
+    }
+  };
+  // Wc: the set the MFMAs read (written only by register copies, so the
+  // chunk loop never waits on a weight load); Wn: the next run's set, loaded
+  // at the current run's first chunk and copied at the next run's.
+  Wt Wc, Wn;
+  ld_w(0, Wc);
+  ld_w(1, Wn);
+  int rho = 0, next_start = start_of(1);
+  St J[D];
+  int rowR[D];
+  Val S[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    ld_idx(cb + k, J[k]);
+    rowR[k] = J[k].row;
+    ld_val(J[k], S[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) ld_idx(cb + D + k, J[k]);
+  for (int64_t c = cb; c < ce; c += D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int i = (int)(c - cb) + k;
+      if (i == next_start) {  // first chunk of run rho + 1 (never true past the last run)
+        ++rho;
+        next_start = start_of(rho + 1);
+        Wc = Wn;
+        ld_w(rho + 1, Wn);
+      }
+      if (i < n) run(S[k], Wc, rowR[k]);
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) asm volatile("" ::"v"(S[k].a[kk][0]), "v"(S[k].a[kk][1]));
+      ld_val(J[k], S[k]);  // chunk c+k+D
+      rowR[k] = J[k].row;
+      ld_idx(c + k + 2 * D, J[k]);
+    }
+  }
+  const int64_t row0 = tile * TR;
+  const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
+  constexpr int V4 = NC / 4;
+  const int c0 = cy * NC;
+  for (int i = lane; i < nr * V4; i += 64) {
+    const int rr = i / V4, g = i % V4;
+    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
+        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
+  }
+}
+
 // Per-wave form for narrow outputs; ws holds the weight images (x6p_ws_bytes).
-int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
-               const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
-               float* out, void* ws, hipStream_t s) {
-  const int NT = c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1;
+// force_nt / depth: 0 = the plan's choice; tile_rows 64 or 128 (the rulebook's).
+int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s, int force_nt,
+               int depth, int form) {
+  int NT = c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1;
+  if (force_nt > 0) NT = force_nt;
+  if (force_nt < 0) NT = 2;
+  const int D = depth > 0 ? depth : 2;
   const int NKK = (c_in + 31) / 32;
+  if ((c_out / 16) % NT != 0) {
+    set_error("msp_conv_tile: per-wave x6: nt %d does not divide c_out/16 = %d", NT, c_out / 16);
+    return MSP_EINVAL;
+  }
   const int n_y = c_out / (16 * NT);
-  const int64_t n_tiles = ceil_div(n_rows, 128);
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   u32x4* wimg = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)K * c_out * NKK * 32 * 6 / 16;
   split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg);
   const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
   bool launched = false;
-#define LP(N, C)                                                                                            \
-  if (!launched && NT == N && NKK == C) {                                                                   \
-    conv_x6p_kernel<N, C><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start, chunk_off,  \
-                                                    chunk_src, chunk_row, n_rows, n_tiles, n_y, out);       \
-    launched = true;                                                                                        \
+#define LP(N, C, R, DD)                                                                                      \
+  if (!launched && NT == N && NKK == C && tile_rows == R && D == DD) {                                       \
+    conv_x6p_kernel<N, C, R, DD><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,        \
+                                                           chunk_off, chunk_src, chunk_row, n_rows, n_tiles, \
+                                                           n_y, out);                                        \
+    launched = true;                                                                                          \
   }
-  LP(1, 1) LP(1, 2) LP(2, 1) LP(2, 2)
+#define LR(N, C, DD, NWW)                                                                                    \
+  if (!launched && form == NWW - 1 && NT == N && NKK == C && tile_rows == 128 && D == DD) {                   \
+    conv_x6r_kernel<N, C, DD, NWW><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,       \
+                                                             chunk_off, chunk_src, chunk_row, n_rows, n_tiles, \
+                                                             n_y, out);                                        \
+    launched = true;                                                                                            \
+  }
+  LR(2, 1, 3, 2) LR(2, 2, 3, 2) LR(1, 1, 3, 2) LR(1, 2, 3, 2) LR(2, 1, 2, 2) LR(2, 2, 2, 2) LR(2, 1, 4, 2)
+#undef LR
+  if (!launched && force_nt < 0 && NKK <= 2) {  // ablation (timing only): weights loaded once per wave
+    if (NKK == 1)
+      conv_x6p_kernel<2, 1, 128, 2, 2><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,
+                                                                 chunk_off, chunk_src, chunk_row, n_rows, n_tiles,
+                                                                 n_y, out);
+    else
+      conv_x6p_kernel<2, 2, 128, 2, 2><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,
+                                                                 chunk_off, chunk_src, chunk_row, n_rows, n_tiles,
+                                                                 n_y, out);
+    launched = true;
+  }
+  LP(1, 1, 128, 2) LP(1, 2, 128, 2) LP(2, 1, 128, 2) LP(2, 2, 128, 2)
+  LP(1, 1, 64, 2) LP(1, 2, 64, 2) LP(2, 1, 64, 2) LP(2, 2, 64, 2)
+  LP(2, 1, 64, 3) LP(2, 2, 64, 3) LP(2, 1, 128, 3) LP(2, 2, 128, 3) LP(1, 1, 64, 3) LP(1, 2, 64, 3)
+  LP(2, 1, 64, 4) LP(1, 1, 64, 4)
 #undef LP
   if (!launched) {
-    set_error("msp_conv_tile: no per-wave x6 kernel for c_in=%d c_out=%d", c_in, c_out);
+    set_error("msp_conv_tile: no per-wave x6 kernel for c_in=%d c_out=%d nt=%d tile_rows=%d depth=%d", c_in, c_out,
+              NT, tile_rows, D);
     return MSP_EINVAL;
   }
   return MSP_OK;
@@ -891,11 +1091,12 @@ int64_t msp_debug_conv_x6(int nt, int ks, int depth, int abl, int tile_rows, con
                           const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                           const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
                           msp_stream_t stream) {
-  if (abl == 512) {  // per-wave form regardless of the channel counts (c_in <= 64)
+  if (abl >= 512 && abl <= 514) {  // per-wave forms regardless of the channel counts (c_in <= 64)
     const size_t needp = x6p_ws_bytes(K, c_in, c_out);
     if (!ws) return (int64_t)needp;
-    const int rc = launch_x6p(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows,
-                              out, ws, as_stream(stream));
+    const int rc = launch_x6p(x, c_in, wt, K, flip, c_out, tile_rows > 0 ? tile_rows : 128, tile_start,
+                              chunk_off, chunk_src, chunk_row, n_rows, out, ws, as_stream(stream), nt, depth,
+                              abl - 512);
     return rc ? rc : check_launch("msp_debug_conv_x6");
   }
   PlanX6 p = plan_x6(n_rows, c_out, nt, ks, tile_rows > 0 ? tile_rows : 128);

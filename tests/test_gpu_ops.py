@@ -293,7 +293,7 @@ def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
     an fp64 evaluation must be fp32-class: at most 2x that of the f32-input
     MFMA kernel (one fmaf chain, exact fp32) on the same rulebook, and below
     1e-6 of the output scale.  c_out <= 32 with c_in <= 64 takes the per-wave
-    form (conv_x6p_kernel), the rest the shared-tile form."""
+    form (conv_x6r_kernel: weights per offset run), the rest the shared-tile form."""
     import ctypes
     from sparseconvnet import _lib, ops
     from sparseconvnet._lib import ptr
