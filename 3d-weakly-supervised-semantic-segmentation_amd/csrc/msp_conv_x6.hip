@@ -766,6 +766,206 @@ int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c
 
 size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c_in + 31) / 32) * 32 * 6; }
 
+// ---------------------------------------------------------------- dense row groups
+// Submanifold convolutions on large levels, straight from the neighbour map
+// nbr[K][n] (int32, -1 absent): no tile rulebook and no LDS accumulation.
+// A wave owns G groups of 16 consecutive output rows and 16 NT output
+// channels, and keeps their accumulators in registers (G x NT MFMA tiles);
+// it walks the K x ceil(c_in / 32) steps (offset, 32-deep k-slice) in order,
+// gathering the 16 rows' neighbours of each group (absent neighbours and k
+// past c_in read as zero) and skipping a group's MFMAs when none of its rows
+// has the offset (wave-uniform ballot).  Rows with a neighbour are only
+// 30-55 % of a group's (offset, row) slots at levels 0-2, but every wave of a
+// block does the same steps, so the block shares each step's split weight
+// slice through LDS (double buffered, one barrier per step, staged from
+// registers loaded two steps ahead) instead of reloading it per wave.
+// Gathered values run two steps ahead, neighbour indices four; each step's six
+// piece products are summed in a zeroed accumulator and added once.
+template <int NT, int G>
+__global__ __launch_bounds__(kThreads) void conv_x6g_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
+    const int32_t* __restrict__ nbr, int64_t n_rows, int n_y, float* __restrict__ out) {
+  constexpr int NC = 16 * NT;
+  constexpr int WU = 3 * 4 * NC;  // 16-byte units of one step's split weight slice
+  constexpr int TRW = 16 * G;     // rows per wave
+  constexpr int WPT = (WU + kThreads - 1) / kThreads;
+  __shared__ u32x4 wl[2][WU];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int cy = (int)(lb % n_y);
+  const int64_t row0 = (lb / n_y) * (int64_t)(kWaves * TRW) + wave * TRW;
+  const int nks = (c_in + 31) / 32;
+  const int n_steps = K * nks;
+  uint32_t rowok = 0;  // lane's rows inside the level
+#pragma unroll
+  for (int g = 0; g < G; ++g) rowok |= (row0 + 16 * g + r < n_rows ? 1u : 0u) << g;
+
+  struct Wst {
+    u32x4 u[WPT];
+  };
+  struct Ix {
+    int v[G];
+  };
+  struct Xv {
+    floatx4 a[G][2];
+    uint32_t ok;  // lane: bit g = its row of group g has the neighbour (and k < c_in)
+  };
+  auto ld_wst = [&](int s, Wst& w) {
+    const int sc = s < n_steps ? s : n_steps - 1;
+    const int o = sc / nks, ks = sc - o * nks;
+    const int ow = flip ? K - 1 - o : o;
+    const u32x4* src = wimg + ((int64_t)(ow * n_y + cy) * nks + ks) * WU;
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int u = tid + i * kThreads;
+      w.u[i] = src[u < WU ? u : WU - 1];
+    }
+  };
+  auto st_wst = [&](const Wst& w, int buf) {
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int u = tid + i * kThreads;
+      if (WU % kThreads == 0 || u < WU) wl[buf][u] = w.u[i];
+    }
+  };
+  auto ld_ix = [&](int s, Ix& d) {
+    const int sc = s < n_steps ? s : n_steps - 1;
+    const int o = sc / nks;
+    const int32_t* m = nbr + (int64_t)o * n_rows;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t row = row0 + 16 * g + r;
+      d.v[g] = m[row < n_rows ? row : n_rows - 1];
+    }
+  };
+  // values of step s from its neighbour indices; returns the wave's mask of
+  // groups with any neighbour
+  auto ld_x = [&](int s, const Ix& d, Xv& v) -> uint32_t {
+    const int sc = s < n_steps ? s : n_steps - 1;
+    const int ks = sc % nks;
+    const int k = 32 * ks + 8 * q;
+    uint32_t am = 0, ok = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const bool has = d.v[g] >= 0 && ((rowok >> g) & 1);
+      am |= (ballot64(has) != 0 ? 1u : 0u) << g;
+      const bool lo = has && k < c_in;
+      ok |= (lo ? 1u : 0u) << g;
+      const floatx4* pv = reinterpret_cast<const floatx4*>(x + (int64_t)(lo ? d.v[g] : 0) * c_in + (lo ? k : 0));
+      v.a[g][0] = pv[0];
+      v.a[g][1] = pv[1];
+    }
+    v.ok = ok;
+    return am;
+  };
+  floatx4 acc[G][NT];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto run = [&](int buf, const Xv& v, uint32_t am) {
+    u32x4 w[NT][3];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[t][p] = wl[buf][(p * 4 + q) * NC + 16 * t + r];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if ((am >> g) & 1) {  // wave-uniform
+        const bool lo = (v.ok >> g) & 1;
+        const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+        u32x4 xp[3];
+        split8(lo ? v.a[g][0] : z, lo ? v.a[g][1] : z, xp);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {  // the step's six products summed apart, then added once
+          floatx4 c = {0.f, 0.f, 0.f, 0.f};
+          c = mfma_bf16(w[t][2], xp[0], c);
+          c = mfma_bf16(w[t][1], xp[1], c);
+          c = mfma_bf16(w[t][0], xp[2], c);
+          c = mfma_bf16(w[t][1], xp[0], c);
+          c = mfma_bf16(w[t][0], xp[1], c);
+          acc[g][t] += mfma_bf16(w[t][0], xp[0], c);
+        }
+      }
+    }
+  };
+  Wst S[2];
+  Ix I[2];
+  Xv X[2];
+  uint32_t am[2];
+  ld_wst(0, S[0]);
+  ld_wst(1, S[1]);
+  ld_ix(0, I[0]);
+  ld_ix(1, I[1]);
+  st_wst(S[0], 0);
+  ld_wst(2, S[0]);
+  am[0] = ld_x(0, I[0], X[0]);
+  am[1] = ld_x(1, I[1], X[1]);
+  ld_ix(2, I[0]);
+  ld_ix(3, I[1]);
+  // step s (slot k = s & 1): wl[k] holds its weight slice, X[k] its values,
+  // S[k ^ 1] the slice of s + 1, I[k] the indices of s + 2, I[k ^ 1] of s + 3
+  auto step = [&](int s, auto kc) {
+    constexpr int k = decltype(kc)::value;
+    __syncthreads();
+    st_wst(S[k ^ 1], k ^ 1);
+    ld_wst(s + 3, S[k ^ 1]);
+    run(k, X[k], am[k]);
+    am[k] = ld_x(s + 2, I[k], X[k]);
+    ld_ix(s + 4, I[k]);
+  };
+  for (int s = 0; s < n_steps; s += 2) {
+    step(s, std::integral_constant<int, 0>{});
+    if (s + 1 < n_steps) step(s + 1, std::integral_constant<int, 1>{});
+  }
+  float* dst = out + cy * NC + 4 * q;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if ((rowok >> g) & 1) {
+      float* rowp = dst + (row0 + 16 * g + r) * c_out;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(rowp + 16 * t) = acc[g][t];
+    }
+  }
+}
+
+// Dense row-group form; ws holds the split weight slices (x6g_ws_bytes).
+int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
+               int64_t n_rows, float* out, void* ws, hipStream_t s, int nt, int g) {
+  const int n16 = c_out / 16;
+  // NT = 4 (3 for 96 channels) with G = 2: scripts/kbench_nbr.py,
+  // profiles/r01/kbench_nbr_r01v.log
+  if (nt <= 0) nt = n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1));
+  if (g <= 0) g = 2;
+  if (n16 % nt != 0) {
+    set_error("msp_conv_nbr: nt %d does not divide c_out/16 = %d", nt, n16);
+    return MSP_EINVAL;
+  }
+  const int n_y = n16 / nt;
+  const int nks = (c_in + 31) / 32;
+  u32x4* wimg = static_cast<u32x4*>(ws);
+  const int64_t units = (int64_t)K * c_out * nks * 32 * 6 / 16;
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * nt, 32, wimg);
+  const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)kWaves * 16 * g) * n_y);
+  bool launched = false;
+#define LG(N, GG)                                                                                             \
+  if (!launched && nt == N && g == GG) {                                                                      \
+    conv_x6g_kernel<N, GG><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, n_rows, n_y, out);   \
+    launched = true;                                                                                          \
+  }
+  LG(4, 2) LG(3, 2) LG(2, 2) LG(1, 2) LG(6, 2) LG(4, 3)
+#undef LG
+  if (!launched) {
+    set_error("msp_conv_nbr: no dense-group kernel for nt=%d g=%d", nt, g);
+    return MSP_EINVAL;
+  }
+  return MSP_OK;
+}
+
+size_t x6g_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c_in + 31) / 32) * 32 * 6; }
+
 // ---------------------------------------------------------------- weight gradient
 // dW[o] = sum over the pairs (i, j) of offset o of x[i]^T dy[j], on bf16 MFMA
 // over exact three-piece splits of both operands (six products per fp32
@@ -1083,6 +1283,49 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
 }  // namespace msp
 
 extern "C" {
+
+// Dense row-group form on the large levels with c_out >= 64 (measured against
+// msp_conv_tile on the headline batch, profiles/r01/kbench_nbr_r01v.log: L0
+// 32->64 -13 %, L1 64->64 -3 %, L2 96->96 -9 %, 192->96 -6 %; the narrow
+// per-wave form stays ahead for c_out = 32 and the shared tile below 10^5 rows).
+int msp_conv_nbr_preferred(int64_t n_rows, int c_in, int c_out) {
+  (void)c_in;
+  return n_rows >= 100000 && c_out >= 64 && c_out % 16 == 0 ? 1 : 0;
+}
+
+size_t msp_conv_nbr_workspace_size(int K, int c_in, int c_out) {
+  if (K <= 0 || c_in <= 0 || c_out <= 0) return 0;
+  return x6g_ws_bytes(K, c_in, c_out);
+}
+
+int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
+                 int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
+              "msp_conv_nbr: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
+  MSP_REQUIRE(K >= 1 && K <= 128, "msp_conv_nbr: K must be in [1, 128] (got %d)", K);
+  MSP_REQUIRE(n_rows >= 0, "msp_conv_nbr: n_rows must be >= 0");
+  if (n_rows == 0) return MSP_OK;
+  MSP_REQUIRE(x && wt && nbr && out, "msp_conv_nbr: null pointer");
+  const size_t need = x6g_ws_bytes(K, c_in, c_out);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_nbr: workspace too small (%zu < %zu)", ws_bytes, need);
+  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, n_rows, out, ws, as_stream(stream), 0, 0);
+  return rc ? rc : check_launch("msp_conv_nbr");
+}
+
+// Experiment hook (not part of the public ABI; scripts/kbench_nbr.py): the
+// dense row-group form with NT / G forced (0 = the plan's choice).  With
+// ws == nullptr returns the workspace bytes needed.
+int64_t msp_debug_conv_nbr(int nt, int g, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+                           const int32_t* nbr, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                           msp_stream_t stream) {
+  const size_t need = x6g_ws_bytes(K, c_in, c_out);
+  if (!ws) return (int64_t)need;
+  MSP_REQUIRE(ws_bytes >= need, "msp_debug_conv_nbr: workspace too small");
+  MSP_REQUIRE(c_in % 16 == 0 && c_out % 16 == 0, "msp_debug_conv_nbr: channels must be multiples of 16");
+  if (n_rows == 0) return 0;
+  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, n_rows, out, ws, as_stream(stream), nt, g);
+  return rc ? rc : check_launch("msp_debug_conv_nbr");
+}
 
 // Experiment hook (not part of the public ABI; scripts/kbench_conv.py): the
 // x6 shared-tile form with NT / KS forced (0 = the plan's choice).  With

@@ -9,7 +9,7 @@ value = sum over ranks of level-0 active voxels per step x steps / max-over-
 ranks wall time.  N>1: one process per GPU (torchrun), each rank its own
 scenes (weak scaling), DDP gradient all-reduce over RCCL.
 
-Also reported: roofline of the dominant kernel (msp_conv_tile: bf16 MFMA on
+Also reported: roofline of the dominant kernel (msp_conv_tile / msp_conv_nbr: bf16 MFMA on
 exact three-piece splits -- six bf16 products per fp32 multiply-add -- so the
 peak is 2500/6 TF/s fp32-equivalent; a call on the f32-MFMA forms would be
 priced at 157.3 and the peak reported is the FLOP-weighted mix)
@@ -41,12 +41,12 @@ X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
 
 
 def kind_peak(kind):
-    return X6_PEAK_TFLOPS if kind.endswith("/x6") else FP32_MFMA_PEAK_TFLOPS
+    return X6_PEAK_TFLOPS if kind.endswith("/x6") or kind.endswith("/x6g") else FP32_MFMA_PEAK_TFLOPS
 HBM_PEAK_GBS = 8000.0
 
 
 class KernelRecorder:
-    """Brackets every msp_conv_tile launch with torch.cuda.Events on the
+    """Brackets every msp_conv_tile / msp_conv_nbr launch with torch.cuda.Events on the
     current stream (the stream the kernel is launched on) and accumulates the
     algorithmic FLOPs (2 * rules * c_in * c_out) per launch."""
 
@@ -286,7 +286,7 @@ def main():
                 "fwd_multiply_adds": macs,
             },
             "roofline": {
-                "kernel": "msp_conv_tile (submanifold fwd/bwd-data, strided conv fwd, deconv bwd-data)",
+                "kernel": "msp_conv_tile / msp_conv_nbr (submanifold fwd/bwd-data, strided conv fwd, deconv bwd-data)",
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": peak,
@@ -296,7 +296,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / peak,
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per msp_conv_tile call (PMC 2*FETCH_SIZE + WRITE_SIZE)",
+                "traffic_unit": "HBM bytes per msp_conv_tile / msp_conv_nbr call (PMC 2*FETCH_SIZE + WRITE_SIZE)",
                 "traffic_source": traffic_src,
                 "alg_bytes_per_call": abytes / max(nlaunch, 1),
                 "alg_bytes_gbs": abytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0,

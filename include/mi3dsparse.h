@@ -138,6 +138,19 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                   const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
                   msp_stream_t stream);
+/* Dense row-group form of the submanifold convolution, straight from the
+ * neighbour map nbr[K][n_rows] (int32, -1 absent, row stride n_rows): same
+ * sum as msp_conv_tile over that map's tile rulebook (same flip and weight
+ * layout), with every 16 consecutive output rows computed together over all
+ * K offsets (absent neighbours contribute zero, a group with none of an
+ * offset skips it) and accumulated in registers: no tile rulebook needed.
+ * Same split-bf16 arithmetic and error class as msp_conv_tile.
+ * msp_conv_nbr_preferred says for which shapes the library runs it (the
+ * large levels, c_out >= 64); ws_bytes >= msp_conv_nbr_workspace_size. */
+int msp_conv_nbr_preferred(int64_t n_rows, int c_in, int c_out);
+size_t msp_conv_nbr_workspace_size(int K, int c_in, int c_out);
+int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
+                 int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
 /* One contribution per output row (deconvolution forward, strided
  * convolution backward-data): out[pair_out[p]] = W'[o]^T x[pair_in[p]] for the
  * pairs of offset o.  chunk_start[K+1] (device) = prefix sums of

@@ -3,7 +3,7 @@
 HBM/rocprofv3 section): FETCH_SIZE is doubled (gfx950 tallies 128-B
 requests at 64 B), WRITE_SIZE taken as is; both are in KB per dispatch.
 
-One msp_conv_tile call launches one conv kernel (conv_x6d / conv_x6p / conv_tilep /
+One msp_conv_tile call launches one conv kernel (conv_x6d / conv_x6r / conv_x6g / conv_x6p / conv_tilep /
 conv_tile7 / conv_tile4 / conv_tile) plus, for the x6 form, a
 split_weights and, for split grids, a split_reduce; traffic per call = sum
 over the family's dispatches / number of conv kernel dispatches.
@@ -11,7 +11,7 @@ Writes JSON: python scripts/pmc_traffic.py gpurun_out/pmc_<tag> out.json"""
 import csv, glob, json, os, sys
 
 root, out_path = sys.argv[1], sys.argv[2]
-conv_names = ("conv_x6d_kernel", "conv_x6p_kernel", "conv_tile7_kernel", "conv_tilep_kernel", "conv_tile4_kernel", "conv_tile_kernel")
+conv_names = ("conv_x6d_kernel", "conv_x6p_kernel", "conv_x6r_kernel", "conv_x6g_kernel", "conv_tile7_kernel", "conv_tilep_kernel", "conv_tile4_kernel", "conv_tile_kernel")
 tot = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
 ndisp = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}
 dur = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}

@@ -329,3 +329,92 @@ def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
     e_x6 = (y.double() - ref).abs().max().item() / scale
     e_f32 = (y32.double() - ref).abs().max().item() / scale
     assert e_x6 <= max(2.0 * e_f32, 1e-7) and e_x6 < 1e-6, (e_x6, e_f32)
+
+
+@pytest.mark.parametrize("cin,cout,flip", [(64, 64, 0), (64, 64, 1), (32, 64, 1), (96, 96, 0), (192, 96, 1),
+                                           (96, 192, 0), (48, 64, 0), (64, 128, 1), (32, 32, 0), (16, 80, 1)])
+def test_conv_nbr_accuracy(cin, cout, flip):
+    """msp_conv_nbr (dense row groups over the neighbour map, register
+    accumulators) against an fp64 evaluation of the same convolution: the
+    error bar of the split-bf16 tile form (at most 2x the f32-input MFMA
+    kernel's error on the same rulebook, and below 1e-6 of the output
+    scale), and agreement with msp_conv_tile.  Includes c_in not a multiple
+    of 32 (zero k-padding) and a last group of rows past the level."""
+    import ctypes
+    from sparseconvnet import _lib, ops
+    from sparseconvnet._lib import ptr
+    torch.manual_seed(cin * 7 + cout)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    lvl = t.metadata.level(64)
+    rules = lvl.subm_rules(3)
+    V = lvl.n
+    assert V % 16 != 0 or V % 128 != 0  # a partial row group or block
+    x = torch.randn(V, cin, device=DEV)
+    wt = torch.randn(27, cout, cin, device=DEV) / (27 * cin) ** 0.5
+    y = ops.conv_nbr(x, wt, 27, flip, cout, rules.nbr, V)
+    tl = rules.tiles_for(128)
+    yt = torch.empty(V, cout, device=DEV)
+    wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(V), 27, cin, cout, 128))
+    ws = torch.empty(max(wsb // 4, 1), device=DEV)
+    _lib.call("msp_conv_tile", ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]),
+              ptr(tl["chunk_off"]), ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(yt), ptr(ws), wsb,
+              _lib.stream(x.device))
+    lib = _lib.load()
+    fn = lib.msp_debug_conv_tile
+    P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    fn.restype = I
+    fn.argtypes = [I, I, P, I, P, I, I, I, I, P, P, P, P, I64, P, P, P]
+    nt = 2 if (cout // 16) % 2 == 0 else 1
+    y32 = torch.empty(V, cout, device=DEV)
+    rc = fn(81, nt, ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
+            ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(y32), None, _lib.stream(x.device))
+    assert rc == 0, lib.msp_last_error()
+    nb = rules.nbr.long()
+    x64 = torch.cat([x.double(), torch.zeros(1, cin, dtype=torch.float64, device=DEV)])
+    w64 = wt.double().flip(0) if flip else wt.double()
+    ref = torch.zeros(V, cout, dtype=torch.float64, device=DEV)
+    for o in range(27):
+        ref += x64[torch.where(nb[o] >= 0, nb[o], V)] @ w64[o].t()
+    scale = ref.abs().max().item()
+    e_g = (y.double() - ref).abs().max().item() / scale
+    e_f32 = (y32.double() - ref).abs().max().item() / scale
+    e_t = (yt.double() - ref).abs().max().item() / scale
+    assert e_g <= max(2.0 * e_f32, 1e-7) and e_g < 1e-6, (e_g, e_f32, e_t)
+    assert ((y - yt).abs().max().item() / scale) < 2e-6
+
+
+def test_subm_conv_large_level_uses_nbr_form():
+    """A level above the dense-form threshold (>= 10^5 rows) runs the module
+    forward and backward-data through msp_conv_nbr; both match an fp64
+    evaluation from the neighbour map (1e-5 of scale), and the weight gradient
+    matches too."""
+    from sparseconvnet import _lib
+    b = make_batch(1, 50, seed=5)
+    coords = torch.from_numpy(b["coords"]).to(DEV)
+    feats = torch.from_numpy(b["feats"]).to(DEV)
+    t = scn.InputLayer(3, 4096, mode=4)([coords, feats])
+    V = t.features.size(0)
+    assert V >= 100000 and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(V), 64, 64))
+    torch.manual_seed(3)
+    x = torch.randn(V, 64, device=DEV, requires_grad=True)
+    t.features = x
+    conv = scn.SubmanifoldConvolution(3, 64, 64, 3, False).to(DEV)
+    y = conv(t).features
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    nb = t.metadata.level(4096).subm_rules(3).nbr.long()
+    w = conv.weight.detach().double().reshape(27, 64, 64)  # [K][c_in][c_out]
+    x64 = torch.cat([x.detach().double(), torch.zeros(1, 64, dtype=torch.float64, device=DEV)])
+    ref = torch.zeros(V, 64, dtype=torch.float64, device=DEV)
+    dx = torch.zeros(V + 1, 64, dtype=torch.float64, device=DEV)
+    dw = torch.zeros(27, 64, 64, dtype=torch.float64, device=DEV)
+    g64 = gy.double()
+    for o in range(27):
+        src = torch.where(nb[o] >= 0, nb[o], V)
+        ref += x64[src] @ w[o]
+        dx.index_add_(0, src, g64 @ w[o].t())
+        dw[o] = x64[src].t() @ g64
+    close(y, ref, 1e-5, "nbr fwd")
+    close(x.grad, dx[:V], 1e-5, "nbr bwd-data")
+    close(conv.weight.grad.reshape(27, 64, 64), dw, 1e-5, "nbr dW")
