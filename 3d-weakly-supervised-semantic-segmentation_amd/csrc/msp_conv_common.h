@@ -79,7 +79,7 @@ size_t x6p_ws_bytes(int K, int c_in, int c_out);
 
 // Dense row-group split-bf16 form over the neighbour map (submanifold convs).
 int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
-               int64_t n_rows, float* out, void* ws, hipStream_t s, int nt = 0, int g = 0);
+               const int32_t* perm, int64_t n_rows, float* out, void* ws, hipStream_t s, int nt = 0, int g = 0);
 size_t x6g_ws_bytes(int K, int c_in, int c_out);
 
 // bf16-split weight gradient (msp_conv_x6.hip), used by msp_conv_wgrad.

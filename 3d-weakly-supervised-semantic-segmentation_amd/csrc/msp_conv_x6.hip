@@ -784,7 +784,8 @@ size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c
 template <int NT, int G>
 __global__ __launch_bounds__(kThreads) void conv_x6g_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
-    const int32_t* __restrict__ nbr, int64_t n_rows, int n_y, float* __restrict__ out) {
+    const int32_t* __restrict__ nbr, const int32_t* __restrict__ perm, int64_t n_rows, int n_y,
+    float* __restrict__ out) {
   constexpr int NC = 16 * NT;
   constexpr int WU = 3 * 4 * NC;  // 16-byte units of one step's split weight slice
   constexpr int TRW = 16 * G;     // rows per wave
@@ -912,19 +913,22 @@ __global__ __launch_bounds__(kThreads) void conv_x6g_kernel(
     __syncthreads();
     st_wst(S[k ^ 1], k ^ 1);
     ld_wst(s + 3, S[k ^ 1]);
-    run(k, X[k], am[k]);
+    run(k, X[k], s < n_steps ? am[k] : 0u);
     am[k] = ld_x(s + 2, I[k], X[k]);
     ld_ix(s + 4, I[k]);
   };
+  // an even step count (a trailing step with no work), so both halves of the
+  // unrolled loop always run and the wait counts are the same every lap
   for (int s = 0; s < n_steps; s += 2) {
     step(s, std::integral_constant<int, 0>{});
-    if (s + 1 < n_steps) step(s + 1, std::integral_constant<int, 1>{});
+    step(s + 1, std::integral_constant<int, 1>{});
   }
   float* dst = out + cy * NC + 4 * q;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if ((rowok >> g) & 1) {
-      float* rowp = dst + (row0 + 16 * g + r) * c_out;
+      const int64_t j = row0 + 16 * g + r;
+      float* rowp = dst + (perm ? (int64_t)perm[j] : j) * c_out;
 #pragma unroll
       for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(rowp + 16 * t) = acc[g][t];
     }
@@ -933,7 +937,7 @@ __global__ __launch_bounds__(kThreads) void conv_x6g_kernel(
 
 // Dense row-group form; ws holds the split weight slices (x6g_ws_bytes).
 int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
-               int64_t n_rows, float* out, void* ws, hipStream_t s, int nt, int g) {
+               const int32_t* perm, int64_t n_rows, float* out, void* ws, hipStream_t s, int nt, int g) {
   const int n16 = c_out / 16;
   // NT = 4 (3 for 96 channels) with G = 2: scripts/kbench_nbr.py,
   // profiles/r01/kbench_nbr_r01v.log
@@ -952,7 +956,8 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   bool launched = false;
 #define LG(N, GG)                                                                                             \
   if (!launched && nt == N && g == GG) {                                                                      \
-    conv_x6g_kernel<N, GG><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, n_rows, n_y, out);   \
+    conv_x6g_kernel<N, GG><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, perm, n_rows, n_y,    \
+                                                     out);                                                    \
     launched = true;                                                                                          \
   }
   LG(4, 2) LG(3, 2) LG(2, 2) LG(1, 2) LG(6, 2) LG(4, 3)
@@ -1299,7 +1304,7 @@ size_t msp_conv_nbr_workspace_size(int K, int c_in, int c_out) {
 }
 
 int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
-                 int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream) {
+                 const int32_t* perm, int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream) {
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_nbr: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= 128, "msp_conv_nbr: K must be in [1, 128] (got %d)", K);
@@ -1308,7 +1313,7 @@ int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int
   MSP_REQUIRE(x && wt && nbr && out, "msp_conv_nbr: null pointer");
   const size_t need = x6g_ws_bytes(K, c_in, c_out);
   MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_nbr: workspace too small (%zu < %zu)", ws_bytes, need);
-  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, n_rows, out, ws, as_stream(stream), 0, 0);
+  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream), 0, 0);
   return rc ? rc : check_launch("msp_conv_nbr");
 }
 
@@ -1316,14 +1321,14 @@ int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int
 // dense row-group form with NT / G forced (0 = the plan's choice).  With
 // ws == nullptr returns the workspace bytes needed.
 int64_t msp_debug_conv_nbr(int nt, int g, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
-                           const int32_t* nbr, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
-                           msp_stream_t stream) {
+                           const int32_t* nbr, const int32_t* perm, int64_t n_rows, float* out, void* ws,
+                           size_t ws_bytes, msp_stream_t stream) {
   const size_t need = x6g_ws_bytes(K, c_in, c_out);
   if (!ws) return (int64_t)need;
   MSP_REQUIRE(ws_bytes >= need, "msp_debug_conv_nbr: workspace too small");
   MSP_REQUIRE(c_in % 16 == 0 && c_out % 16 == 0, "msp_debug_conv_nbr: channels must be multiples of 16");
   if (n_rows == 0) return 0;
-  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, n_rows, out, ws, as_stream(stream), nt, g);
+  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream), nt, g);
   return rc ? rc : check_launch("msp_debug_conv_nbr");
 }
 

@@ -409,6 +409,72 @@ int msp_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* v
   return MSP_OK;
 }
 
+// ---------------------------------------------------------------- dense row order
+// Row order for the dense row-group convolution (msp_conv_nbr): inside each
+// window of 2^lw consecutive rows (spatially compact in key order), rows are
+// sorted stably by their neighbour mask, so a 16-row group mostly shares its
+// offsets (fewer zero rows in the MFMA tiles: at 4096-row windows about 0.74
+// of a group's (offset, row) slots carry a rule at level 1 instead of 0.49)
+// while the gathers of a window stay local.  Keys (window << K | mask) are
+// radix sorted with their row numbers; the neighbour map is then permuted.
+static __global__ __launch_bounds__(256) void dense_keys_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
+                                                                int lw, uint64_t* __restrict__ keys,
+                                                                int32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t m = 0;
+  for (int o = 0; o < K; ++o) m |= (uint64_t)(nbr[(int64_t)o * n + i] >= 0) << o;
+  keys[i] = ((uint64_t)(i >> lw) << K) | m;
+  vals[i] = (int32_t)i;
+}
+
+static __global__ __launch_bounds__(256) void permute_map_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
+                                                                 const int32_t* __restrict__ perm,
+                                                                 int32_t* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const int64_t src = perm[j];
+  for (int o = 0; o < K; ++o) out[(int64_t)o * n + j] = nbr[(int64_t)o * n + src];
+}
+
+static int dense_order_bits(int64_t n, int K, int lw) {
+  int wb = 0;
+  while (wb < 40 && ((n - 1) >> lw) >> wb) ++wb;
+  return K + wb;
+}
+
+size_t msp_dense_order_workspace_size(int64_t n, int K, int log2_window) {
+  if (n <= 0 || K <= 0 || K > 32 || log2_window < 4 || log2_window > 30) return 0;
+  const int end_bit = dense_order_bits(n, K, log2_window);
+  auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  return 2 * r((size_t)n * 8) + r((size_t)n * 4) + r(msp_sort_workspace_size(n, end_bit));
+}
+
+int msp_dense_order(const int32_t* nbr, int K, int64_t n, int log2_window, int32_t* perm, int32_t* nbr_perm,
+                    void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && K <= 32, "msp_dense_order: K must be in [1, 32] (got %d)", K);
+  MSP_REQUIRE(log2_window >= 4 && log2_window <= 30, "msp_dense_order: log2_window must be in [4, 30]");
+  MSP_REQUIRE(n >= 0, "msp_dense_order: n must be >= 0");
+  if (n == 0) return MSP_OK;
+  const size_t need = msp_dense_order_workspace_size(n, K, log2_window);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_dense_order: workspace too small (%zu < %zu)", ws_bytes, need);
+  hipStream_t s = as_stream(stream);
+  auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  char* w = static_cast<char*>(ws);
+  uint64_t* k_in = reinterpret_cast<uint64_t*>(w);
+  uint64_t* k_out = reinterpret_cast<uint64_t*>(w + r((size_t)n * 8));
+  int32_t* v_in = reinterpret_cast<int32_t*>(w + 2 * r((size_t)n * 8));
+  void* sws = w + 2 * r((size_t)n * 8) + r((size_t)n * 4);
+  const int end_bit = dense_order_bits(n, K, log2_window);
+  const unsigned nb = (unsigned)ceil_div(n, 256);
+  dense_keys_kernel<<<nb, 256, 0, s>>>(nbr, K, n, log2_window, k_in, v_in);
+  size_t sbytes = msp_sort_workspace_size(n, end_bit);
+  MSP_HIP(rocprim::radix_sort_pairs(sws, sbytes, k_in, k_out, v_in, perm, (size_t)n, 0u, (unsigned)end_bit, s),
+          "msp_dense_order");
+  permute_map_kernel<<<nb, 256, 0, s>>>(nbr, K, n, perm, nbr_perm);
+  return check_launch("msp_dense_order");
+}
+
 int msp_segment(const uint64_t* sorted_keys, int64_t n, int shift, const int32_t* perm, int32_t* seg_of,
                 int32_t* p2v, uint64_t* uniq_keys, int32_t* seg_start, int64_t* n_uniq, void* ws,
                 size_t ws_bytes, msp_stream_t stream) {

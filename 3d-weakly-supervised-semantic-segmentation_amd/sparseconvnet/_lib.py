@@ -38,7 +38,9 @@ PROTOTYPES = {
     "msp_conv_tile": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_nbr_preferred": (I, [I64, I, I]),
     "msp_conv_nbr_workspace_size": (SZ, [I, I, I]),
-    "msp_conv_nbr": (I, [P, I, P, I, I, I, P, I64, P, P, SZ, P]),
+    "msp_conv_nbr": (I, [P, I, P, I, I, I, P, P, I64, P, P, SZ, P]),
+    "msp_dense_order_workspace_size": (SZ, [I64, I, I]),
+    "msp_dense_order": (I, [P, I, I64, I, P, P, P, SZ, P]),
     "msp_conv_pairs": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
     "msp_wgrad_pieces": (I64, [I64, I, I, I]),
     "msp_conv_wgrad": (I, [P, I, P, I, P, P, P, I, I64, P, P, P]),

@@ -85,6 +85,9 @@ class PairLists:
         self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(device, non_blocking=True)
 
 
+DENSE_LOG2_WINDOW = 12  # rows of one mask-sorting window of msp_dense_order
+
+
 class SubmRules:
     def __init__(self, level, filter_size):
         dev, s = level.device, _lib.stream(level.device)
@@ -97,9 +100,29 @@ class SubmRules:
             call("msp_subm_map", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(table), cap,
                  ptr(self.nbr), s)
         self._tiles = {}
+        self._dense = None
         self._map, self._n = self.nbr, V
         self.pairs = PairLists(self.nbr, K, V, dev, s)
         self.n_rules = self.pairs.total  # = SCN rulebook size (centre included)
+
+    def dense_order(self):
+        """(perm, permuted neighbour map) for the dense row-group convolution
+        (msp_dense_order: rows sorted by neighbour mask inside 4096-row
+        windows), built on first use; (None, nbr) when K > 32."""
+        if self._dense is None:
+            V, K = self._n, self.K
+            if K > 32 or V == 0:
+                self._dense = (None, self.nbr)
+            else:
+                dev, s = self.nbr.device, _lib.stream(self.nbr.device)
+                perm = torch.empty(V, dtype=torch.int32, device=dev)
+                nbr_p = torch.empty((K, V), dtype=torch.int32, device=dev)
+                wsb = int(_lib.query("msp_dense_order_workspace_size", _lib.I64(V), K, DENSE_LOG2_WINDOW))
+                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+                call("msp_dense_order", ptr(self.nbr), K, V, DENSE_LOG2_WINDOW, ptr(perm), ptr(nbr_p), ptr(ws), wsb,
+                     s)
+                self._dense = (perm, nbr_p)
+        return self._dense
 
     def tiles_for(self, tile_rows):
         """Tile rulebook with tile_rows-row tiles, built on first use."""

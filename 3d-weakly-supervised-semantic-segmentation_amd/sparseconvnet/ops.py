@@ -61,7 +61,8 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     c_in = x.size(1)
     nbr = getattr(rules, "nbr", None)  # submanifold rules carry the neighbour map
     if nbr is not None and n_rows and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(n_rows), c_in, c_out)):
-        return conv_nbr(x, wt, K, flip, c_out, nbr, n_rows, kind, flops)
+        perm, nbr_p = rules.dense_order()
+        return conv_nbr(x, wt, K, flip, c_out, nbr_p, n_rows, kind, flops, perm)
     tr = int(_lib.query("msp_conv_tile_rows", _lib.I64(n_rows), c_in, c_out))
     tiles = rules.tiles_for(tr)
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
@@ -100,18 +101,19 @@ def conv_wgrad(x, dy, pairs, pin, pout, K):
     return dw
 
 
-def conv_nbr(x, wt, K, flip, c_out, nbr, n_rows, kind="conv_nbr", flops=0):
+def conv_nbr(x, wt, K, flip, c_out, nbr, n_rows, kind="conv_nbr", flops=0, perm=None):
     """Dense row-group form of the submanifold convolution straight from the
-    neighbour map nbr[K][n_rows] (msp_conv_nbr: no tile rulebook)."""
+    neighbour map nbr[K][n_rows] (msp_conv_nbr: no tile rulebook); with perm,
+    nbr is the map permuted by it (SubmRules.dense_order)."""
     c_in = x.size(1)
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
     wsb = int(_lib.query("msp_conv_nbr_workspace_size", K, c_in, c_out))
     ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
-    # compulsory bytes: input rows, output rows, weights, the neighbour map
-    nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out + K * n_rows)
+    # compulsory bytes: input rows, output rows, weights, the neighbour map (+ row order)
+    nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out + K * n_rows + (n_rows if perm is not None else 0))
     _record(kind + "/x6g", flops, lambda: call(
-        "msp_conv_nbr", ptr(x), c_in, ptr(wt), K, int(flip), c_out, ptr(nbr), n_rows, ptr(out), ptr(ws), wsb,
-        _stream(x)), nbytes)
+        "msp_conv_nbr", ptr(x), c_in, ptr(wt), K, int(flip), c_out, ptr(nbr), ptr(perm) if perm is not None else None,
+        n_rows, ptr(out), ptr(ws), wsb, _stream(x)), nbytes)
     return out[:n_rows]
 
 

@@ -147,10 +147,21 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
  * Same split-bf16 arithmetic and error class as msp_conv_tile.
  * msp_conv_nbr_preferred says for which shapes the library runs it (the
  * large levels, c_out >= 64); ws_bytes >= msp_conv_nbr_workspace_size. */
+/* With perm non-NULL, position j of the groups is output row perm[j] and
+ * nbr holds the permuted map (nbr[o][j] = neighbour of row perm[j]), as
+ * msp_dense_order makes them: rows with similar neighbour masks share a
+ * group, so fewer MFMA rows are zero. */
 int msp_conv_nbr_preferred(int64_t n_rows, int c_in, int c_out);
 size_t msp_conv_nbr_workspace_size(int K, int c_in, int c_out);
 int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
-                 int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
+                 const int32_t* perm, int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
+/* Row order for msp_conv_nbr: inside each window of 2^log2_window
+ * consecutive rows, rows sorted stably by their neighbour mask (K <= 32):
+ * perm[j] = row at position j, nbr_perm[o][j] = nbr[o][perm[j]] (both [n] /
+ * [K][n], caller-owned); ws_bytes >= msp_dense_order_workspace_size. */
+size_t msp_dense_order_workspace_size(int64_t n, int K, int log2_window);
+int msp_dense_order(const int32_t* nbr, int K, int64_t n, int log2_window, int32_t* perm, int32_t* nbr_perm,
+                    void* ws, size_t ws_bytes, msp_stream_t stream);
 /* One contribution per output row (deconvolution forward, strided
  * convolution backward-data): out[pair_out[p]] = W'[o]^T x[pair_in[p]] for the
  * pairs of offset o.  chunk_start[K+1] (device) = prefix sums of

@@ -16,7 +16,7 @@ lib = _lib.load()
 P, I, I64, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
 fn = lib.msp_debug_conv_nbr
 fn.restype = I64
-fn.argtypes = [I, I, P, I, P, I, I, I, P, I64, P, P, SZ, P]
+fn.argtypes = [I, I, P, I, P, I, I, I, P, P, I64, P, P, SZ, P]
 b = make_batch(8, 50, seed=1)
 t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
 meta = t.metadata
@@ -27,7 +27,9 @@ sizes = [4096 >> i for i in range(n_lv)]
 for s_ in sizes[:-1]:
     meta.downsample(s_, 2)
 s = _lib.stream()
-VAR = [tuple(int(v) for v in e.split(":")) for e in os.environ.get("NBR", "0:0").split(",")]
+# nt:g[:ordered]  (ordered 1 = rows in SubmRules.dense_order's mask-sorted order)
+VAR = [tuple([int(v) for v in e.split(":")] + [0, 0, 1][len(e.split(":")):]) for e in
+       os.environ.get("NBR", "0:0:1,0:0:0").split(",")]
 NSUB = 4096
 
 
@@ -70,13 +72,15 @@ for L, size in enumerate(sizes):
         err = (out[:len(rows)].double() - ref).abs().max().item() / scale
         print(f"   {cin:3d}->{cout:3d} tile (production) {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF  err {err:.2e}", flush=True)
         prod = out.clone()
-        for nt, gg in VAR:
+        perm, nbr_p = rules.dense_order()
+        for nt, gg, ordered in VAR:
             if nt and (cout // 16) % nt:
                 continue
             o2 = torch.empty(V, cout, device="cuda")
-            need = fn(nt, gg, ptr(x), cin, ptr(wt), 27, flip, cout, ptr(rules.nbr), V, ptr(o2), None, 0, s)
+            mp, pp = (nbr_p, ptr(perm)) if ordered else (rules.nbr, None)
+            need = fn(nt, gg, ptr(x), cin, ptr(wt), 27, flip, cout, ptr(mp), pp, V, ptr(o2), None, 0, s)
             ws = torch.empty(need // 4 + 1, device="cuda")
-            args = (nt, gg, ptr(x), cin, ptr(wt), 27, flip, cout, ptr(rules.nbr), V, ptr(o2), ptr(ws), int(need), s)
+            args = (nt, gg, ptr(x), cin, ptr(wt), 27, flip, cout, ptr(mp), pp, V, ptr(o2), ptr(ws), int(need), s)
 
             def fx(args=args):
                 rc = fn(*args)
@@ -84,5 +88,5 @@ for L, size in enumerate(sizes):
             ms = timeit(fx)
             err = (o2[:len(rows)].double() - ref).abs().max().item() / scale
             dprod = ((o2 - prod).abs().max() / prod.abs().max()).item()
-            print(f"   {cin:3d}->{cout:3d} nbr nt{nt} g{gg}        {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF  err {err:.2e}"
+            print(f"   {cin:3d}->{cout:3d} nbr nt{nt} g{gg} o{ordered}     {ms:7.3f} ms {flops / ms / 1e9:6.1f} TF  err {err:.2e}"
                   f"  vs prod {dprod:.1e}", flush=True)

@@ -338,8 +338,9 @@ def test_conv_nbr_accuracy(cin, cout, flip):
     accumulators) against an fp64 evaluation of the same convolution: the
     error bar of the split-bf16 tile form (at most 2x the f32-input MFMA
     kernel's error on the same rulebook, and below 1e-6 of the output
-    scale), and agreement with msp_conv_tile.  Includes c_in not a multiple
-    of 32 (zero k-padding) and a last group of rows past the level."""
+    scale), and agreement with msp_conv_tile; the mask-sorted row order
+    (msp_dense_order) gives bitwise the same rows.  Includes c_in not a
+    multiple of 32 (zero k-padding) and a last group of rows past the level."""
     import ctypes
     from sparseconvnet import _lib, ops
     from sparseconvnet._lib import ptr
@@ -352,7 +353,11 @@ def test_conv_nbr_accuracy(cin, cout, flip):
     assert V % 16 != 0 or V % 128 != 0  # a partial row group or block
     x = torch.randn(V, cin, device=DEV)
     wt = torch.randn(27, cout, cin, device=DEV) / (27 * cin) ** 0.5
+    perm, nbr_p = rules.dense_order()
+    assert sorted(perm.tolist()) == list(range(V))
+    assert torch.equal(nbr_p, rules.nbr[:, perm.long()])
     y = ops.conv_nbr(x, wt, 27, flip, cout, rules.nbr, V)
+    yp = ops.conv_nbr(x, wt, 27, flip, cout, nbr_p, V, perm=perm)
     tl = rules.tiles_for(128)
     yt = torch.empty(V, cout, device=DEV)
     wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(V), 27, cin, cout, 128))
@@ -380,8 +385,13 @@ def test_conv_nbr_accuracy(cin, cout, flip):
     e_g = (y.double() - ref).abs().max().item() / scale
     e_f32 = (y32.double() - ref).abs().max().item() / scale
     e_t = (yt.double() - ref).abs().max().item() / scale
+    e_p = (yp.double() - ref).abs().max().item() / scale
     assert e_g <= max(2.0 * e_f32, 1e-7) and e_g < 1e-6, (e_g, e_f32, e_t)
+    assert e_p <= max(2.0 * e_f32, 1e-7) and e_p < 1e-6, (e_p, e_f32, e_t)
     assert ((y - yt).abs().max().item() / scale) < 2e-6
+    # same row groups' sums per row whatever the order: only the grouping of
+    # zero rows differs, and zero products are exact
+    assert torch.equal(y, yp)
 
 
 def test_subm_conv_large_level_uses_nbr_form():
