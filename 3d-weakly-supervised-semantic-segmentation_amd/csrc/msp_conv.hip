@@ -1039,6 +1039,9 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
+  MSP_REQUIRE(flip >= 0 && flip <= 3, "msp_conv_tile: flip must be 0..3 (got %d)", flip);
+  MSP_REQUIRE(tile_rows == 128 || !(flip & 2),
+              "msp_conv_tile: the [K][c_in][c_out] weight layout (flip bit 1) needs 128-row tiles");
   if (tile_rows == 64) {
     const int64_t n_tb = ceil_div(n_tiles, kWaves);
     const int NT = (c_out / 16) % 2 == 0 ? 2 : 1;

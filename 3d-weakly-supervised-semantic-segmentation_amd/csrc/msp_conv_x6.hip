@@ -76,8 +76,9 @@ __device__ __forceinline__ void split8(const floatx4& a, const floatx4& b, u32x4
 // group ({0-3,12-15,20-27}, ... -- MI355X_MICROARCH.md LDS table) on 16
 // distinct bank quads (r of q covers 0-3 and 12-15, r of q+1 covers 4-11).
 // One thread per unit.
+// wlay 1: wt given as [K][c_in][c_out] (the module's own layout; no transposed copy).
 __global__ __launch_bounds__(256) void split_weights_kernel(const float* __restrict__ wt, int K, int c_out, int c_in,
-                                                            int NC, int KS, u32x4* __restrict__ img) {
+                                                            int NC, int KS, u32x4* __restrict__ img, int wlay = 0) {
   const int K8 = KS / 8, WU = 3 * K8 * NC;
   const int n_y = c_out / NC, nks = (c_in + KS - 1) / KS;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -92,8 +93,14 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float* __restr
   const int k = ks * KS + 8 * k8;
   u32x4 pc[3] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
   if (k < c_in) {  // c_in % 16 == 0: a unit is all data or all padding
-    const floatx4* src = reinterpret_cast<const floatx4*>(wt + ((o * c_out) + cy * NC + n) * c_in + k);
-    split8(src[0], src[1], pc);
+    if (wlay) {
+      const float* src = wt + (o * c_in + k) * c_out + cy * NC + n;
+      split8(floatx4{src[0], src[c_out], src[2 * c_out], src[3 * c_out]},
+             floatx4{src[4 * c_out], src[5 * c_out], src[6 * c_out], src[7 * c_out]}, pc);
+    } else {
+      const floatx4* src = reinterpret_cast<const floatx4*>(wt + ((o * c_out) + cy * NC + n) * c_in + k);
+      split8(src[0], src[1], pc);
+    }
   }
   img[g] = p == 0 ? pc[0] : (p == 1 ? pc[1] : pc[2]);
 }
@@ -721,7 +728,9 @@ int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   u32x4* wimg = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)K * c_out * NKK * 32 * 6 / 16;
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg);
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg,
+                                                                       (flip >> 1) & 1);
+  flip &= 1;
   const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
   bool launched = false;
 #define LP(N, C, R, DD)                                                                                      \
@@ -781,8 +790,8 @@ size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c
 // registers loaded two steps ahead) instead of reloading it per wave.
 // Gathered values run two steps ahead, neighbour indices four; each step's six
 // piece products are summed in a zeroed accumulator and added once.
-template <int NT, int G>
-__global__ __launch_bounds__(kThreads) void conv_x6g_kernel(
+template <int NT, int G, int OCC = 1, int LR = 0>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_x6g_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const int32_t* __restrict__ nbr, const int32_t* __restrict__ perm, int64_t n_rows, int n_y,
     float* __restrict__ out) {
@@ -867,6 +876,35 @@ __global__ __launch_bounds__(kThreads) void conv_x6g_kernel(
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
   auto run = [&](int buf, const Xv& v, uint32_t am) {
+    if constexpr (LR) {
+      // column group outer: three weight fragments live at a time
+      u32x4 xp[G][3];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const bool lo = (v.ok >> g) & 1;
+        const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+        if ((am >> g) & 1) split8(lo ? v.a[g][0] : z, lo ? v.a[g][1] : z, xp[g]);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const u32x4 w0 = wl[buf][(0 * 4 + q) * NC + 16 * t + r];
+        const u32x4 w1 = wl[buf][(1 * 4 + q) * NC + 16 * t + r];
+        const u32x4 w2 = wl[buf][(2 * 4 + q) * NC + 16 * t + r];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if ((am >> g) & 1) {  // wave-uniform
+            floatx4 c = {0.f, 0.f, 0.f, 0.f};
+            c = mfma_bf16(w2, xp[g][0], c);
+            c = mfma_bf16(w1, xp[g][1], c);
+            c = mfma_bf16(w0, xp[g][2], c);
+            c = mfma_bf16(w1, xp[g][0], c);
+            c = mfma_bf16(w0, xp[g][1], c);
+            acc[g][t] += mfma_bf16(w0, xp[g][0], c);
+          }
+        }
+      }
+      return;
+    }
     u32x4 w[NT][3];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -892,27 +930,30 @@ __global__ __launch_bounds__(kThreads) void conv_x6g_kernel(
       }
     }
   };
+  constexpr int NS = LR ? 1 : 2;  // weight staging slots (slices loaded NS steps ahead)
   Wst S[2];
   Ix I[2];
   Xv X[2];
   uint32_t am[2];
   ld_wst(0, S[0]);
-  ld_wst(1, S[1]);
+  if (NS == 2) ld_wst(1, S[1]);
   ld_ix(0, I[0]);
   ld_ix(1, I[1]);
   st_wst(S[0], 0);
-  ld_wst(2, S[0]);
+  ld_wst(NS == 2 ? 2 : 1, S[0]);
   am[0] = ld_x(0, I[0], X[0]);
   am[1] = ld_x(1, I[1], X[1]);
   ld_ix(2, I[0]);
   ld_ix(3, I[1]);
   // step s (slot k = s & 1): wl[k] holds its weight slice, X[k] its values,
-  // S[k ^ 1] the slice of s + 1, I[k] the indices of s + 2, I[k ^ 1] of s + 3
+  // S[k ^ 1] (S[0] with one slot) the slice of s + 1, I[k] the indices of
+  // s + 2, I[k ^ 1] of s + 3
   auto step = [&](int s, auto kc) {
     constexpr int k = decltype(kc)::value;
+    constexpr int sk = NS == 2 ? (k ^ 1) : 0;
     __syncthreads();
-    st_wst(S[k ^ 1], k ^ 1);
-    ld_wst(s + 3, S[k ^ 1]);
+    st_wst(S[sk], k ^ 1);
+    ld_wst(s + 1 + NS, S[sk]);
     run(k, X[k], s < n_steps ? am[k] : 0u);
     am[k] = ld_x(s + 2, I[k], X[k]);
     ld_ix(s + 4, I[k]);
@@ -940,9 +981,10 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
                const int32_t* perm, int64_t n_rows, float* out, void* ws, hipStream_t s, int nt, int g) {
   const int n16 = c_out / 16;
   // NT = 4 (3 for 96 channels) with G = 2: scripts/kbench_nbr.py,
-  // profiles/r01/kbench_nbr_r01v.log
+  // profiles/r01/kbench_nbr_r01v.log; g = 2: the base form (all fragments
+  // first, two staging slots)
   if (nt <= 0) nt = n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1));
-  if (g <= 0) g = 2;
+  if (g <= 0) g = 132;
   if (n16 % nt != 0) {
     set_error("msp_conv_nbr: nt %d does not divide c_out/16 = %d", nt, n16);
     return MSP_EINVAL;
@@ -951,8 +993,10 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   const int nks = (c_in + 31) / 32;
   u32x4* wimg = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)K * c_out * nks * 32 * 6 / 16;
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * nt, 32, wimg);
-  const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)kWaves * 16 * g) * n_y);
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * nt, 32, wimg,
+                                                                       (flip >> 1) & 1);
+  flip &= 1;
+  const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)kWaves * 16 * (g % 10)) * n_y);
   bool launched = false;
 #define LG(N, GG)                                                                                             \
   if (!launched && nt == N && g == GG) {                                                                      \
@@ -962,6 +1006,17 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   }
   LG(4, 2) LG(3, 2) LG(2, 2) LG(1, 2) LG(6, 2) LG(4, 3)
 #undef LG
+#define LL(N, GG, O)                                                                                          \
+  if (!launched && nt == N && g == GG + 10 * O + 100) {                                                       \
+    conv_x6g_kernel<N, GG, O, 1><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, perm, n_rows,  \
+                                                           n_y, out);                                         \
+    launched = true;                                                                                          \
+  }
+  // production (g = 0 -> 132): column-group-outer MFMAs, one staging slot, a 3-waves-per-SIMD register
+  // budget (156 / 142 VGPRs, no spills): 5-12 % over the G = 2 base form within one run
+  // (profiles/r01/kbench_nbr_lr_r01w.log); g = 100 + G + 10 * waves per SIMD selects others
+  LL(4, 2, 3) LL(3, 2, 3) LL(2, 2, 3) LL(1, 2, 3) LL(4, 2, 1) LL(3, 2, 1)
+#undef LL
   if (!launched) {
     set_error("msp_conv_nbr: no dense-group kernel for nt=%d g=%d", nt, g);
     return MSP_EINVAL;
@@ -1246,7 +1301,9 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
   const int64_t n_tiles = ceil_div(n_rows, p.tr);
   u32x4* wsp = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)x6_weight_bytes(K, c_in, c_out, p.ks) / 16;
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * p.nt, p.ks, wsp);
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * p.nt, p.ks, wsp,
+                                                                       (flip >> 1) & 1);
+  flip &= 1;
   float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + round256(x6_weight_bytes(K, c_in, c_out, p.ks)));
   float* dst = p.split > 1 ? part : out;
   const unsigned grid = (unsigned)(n_tiles * p.n_y * p.split);
@@ -1293,6 +1350,12 @@ extern "C" {
 // msp_conv_tile on the headline batch, profiles/r01/kbench_nbr_r01v.log: L0
 // 32->64 -13 %, L1 64->64 -3 %, L2 96->96 -9 %, 192->96 -6 %; the narrow
 // per-wave form stays ahead for c_out = 32 and the shared tile below 10^5 rows).
+static int g_nbr_variant = 0;  // msp_debug_conv_nbr_variant (experiments: scripts/bench_ab.py)
+int msp_debug_conv_nbr_variant(int g) {
+  g_nbr_variant = g;
+  return 0;
+}
+
 int msp_conv_nbr_preferred(int64_t n_rows, int c_in, int c_out) {
   (void)c_in;
   return n_rows >= 100000 && c_out >= 64 && c_out % 16 == 0 ? 1 : 0;
@@ -1313,7 +1376,8 @@ int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int
   MSP_REQUIRE(x && wt && nbr && out, "msp_conv_nbr: null pointer");
   const size_t need = x6g_ws_bytes(K, c_in, c_out);
   MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_nbr: workspace too small (%zu < %zu)", ws_bytes, need);
-  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream), 0, 0);
+  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream), 0,
+                            g_nbr_variant);
   return rc ? rc : check_launch("msp_conv_nbr");
 }
 

@@ -128,9 +128,9 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         cin_p, cout_p = _pad16(cin), _pad16(cout)
         xp = _pad_cols(x.contiguous(), cin_p)
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
-        wt = wp.transpose(1, 2).contiguous()  # [K][cout][cin]
         V = x.size(0)
-        out = conv_tile(xp, wt, K, 0, cout_p, rules, V, "subm_fwd",
+        # flip bit 1: the weights in their own [K][c_in][c_out] layout (no transposed copy)
+        out = conv_tile(xp, wp, K, 2, cout_p, rules, V, "subm_fwd",
                         2.0 * rules.n_rules * cin * cout)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims = rules, (cin, cout)
@@ -165,8 +165,7 @@ class ConvolutionFunction(torch.autograd.Function):
         cin_p, cout_p = _pad16(cin), _pad16(cout)
         xp = _pad_cols(x.contiguous(), cin_p)
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
-        wt = wp.transpose(1, 2).contiguous()
-        out = conv_tile(xp, wt, K, 0, cout_p, rules, n_coarse, "conv_fwd", 2.0 * x.size(0) * cin * cout)
+        out = conv_tile(xp, wp, K, 2, cout_p, rules, n_coarse, "conv_fwd", 2.0 * x.size(0) * cin * cout)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims = rules, (cin, cout)
         return out if cout_p == cout else out[:, :cout].contiguous()

@@ -120,8 +120,10 @@ int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coo
 /* Output-stationary gather-MFMA convolution over a tile rulebook built with
  * the same tile_rows:
  *   out[r, :] = sum over chunks of r's tile: sum_j W'[o]^T x[src_j, :]
- * wt is [K][c_out][c_in] (k contiguous).  If flip, offset o reads
- * wt[K-1-o] (submanifold backward-data with the forward weight layout).
+ * wt is [K][c_out][c_in] (k contiguous).  flip bit 0: offset o reads
+ * wt[K-1-o] (submanifold backward-data with the forward weight layout);
+ * bit 1 (128-row tiles): wt is given as [K][c_in][c_out] instead, the
+ * module's own layout, so the forward needs no transposed copy.
  * c_in % 16 == 0, c_out % 16 == 0.  Every output row is written.
  * tile_rows 64: per-wave tiles; 128 / 256: one tile shared by the 4 waves of
  * a block.  With 128-row tiles and c_out > 32 (or c_in > 64) the contraction
@@ -140,8 +142,8 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
                   msp_stream_t stream);
 /* Dense row-group form of the submanifold convolution, straight from the
  * neighbour map nbr[K][n_rows] (int32, -1 absent, row stride n_rows): same
- * sum as msp_conv_tile over that map's tile rulebook (same flip and weight
- * layout), with every 16 consecutive output rows computed together over all
+ * sum as msp_conv_tile over that map's tile rulebook (same flip bits and weight
+ * layouts), with every 16 consecutive output rows computed together over all
  * K offsets (absent neighbours contribute zero, a group with none of an
  * offset skips it) and accumulated in registers: no tile rulebook needed.
  * Same split-bf16 arithmetic and error class as msp_conv_tile.

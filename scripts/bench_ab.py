@@ -1,0 +1,30 @@
+"""A/B of conv-path variants inside the real training step: runs bench.main()
+once per variant in one process (same box, same batches), prints ms/step.
+Variants (comma list in AB): tile (no dense row groups), nbr0 (dense groups in
+key order), nbr (production: mask-sorted order), g<N> (dense kernel variant N,
+msp_debug_conv_nbr_variant).  Usage: AB=tile,nbr python scripts/bench_ab.py"""
+import io, json, os, sys, contextlib
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
+import __graft_entry__ as g_; g_.add_path()
+import bench
+from sparseconvnet import _lib, metadata
+lib = _lib.load()
+orig_query, orig_order = _lib.query, metadata.SubmRules.dense_order
+res = []
+for v in os.environ.get("AB", "tile,nbr").split(","):
+    _lib.query, metadata.SubmRules.dense_order = orig_query, orig_order
+    lib.msp_debug_conv_nbr_variant(0)
+    if v == "tile":
+        _lib.query = lambda name, *a: 0 if name == "msp_conv_nbr_preferred" else orig_query(name, *a)
+    elif v == "nbr0":
+        metadata.SubmRules.dense_order = lambda self: (None, self.nbr)
+    elif v.startswith("g"):
+        lib.msp_debug_conv_nbr_variant(int(v[1:]))
+    sys.argv = ["bench.py", "--steps", os.environ.get("STEPS", "10"), "--warmup", "2", "--no-cpu"]
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main()
+    line = [l for l in buf.getvalue().splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    res.append((v, d["ms_per_step"]))
+    print(f"{v:8s} {d['ms_per_step']:.2f} ms/step  conv TF/s {d['roofline']['achieved']:.1f}", flush=True)

@@ -428,3 +428,36 @@ def test_subm_conv_large_level_uses_nbr_form():
     close(y, ref, 1e-5, "nbr fwd")
     close(x.grad, dx[:V], 1e-5, "nbr bwd-data")
     close(conv.weight.grad.reshape(27, 64, 64), dw, 1e-5, "nbr dW")
+
+
+@pytest.mark.parametrize("cin,cout,nbr_form", [(32, 32, False), (64, 32, False), (64, 64, False), (96, 192, False),
+                                               (64, 64, True), (96, 96, True)])
+def test_weight_layout_flag(cin, cout, nbr_form):
+    """flip bit 1 (weights in the module's [K][c_in][c_out] layout, no
+    transposed copy) gives bitwise the same output as the [K][c_out][c_in]
+    layout, with and without the flip bit, on every 128-row-tile form and on
+    msp_conv_nbr; 64-row tiles reject it."""
+    from sparseconvnet import _lib, ops
+    from sparseconvnet._lib import ptr
+    torch.manual_seed(cin + 3 * cout)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    rules = t.metadata.level(64).subm_rules(3)
+    V = t.metadata.level(64).n
+    x = torch.randn(V, cin, device=DEV)
+    w = torch.randn(27, cin, cout, device=DEV) / (27 * cin) ** 0.5  # module layout
+    wt = w.transpose(1, 2).contiguous()
+    for flip in (0, 1):
+        if nbr_form:
+            a = ops.conv_nbr(x, wt, 27, flip, cout, rules.nbr, V)
+            b = ops.conv_nbr(x, w, 27, flip | 2, cout, rules.nbr, V)
+        else:
+            a = ops.conv_tile(x, wt, 27, flip, cout, rules, V)
+            b = ops.conv_tile(x, w, 27, flip | 2, cout, rules, V)
+        assert torch.equal(a, b), (flip, (a - b).abs().max().item())
+    tl = rules.tiles_for(64)
+    out = torch.empty(V, cout, device=DEV)
+    rc = _lib.load().msp_conv_tile(ptr(x), cin, ptr(w), 27, 2, cout, 64, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
+                                   ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), None, 0,
+                                   _lib.stream(x.device))
+    assert rc != 0 and b"128-row" in _lib.load().msp_last_error()
