@@ -29,7 +29,7 @@ for f in sorted(glob.glob(os.path.join(root, "pass*", "**", "*counter_collection
                 dur[ctr] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
 fetch = 2.0 * tot["FETCH_SIZE"] / max(ndisp["FETCH_SIZE"], 1)
 write = tot["WRITE_SIZE"] / max(ndisp["WRITE_SIZE"], 1)
-res = {"kernel": "msp_conv_tile", "calls": ndisp["FETCH_SIZE"],
+res = {"kernel": "msp_conv_tile / msp_conv_nbr", "calls": ndisp["FETCH_SIZE"],
        "fetch_bytes_per_call": fetch, "write_bytes_per_call": write, "traffic_bytes_per_call": fetch + write,
        "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE in separate runs of "
                "`bench.py --steps 2 --warmup 1 --no-cpu`; conv kernel + split_weights + split_reduce dispatches per call"}
