@@ -10,7 +10,7 @@ from .sparseConvNetTensor import SparseConvNetTensor
 from .metadata import Metadata
 from .modules import (AddTable, BatchNormalization, BatchNormLeakyReLU, BatchNormReLU, ConcatTable, Convolution,
                       Deconvolution, Identity, InputLayer, JoinTable, MaxPooling, NetworkInNetwork, OutputLayer,
-                      Sequential, SparseToDense, SubmanifoldConvolution, UnPooling)
+                      Sequential, SparseToDense, SubmanifoldConvolution, UnPooling, prefetch_metadata)
 from .networkArchitectures import FullyConvolutionalNet, FullyConvolutionalNetEncoder, UNet
 from .utils import checkpoint_restore, checkpoint_save, is_power2
 from . import _lib
@@ -25,5 +25,5 @@ __all__ = [
     "Deconvolution", "NetworkInNetwork", "UnPooling", "MaxPooling", "BatchNormalization", "BatchNormReLU",
     "BatchNormLeakyReLU", "Sequential", "ConcatTable", "AddTable", "JoinTable", "Identity", "SparseToDense",
     "UNet", "FullyConvolutionalNet", "FullyConvolutionalNetEncoder", "checkpoint_save", "checkpoint_restore",
-    "is_power2", "forward_pass_multiplyAdd_count", "forward_pass_hidden_states",
+    "is_power2", "forward_pass_multiplyAdd_count", "forward_pass_hidden_states", "prefetch_metadata",
 ]

@@ -90,6 +90,7 @@ DENSE_LOG2_WINDOW = 12  # rows of one mask-sorting window of msp_dense_order
 
 class SubmRules:
     def __init__(self, level, filter_size):
+        self._plan, self._key = level.plan, ("subm", level.size, filter_size)
         dev, s = level.device, _lib.stream(level.device)
         K = filter_size ** 3
         self.K, self.filter_size = K, filter_size
@@ -110,6 +111,7 @@ class SubmRules:
         (msp_dense_order: rows sorted by neighbour mask inside 4096-row
         windows), built on first use; (None, nbr) when K > 32."""
         if self._dense is None:
+            self._plan.append(("dense", self._key))
             V, K = self._n, self.K
             if K > 32 or V == 0:
                 self._dense = (None, self.nbr)
@@ -128,6 +130,7 @@ class SubmRules:
         """Tile rulebook with tile_rows-row tiles, built on first use."""
         t = self._tiles.get(tile_rows)
         if t is None:
+            self._plan.append(("tiles", self._key, tile_rows))
             t = self._tiles[tile_rows] = tile_rulebook(self._map, self.K, self._n, self._map.device,
                                                        _lib.stream(self._map.device), tile_rows)
         return t
@@ -137,6 +140,7 @@ class DownRules:
     """Strided (size == stride) relation between a fine and a coarse level."""
 
     def __init__(self, fine, coarse, parent_of, child_start, log2_stride):
+        self._plan, self._key = fine.plan, ("down", fine.size, 1 << log2_stride)
         dev, s = fine.device, _lib.stream(fine.device)
         K = 8 ** log2_stride
         self.K = K
@@ -154,8 +158,9 @@ class DownRules:
 
 
 class Level:
-    def __init__(self, size, log2, keys, n, device):
+    def __init__(self, size, log2, keys, n, device, plan=None):
         self.size, self.log2, self.keys, self.n, self.device = int(size), int(log2), keys, int(n), device
+        self.plan = plan if plan is not None else []
         self._hash = None
         self.subm = {}
         self.down = {}  # stride -> (coarse size, DownRules)
@@ -172,6 +177,7 @@ class Level:
     def subm_rules(self, filter_size):
         r = self.subm.get(filter_size)
         if r is None:
+            self.plan.append(("subm", self.size, filter_size))
             r = self.subm[filter_size] = SubmRules(self, filter_size)
         return r
 
@@ -189,6 +195,9 @@ class Metadata:
         self.device = torch.device(device)
         self.levels = {}
         self.input = None
+        # every lazily built rulebook, in build order: a later Metadata of the
+        # same network can build them all up front (replay, prefetch)
+        self.plan = []
 
     # ------------------------------------------------------------ level 0
     def build_input(self, coords, spatial_size):
@@ -226,7 +235,7 @@ class Metadata:
         call("msp_segment", ptr(skeys), n, 0, ptr(perm), ptr(seg_of), ptr(p2v), ptr(uniq), ptr(vstart), ptr(nu),
              ptr(ws), ws.numel(), s)
         V = int(nu.item())
-        lvl = Level(size, log2, uniq[:max(V, 1)], V, dev)
+        lvl = Level(size, log2, uniq[:max(V, 1)], V, dev, self.plan)
         self.levels[size] = lvl
         self.input = InputRules(n, perm[:n], p2v[:n], vstart[:V + 1], int(max_b) + 1 if n else 0)
         self.input.batch_monotonic = n_desc == 0
@@ -251,6 +260,7 @@ class Metadata:
         hit = fine.down.get(stride)
         if hit is not None:
             return self.levels[hit[0]], hit[1]
+        self.plan.append(("down", fine.size, stride))
         k = stride.bit_length() - 1
         if fine.log2 < k:
             raise ValueError("spatial size too small for this stride")
@@ -268,7 +278,7 @@ class Metadata:
         csize = fine.size // stride
         coarse = self.levels.get(csize)
         if coarse is None:
-            coarse = Level(csize, fine.log2 - k, uniq[:max(Vc, 1)], Vc, dev)
+            coarse = Level(csize, fine.log2 - k, uniq[:max(Vc, 1)], Vc, dev, self.plan)
             self.levels[csize] = coarse
         elif coarse.n != Vc:
             raise RuntimeError("inconsistent coarse level")
@@ -286,9 +296,107 @@ class Metadata:
                                "the matching Convolution/MaxPooling earlier in the same forward")
         return fine, fine.down[int(stride)][1]
 
+    # ------------------------------------------------------------ replay / prefetch
+    def _rules(self, key):
+        kind, size, param = key
+        if kind == "subm":
+            return self.level(size).subm_rules(param)
+        return self.downsample(size, param)[1]
+
+    def replay(self, plan):
+        """Build, in order, the rulebooks another forward of the same network
+        requested (its `plan`); later requests then find them built."""
+        for entry in plan:
+            if entry[0] == "down":
+                self.downsample(entry[1], entry[2])
+            elif entry[0] == "subm":
+                self.level(entry[1]).subm_rules(entry[2])
+            elif entry[0] == "tiles":
+                self._rules(entry[1]).tiles_for(entry[2])
+            elif entry[0] == "dense":
+                self._rules(entry[1]).dense_order()
+
+    def tensors(self):
+        """Every device tensor this metadata holds (for stream bookkeeping)."""
+        out, seen = [], set()
+
+        def walk(v):
+            if torch.is_tensor(v):
+                out.append(v)
+            elif isinstance(v, dict):
+                for x in v.values():
+                    walk(x)
+            elif isinstance(v, (list, tuple)):
+                for x in v:
+                    walk(x)
+            elif isinstance(v, (Level, SubmRules, DownRules, PairLists, InputRules)) and id(v) not in seen:
+                seen.add(id(v))
+                for k, x in vars(v).items():
+                    if k != "_plan" and k != "plan":
+                        walk(x)
+        walk(self.levels)
+        walk(self.input)
+        return out
+
     def locations(self, size):
         lvl = self.level(size)
         out = torch.empty((max(lvl.n, 1), 4), dtype=torch.int64, device=self.device)
         if lvl.n:
             call("msp_decode_keys", ptr(lvl.keys), lvl.n, lvl.log2, ptr(out), _lib.stream(self.device))
         return out[:lvl.n]
+
+
+# ---------------------------------------------------------------- prefetch
+# Input pipelining: the metadata of the NEXT batch (voxelisation, every
+# rulebook the network requested last time) is built on a side stream while
+# the current step's backward still runs on the compute stream; the next
+# InputLayer forward then finds it ready (its stream waits on an event) and
+# the forward issues no device-to-host reads at all.  Nothing is skipped:
+# each batch's metadata is still built once, inside the step before it.
+_PREFETCHED = {}
+_SIDE = {}
+
+
+def _coords_key(coords, spatial_size):
+    return (coords.data_ptr(), tuple(coords.shape), coords.dtype, coords._version, int(spatial_size))
+
+
+def prefetch(coords, spatial_size, plan, wait_for_producer=True):
+    """Build Metadata for `coords` (device, (N, 4) int64) on a side stream.
+    wait_for_producer: order the side stream after all work already queued on
+    the current stream (safe for coords made by queued kernels); False when
+    coords have long been complete on the device (more overlap)."""
+    dev = coords.device
+    if dev.type != "cuda":
+        raise RuntimeError("sparseconvnet.prefetch: coords must be on a HIP device")
+    side = _SIDE.get(dev.index)
+    if side is None:
+        side = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    cur = torch.cuda.current_stream(dev)
+    if wait_for_producer:
+        side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        m = Metadata(dev)
+        m.build_input(coords, spatial_size)
+        m.replay(plan)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    _PREFETCHED[_coords_key(coords, spatial_size)] = (m, ev)
+    return m
+
+
+def take_prefetched(coords, spatial_size):
+    """The Metadata prefetched for these coords (popped), with the current
+    stream ordered after its build and its tensors marked as used by the
+    current stream; None if there is none."""
+    if not _PREFETCHED:
+        return None
+    hit = _PREFETCHED.pop(_coords_key(coords, spatial_size), None)
+    if hit is None:
+        return None
+    m, ev = hit
+    cur = torch.cuda.current_stream(coords.device)
+    cur.wait_event(ev)
+    for t in m.tensors():
+        t.record_stream(cur)
+    return m

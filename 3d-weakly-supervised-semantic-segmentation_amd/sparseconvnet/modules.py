@@ -22,7 +22,7 @@ import torch
 from torch import nn
 
 from . import ops
-from .metadata import Metadata
+from .metadata import Metadata, prefetch, take_prefetched
 from .sparseConvNetTensor import SparseConvNetTensor
 
 
@@ -71,9 +71,13 @@ class InputLayer(nn.Module):
             coords = torch.cat([coords.long(), torch.zeros_like(coords[:, :1]).long()], 1)
         if coords.size(0) != feats.size(0):
             raise ValueError(f"InputLayer: {coords.size(0)} coordinates but {feats.size(0)} feature rows")
-        meta = Metadata(feats.device)
         size = int(self.spatial_size[0])
-        lvl = meta.build_input(coords.long(), size)
+        meta = take_prefetched(coords, size) if coords.is_cuda else None
+        if meta is None:
+            meta = Metadata(feats.device)
+            meta.build_input(coords.long(), size)
+        lvl = meta.level(size)
+        self.last_plan = meta.plan
         rules = meta.input
         if self.mode in (3, 4):
             out = ops.InputLayerFunction.apply(feats, rules, lvl.n, self.mode)
@@ -309,3 +313,19 @@ class SparseToDense(nn.Module):
         idx = ((loc[:, 3] * S + loc[:, 0]) * S + loc[:, 1]) * S + loc[:, 2]
         flat = flat.index_add(0, idx, f)
         return flat.view(B, S, S, S, self.nPlanes).permute(0, 4, 1, 2, 3).contiguous()
+
+
+def prefetch_metadata(model, coords, wait_for_producer=True):
+    """Input pipelining (an addition to the SCN API, optional): build the
+    Metadata of the batch with these coords -- voxelisation and every
+    rulebook the model's last forward requested -- on a side stream now
+    (typically right after the current step's backward/optimizer calls were
+    queued), so the next forward on these coords starts with it ready.
+    Returns the Metadata, or None before the model's first forward."""
+    for m in model.modules():
+        if isinstance(m, InputLayer):
+            plan = getattr(m, "last_plan", None)
+            if plan is None:
+                return None
+            return prefetch(coords.long(), int(m.spatial_size[0]), list(plan), wait_for_producer)
+    return None

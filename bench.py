@@ -142,6 +142,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--residual", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="build each batch's metadata inside its own forward (no side-stream input pipelining)")
     ap.add_argument("--workload", choices=["unet", "contrastive"], default="unet",
                     help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
                          "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
@@ -208,6 +210,10 @@ def main():
             loss = loss + con_loss(*meta)
         loss.backward()
         opt.step()
+        if not args.no_prefetch:
+            # input pipelining: the next batch's voxelisation and rulebooks on a
+            # side stream while this step's backward drains (sparseconvnet.prefetch_metadata)
+            scn.prefetch_metadata(model, batches[(i + 1) % len(batches)][0].coords, wait_for_producer=False)
         return loss
 
     for i in range(args.warmup):
@@ -281,6 +287,8 @@ def main():
                 "scenes_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world}",
+                "input_pipeline": "none" if args.no_prefetch else
+                "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step",
                 "active_voxels_per_step_rank0": batches[0][2],
                 "levels": stats,
                 "fwd_multiply_adds": macs,

@@ -156,3 +156,37 @@ def test_fused_scene_mean_matches_per_point_path(name, m):
         from wsss3d.encoders import segment_mean
         refb = segment_mean(model(xb), xb.batch_offsets)
     _close(outb, refb, 1e-6, "fallback")
+
+
+def test_metadata_prefetch_matches_inline():
+    """sparseconvnet.prefetch_metadata (side-stream build of the next batch's
+    voxelisation and every rulebook the last forward requested) gives bitwise
+    the same logits and parameter gradients as building it inside the
+    forward, and the prefetched forward records the same plan."""
+    import sparseconvnet as scn
+    from wsss3d import EasyDict, MODEL_REGISTRY
+    from wsss3d.synthetic import make_batch
+    torch.manual_seed(0)
+    cls, _ = MODEL_REGISTRY.get("SparseConvUNet")
+    model = cls("SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=1, residual_blocks=True).cuda()
+    bs = [make_batch(2, 20, seed=s) for s in (11, 12)]
+    xs = [EasyDict(coords=torch.from_numpy(b["coords"]).cuda(), feature=torch.from_numpy(b["feats"]).cuda(),
+                   batch_offsets=b["batch_offsets"]) for b in bs]
+
+    def run(x):
+        model.zero_grad(set_to_none=True)
+        out = model(x)
+        out.square().sum().backward()
+        return out.detach().clone(), [p.grad.clone() for p in model.parameters()]
+
+    run(xs[0])                      # records the plan
+    ref_out, ref_g = run(xs[1])     # inline build
+    plan = list(model.encoder[0].last_plan)
+    assert any(e[0] == "down" for e in plan) and any(e[0] == "subm" for e in plan)
+    m = scn.prefetch_metadata(model, xs[1].coords)
+    assert m is not None
+    out, g = run(xs[1])             # consumes the prefetched metadata
+    assert model.encoder[0].last_plan is m.plan
+    assert torch.equal(out, ref_out)
+    for a, b in zip(g, ref_g):
+        assert torch.equal(a, b)
