@@ -91,6 +91,37 @@ def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out):
     return out[:n_out]
 
 
+_WGRAD_SIDE = {}
+WGRAD_CONCURRENT = True  # False: weight gradients inline on the current stream (A/B, debugging)
+
+
+def conv_wgrad_async(x, dy, pairs, pin, pout, K):
+    """conv_wgrad on a side stream, ordered after the work already queued on
+    the current stream, so it runs concurrently with the backward-data
+    launched next on the current stream (both are latency-bound gathers at
+    2-3 waves per SIMD; co-running fills the chip).  Returns (dw, join):
+    join() makes the current stream wait for it -- call it before the
+    backward returns, so everything after this autograd node is ordered
+    after the weight gradient as well."""
+    if not WGRAD_CONCURRENT:
+        return conv_wgrad(x, dy, pairs, pin, pout, K), lambda: None
+    dev = x.device
+    cur = torch.cuda.current_stream(dev)
+    side = _WGRAD_SIDE.get(dev.index)
+    if side is None:
+        side = _WGRAD_SIDE[dev.index] = torch.cuda.Stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        dw = conv_wgrad(x, dy, pairs, pin, pout, K)
+        ev = torch.cuda.Event()
+        ev.record(side)
+
+    def join():
+        cur.wait_event(ev)
+        dw.record_stream(cur)
+    return dw, join
+
+
 def conv_wgrad(x, dy, pairs, pin, pout, K):
     c_in, c_out = x.size(1), dy.size(1)
     dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
@@ -143,14 +174,17 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         K, cin_p, cout_p = wp.shape
         g = _pad_cols(gout.contiguous(), cout_p)
         dx = dw = None
+        join = None
+        if ctx.needs_input_grad[1]:  # weight gradient beside the backward-data
+            p = rules.pairs
+            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K)
+            dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             dxp = conv_tile(g, wp, K, 1, cin_p, rules, xp.size(0), "subm_bwd_data",
                             2.0 * rules.n_rules * cin * cout)
             dx = dxp if cin_p == cin else dxp[:, :cin]
-        if ctx.needs_input_grad[1]:
-            p = rules.pairs
-            dwp = conv_wgrad(xp, g, p, p.pair_in, p.pair_out, K)
-            dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
+        if join is not None:
+            join()
         return dx, dw, None
 
 
@@ -178,12 +212,16 @@ class ConvolutionFunction(torch.autograd.Function):
         g = _pad_cols(gout.contiguous(), cout_p)
         p = rules.pairs
         dx = dw = None
+        join = None
+        if ctx.needs_input_grad[1]:
+            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K)
+            dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             # dx[fine] = W[o] g[parent]: src = coarse (pair_out), dst = fine (pair_in)
             dxp = conv_pairs(g, wp, K, cin_p, p, p.pair_out, p.pair_in, xp.size(0))
             dx = dxp if cin_p == cin else dxp[:, :cin]
-        if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(xp, g, p, p.pair_in, p.pair_out, K)[:, :cin, :cout].reshape(K, 1, cin, cout)
+        if join is not None:
+            join()
         return dx, dw, None, None
 
 
@@ -213,12 +251,16 @@ class DeconvolutionFunction(torch.autograd.Function):
         g = _pad_cols(gout.contiguous(), cout_p)
         p = rules.pairs
         dx = dw = None
+        join = None
+        if ctx.needs_input_grad[1]:
+            dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K)
+            dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             dxp = conv_tile(g, wp, K, 0, cin_p, rules, xp.size(0), "deconv_bwd_data",
                             2.0 * g.size(0) * cin * cout)
             dx = dxp if cin_p == cin else dxp[:, :cin]
-        if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(xp, g, p, p.pair_out, p.pair_in, K)[:, :cin, :cout].reshape(K, 1, cin, cout)
+        if join is not None:
+            join()
         return dx, dw, None, None
 
 
