@@ -92,7 +92,10 @@ def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out):
 
 
 _WGRAD_SIDE = {}
-WGRAD_CONCURRENT = True  # False: weight gradients inline on the current stream (A/B, debugging)
+# True: weight gradients on a side stream beside the backward-data (bench.py --concurrent-wgrad).
+# Off by default: it saved 0.3 ms of 66.9 per step, inside the box-to-box spread, and the
+# co-running kernels stretch each other's event-timed durations (the conv roofline reads low).
+WGRAD_CONCURRENT = False
 
 
 def conv_wgrad_async(x, dy, pairs, pin, pout, K):

@@ -142,8 +142,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--residual", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--serial-wgrad", action="store_true",
-                    help="weight gradients inline on the compute stream (not beside the backward-data)")
+    ap.add_argument("--concurrent-wgrad", action="store_true",
+                    help="weight gradients on a side stream beside the backward-data (sparseconvnet.ops)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="build each batch's metadata inside its own forward (no side-stream input pipelining)")
     ap.add_argument("--workload", choices=["unet", "contrastive"], default="unet",
@@ -167,9 +167,9 @@ def main():
     from wsss3d.synthetic import make_batch
 
     _lib.load()
-    if args.serial_wgrad:
+    if args.concurrent_wgrad:
         from sparseconvnet import ops as scn_ops
-        scn_ops.WGRAD_CONCURRENT = False
+        scn_ops.WGRAD_CONCURRENT = True
     # two distinct batches per rank, alternated step to step
     host_batches = [make_batch(args.batch, args.scale, seed=1000 * rank + k) for k in range(2)]
     contrastive = args.workload == "contrastive"
