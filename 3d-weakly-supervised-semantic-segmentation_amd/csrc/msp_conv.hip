@@ -1208,6 +1208,63 @@ int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out) {
   return n < 1 ? 1 : n;
 }
 
+// The banded form is correct (tests/test_gpu_ops.py::test_conv_wgrad_band) but
+// measured 1.8-2.2x slower than the pair-list form (profiles/r01/
+// kbench_wgrad_band_r01zz.log): 8-11 % of the pairs have their input row
+// outside a 256-row band's +-64-row halo in key order (Morton neighbours
+// jump), nearly every 32-pair step then waits on one un-prefetched global
+// load.  Off unless msp_debug_wgrad_band(1).
+static int g_wgrad_band_on = 0;
+int msp_debug_wgrad_band(int on) {
+  g_wgrad_band_on = on;
+  return MSP_OK;
+}
+
+int msp_wgrad_band_ok(int64_t n_rows, int K, int c_in, int c_out) {
+  if (!g_wgrad_band_on) return 0;
+  return n_rows > 0 && K >= 1 && K <= 32 && c_in % 32 == 0 && c_out % 32 == 0 && c_in > 0 && c_out > 0 ? 1 : 0;
+}
+
+int64_t msp_wgrad_band_groups(int64_t n_rows, int c_in, int c_out) {
+  if (n_rows <= 0 || c_in < 32 || c_out < 32) return 1;
+  int S;
+  return wgrad_band_groups(n_rows, c_in, c_out, S);
+}
+
+int64_t msp_wgrad_band_seg_len(int64_t n_rows, int K) {
+  return (int64_t)K * (wgrad_band_n_sub(n_rows > 0 ? n_rows : 1) + 1);
+}
+
+int msp_wgrad_band_segments(const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_rows, int64_t* seg,
+                            msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && n_rows >= 0, "msp_wgrad_band_segments: bad arguments");
+  if (n_rows == 0) return MSP_OK;
+  launch_wgrad_band_seg(pair_out, off_start, K, n_rows, seg, as_stream(stream));
+  return check_launch("msp_wgrad_band_segments");
+}
+
+int msp_conv_wgrad_band(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
+                        const int32_t* pair_out, const int64_t* seg, int K, int64_t n_rows, float* slab, float* dw,
+                        msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && K <= 32 && c_in % 32 == 0 && c_out % 32 == 0 && c_in > 0 && c_out > 0,
+              "msp_conv_wgrad_band: needs K <= 32 and channels in multiples of 32 (K=%d c_in=%d c_out=%d)", K, c_in,
+              c_out);
+  hipStream_t s = as_stream(stream);
+  const int64_t cc = (int64_t)c_in * c_out;
+  if (n_rows <= 0) {
+    MSP_HIP(hipMemsetAsync(dw, 0, (size_t)K * cc * sizeof(float), s), "msp_conv_wgrad_band");
+    return MSP_OK;
+  }
+  int S;
+  const int64_t n_groups = wgrad_band_groups(n_rows, c_in, c_out, S);
+  MSP_REQUIRE(launch_wgrad_band(x, c_in, dy, c_out, pair_in, pair_out, seg, K, n_rows, n_groups, S, slab, s) ==
+                  MSP_OK,
+              "msp_conv_wgrad_band: no kernel for K=%d", K);
+  dim3 g2((unsigned)ceil_div(cc, 64), (unsigned)K);
+  wgrad_reduce_kernel<<<g2, 256, 0, s>>>(slab, n_groups, K, cc, dw);
+  return check_launch("msp_conv_wgrad_band");
+}
+
 int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
                    const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
                    float* dw, msp_stream_t stream) {

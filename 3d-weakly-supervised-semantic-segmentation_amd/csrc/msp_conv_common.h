@@ -88,4 +88,13 @@ int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const 
                     hipStream_t s);
 void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb);
 
+// Banded submanifold weight gradient (msp_conv_x6.hip): rows staged in LDS.
+int64_t wgrad_band_n_sub(int64_t n_rows);
+int64_t wgrad_band_groups(int64_t n_rows, int c_in, int c_out, int& S);
+int launch_wgrad_band(const float* x, int c_in, const float* dy, int c_out, const int32_t* pin,
+                      const int32_t* pout, const int64_t* seg, int K, int64_t n_rows, int64_t n_groups, int S,
+                      float* slab, hipStream_t s);
+int launch_wgrad_band_seg(const int32_t* pout, const int64_t* off_start, int K, int64_t n_rows, int64_t* seg,
+                          hipStream_t s);
+
 }  // namespace msp

@@ -1193,6 +1193,233 @@ __global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
   }
 }
 
+// ---------------------------------------------------------------- banded weight gradient
+// Submanifold weight gradients with the rows staged in LDS.  The pair-list
+// kernel above reads x and dy per pair from global memory; at levels 0-1 its
+// L2 hit rate is 0.17-0.23 and it fetches 7-8x the compulsory bytes from
+// HBM (profiles/r01/pmc_wgrad_pieces_r01zz.txt).  Here a block owns one
+// 32 x 32 dW tile (input channels m0.., output channels n0..) and a group of
+// S consecutive 256-row bands of output rows; per band it stages dy[band]
+// and x[band - 64 .. band + 256 + 64) (its 32-channel slices) in LDS once,
+// then every wave runs the pairs of its offsets (o = wave, wave + 4, ...)
+// whose output row is in the band -- the pair lists are sorted by output
+// row inside each offset, seg[o][band] gives the segment -- reading x and
+// dy from LDS (x rows outside the staged range from global memory).  MFMA
+// operands and split arithmetic as wgrad_x6_kernel<2, 2>: lane (r, q) takes
+// pairs 8q..8q+7 of a 32-pair step, input channels m0 + 2r + {0,1} and output
+// channels n0 + 2r + {0,1}; accumulator (oi, sa, sb) register j holds
+// dW[o][m0 + 2 (4q + j) + sa][n0 + 2r + sb].  Each block writes its tile of
+// every offset to slab[group][o] (reduced in group order by
+// wgrad_reduce_kernel: deterministic).
+constexpr int kBandRows = 256, kBandHalo = 64, kBandX = kBandRows + 2 * kBandHalo;
+
+__global__ __launch_bounds__(256) void wgrad_band_seg_kernel(const int32_t* __restrict__ pout,
+                                                             const int64_t* __restrict__ off_start, int K,
+                                                             int64_t n_sub, int64_t* __restrict__ seg) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)K * (n_sub + 1)) return;
+  const int o = (int)(t / (n_sub + 1));
+  const int64_t sb = t % (n_sub + 1);
+  int64_t lo = off_start[o], hi = off_start[o + 1];
+  const int64_t key = sb * kBandRows;
+  while (lo < hi) {  // first pair of offset o with output row >= key
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)pout[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  seg[t] = lo;
+}
+
+template <int NO, int NW = kWaves>
+__global__ __launch_bounds__(64 * NW) void wgrad_band_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
+    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ seg, int K,
+    int64_t n_rows, int64_t n_sub, int S, int n_tiles, float* __restrict__ slab) {
+  __shared__ floatx2 xs[kBandX * 16];      // [row][16] float2 = 32 channels
+  __shared__ floatx2 ys[kBandRows * 16];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int tile = (int)(lb % n_tiles);
+  const int64_t grp = lb / n_tiles;
+  const int n_tn = c_out / 32;
+  const int m0 = (tile / n_tn) * 32, n0 = (tile % n_tn) * 32;
+  const int64_t sb0 = grp * S;
+  const int64_t sb1 = sb0 + S < n_sub ? sb0 + S : n_sub;
+
+  floatx4 acc[NO][2][2];
+#pragma unroll
+  for (int oi = 0; oi < NO; ++oi)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[oi][a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t sb = sb0; sb < sb1; ++sb) {
+    const int64_t j0 = sb * kBandRows, xlo = j0 - kBandHalo;
+    __syncthreads();  // the previous band's reads are done
+    for (int u = tid; u < kBandX * 8; u += 64 * NW) {
+      const int row = u >> 3, c4 = u & 7;
+      const int64_t gr = xlo + row;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gr >= 0 && gr < n_rows) v = *reinterpret_cast<const floatx4*>(x + gr * c_in + m0 + 4 * c4);
+      *reinterpret_cast<floatx4*>(&xs[row * 16 + 2 * c4]) = v;
+    }
+    for (int u = tid; u < kBandRows * 8; u += 64 * NW) {
+      const int row = u >> 3, c4 = u & 7;
+      const int64_t gr = j0 + row;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gr < n_rows) v = *reinterpret_cast<const floatx4*>(dy + gr * c_out + n0 + 4 * c4);
+      *reinterpret_cast<floatx4*>(&ys[row * 16 + 2 * c4]) = v;
+    }
+    __syncthreads();
+    // the wave's offsets o = wave + 4 oi; every offset's segment runs an even
+    // number of 32-pair steps (a trailing empty step at most) through two
+    // index slots, slot 0 holding even steps: the indices of the next step
+    // (the next offset's first at a segment's end) load one step ahead, with
+    // no register copies (static slots keep the wait counts exact)
+    int64_t pbs[NO], pes[NO];
+#pragma unroll
+    for (int oi = 0; oi < NO; ++oi) {
+      const int o = wave + NW * oi < K ? wave + NW * oi : K - 1;
+      const int64_t* so = seg + (int64_t)o * (n_sub + 1);
+      pbs[oi] = wave + NW * oi < K ? so[sb] : 0;
+      pes[oi] = wave + NW * oi < K ? so[sb + 1] : 0;
+    }
+    struct Ix {
+      int i[8], j[8];
+    };
+    auto ld_ix = [&](int64_t p, int64_t pe, Ix& d) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int64_t pp = p + 8 * q + k;
+        const int64_t pc = pp < pe ? pp : (pe > 0 ? pe - 1 : 0);
+        d.i[k] = pin[pc];
+        d.j[k] = pout[pc];
+      }
+    };
+    auto step = [&](int oi, int64_t p, int64_t pe, const Ix& d) {
+      float a[8][2], b[8][2];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool live = p + 8 * q + k < pe;
+        const int xi = d.i[k] - (int)xlo;
+        const int jj = d.j[k] - (int)j0;
+        const bool inb = (unsigned)xi < (unsigned)kBandX;
+        const floatx2 xl = xs[(inb ? xi : 0) * 16 + r];  // LDS, or global for rows outside the staged range
+        floatx2 xg = {0.f, 0.f};
+        if (!inb) xg = *reinterpret_cast<const floatx2*>(x + (int64_t)d.i[k] * c_in + m0 + 2 * r);
+        const floatx2 xa = inb ? xl : xg;
+        const floatx2 yb = ys[((unsigned)jj < (unsigned)kBandRows ? jj : 0) * 16 + r];
+        a[k][0] = live ? xa[0] : 0.f;
+        a[k][1] = live ? xa[1] : 0.f;
+        b[k][0] = yb[0];
+        b[k][1] = yb[1];
+      }
+      u32x4 bp[2][3];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        split8(floatx4{b[0][t], b[1][t], b[2][t], b[3][t]}, floatx4{b[4][t], b[5][t], b[6][t], b[7][t]}, bp[t]);
+#pragma unroll
+      for (int sa = 0; sa < 2; ++sa) {
+        u32x4 ap[3];
+        split8(floatx4{a[0][sa], a[1][sa], a[2][sa], a[3][sa]}, floatx4{a[4][sa], a[5][sa], a[6][sa], a[7][sa]},
+               ap);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          floatx4 c = acc[oi][sa][t];
+          c = mfma_bf16(ap[2], bp[t][0], c);
+          c = mfma_bf16(ap[1], bp[t][1], c);
+          c = mfma_bf16(ap[0], bp[t][2], c);
+          c = mfma_bf16(ap[1], bp[t][0], c);
+          c = mfma_bf16(ap[0], bp[t][1], c);
+          acc[oi][sa][t] = mfma_bf16(ap[0], bp[t][0], c);
+        }
+      }
+    };
+    Ix S2[2];
+    ld_ix(pbs[0], pes[0], S2[0]);
+#pragma unroll
+    for (int oi = 0; oi < NO; ++oi) {
+      if (wave + NW * oi >= K) break;  // wave-uniform
+      const int64_t pb = pbs[oi], pe = pes[oi];
+      const int64_t nst = ((pe - pb + 31) / 32 + 1) & ~(int64_t)1;  // even step count
+      // where the step after this segment starts: the next offset's first
+      const int64_t nb = oi + 1 < NO ? pbs[oi + 1 < NO ? oi + 1 : oi] : 0;
+      const int64_t ne = oi + 1 < NO ? pes[oi + 1 < NO ? oi + 1 : oi] : 0;
+      if (nst == 0) {
+        ld_ix(nb, ne, S2[0]);
+        continue;
+      }
+      for (int64_t t = 0; t < nst; t += 2) {
+        const int64_t p = pb + 32 * t;
+        ld_ix(p + 32, pe, S2[1]);
+        if (p < pe) step(oi, p, pe, S2[0]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S2[0].i[k]), "v"(S2[0].j[k]));
+        if (t + 2 < nst) ld_ix(p + 64, pe, S2[0]);
+        else ld_ix(nb, ne, S2[0]);
+        if (p + 32 < pe) step(oi, p + 32, pe, S2[1]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S2[1].i[k]), "v"(S2[1].j[k]));
+      }
+    }
+  }
+  const int64_t cc = (int64_t)c_in * c_out;
+#pragma unroll
+  for (int oi = 0; oi < NO; ++oi) {
+    const int o = wave + NW * oi;
+    if (o >= K) break;
+    float* so = slab + (grp * K + o) * cc;
+#pragma unroll
+    for (int sa = 0; sa < 2; ++sa)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          so[(int64_t)(m0 + 2 * (4 * q + j) + sa) * c_out + n0 + 2 * r + t] = acc[oi][sa][t][j];
+  }
+}
+
+int64_t wgrad_band_n_sub(int64_t n_rows) { return ceil_div(n_rows, (int64_t)kBandRows); }
+
+// band groups per launch: about 512 blocks (2 per CU at 80 KiB of LDS each)
+int64_t wgrad_band_groups(int64_t n_rows, int c_in, int c_out, int& S) {
+  const int64_t n_sub = wgrad_band_n_sub(n_rows);
+  const int64_t n_tiles = (int64_t)(c_in / 32) * (c_out / 32);
+  int64_t sp = ceil_div(n_sub * n_tiles, (int64_t)512);
+  if (sp < 1) sp = 1;
+  S = (int)sp;
+  return ceil_div(n_sub, sp);
+}
+
+int launch_wgrad_band(const float* x, int c_in, const float* dy, int c_out, const int32_t* pin,
+                      const int32_t* pout, const int64_t* seg, int K, int64_t n_rows, int64_t n_groups, int S,
+                      float* slab, hipStream_t s) {
+  const int n_tiles = (c_in / 32) * (c_out / 32);
+  const unsigned grid = (unsigned)(n_groups * n_tiles);
+  const int64_t n_sub = wgrad_band_n_sub(n_rows);
+  const int no = (K + 7) / 8;  // 8 waves per block, offsets o = wave + 8 oi
+#define LB(N)                                                                                                \
+  if (no <= N) {                                                                                             \
+    wgrad_band_kernel<N, 8><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, pin, pout, seg, K, n_rows, n_sub, S,      \
+                                                 n_tiles, slab);                                             \
+    return MSP_OK;                                                                                           \
+  }
+  LB(1) LB(4)
+#undef LB
+  return MSP_EINVAL;
+}
+
+int launch_wgrad_band_seg(const int32_t* pout, const int64_t* off_start, int K, int64_t n_rows, int64_t* seg,
+                          hipStream_t s) {
+  const int64_t n_sub = wgrad_band_n_sub(n_rows);
+  const int64_t n = (int64_t)K * (n_sub + 1);
+  wgrad_band_seg_kernel<<<(unsigned)ceil_div(n, (int64_t)256), 256, 0, s>>>(pout, off_start, K, n_sub, seg);
+  return MSP_OK;
+}
+
 // dW tile of the x6 weight gradient: WA in {4, 3, 2, 1} (largest dividing
 // c_in / 16), WB in {2, 1} (registers: two value sets of 8 pairs each).
 void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb) {

@@ -125,6 +125,25 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K):
     return dw, join
 
 
+def conv_wgrad_band(x, dy, pairs, K, n_rows):
+    """Submanifold weight gradient with the rows staged in LDS per 256-row band
+    (msp_conv_wgrad_band); pairs = the rules' pair lists (ascending output row
+    per offset), their band segments cached on them."""
+    c_in, c_out = x.size(1), dy.size(1)
+    seg = getattr(pairs, "_band_seg", None)
+    if seg is None:
+        seg = torch.empty(int(_lib.query("msp_wgrad_band_seg_len", _lib.I64(n_rows), K)), dtype=torch.int64,
+                          device=x.device)
+        call("msp_wgrad_band_segments", ptr(pairs.pair_out), ptr(pairs.off_start), K, n_rows, ptr(seg), _stream(x))
+        pairs._band_seg = seg
+    dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
+    n_groups = int(_lib.query("msp_wgrad_band_groups", _lib.I64(n_rows), c_in, c_out))
+    slab = torch.empty((n_groups, K, c_in, c_out), dtype=torch.float32, device=x.device)
+    call("msp_conv_wgrad_band", ptr(x), c_in, ptr(dy), c_out, ptr(pairs.pair_in), ptr(pairs.pair_out), ptr(seg), K,
+         n_rows, ptr(slab), ptr(dw), _stream(x))
+    return dw
+
+
 def conv_wgrad(x, dy, pairs, pin, pout, K):
     c_in, c_out = x.size(1), dy.size(1)
     dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
@@ -178,9 +197,13 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         g = _pad_cols(gout.contiguous(), cout_p)
         dx = dw = None
         join = None
-        if ctx.needs_input_grad[1]:  # weight gradient beside the backward-data
+        if ctx.needs_input_grad[1]:
             p = rules.pairs
-            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K)
+            V = xp.size(0)
+            if int(_lib.query("msp_wgrad_band_ok", _lib.I64(V), K, cin_p, cout_p)):
+                dwp = conv_wgrad_band(xp, g, p, K, V)  # rows staged in LDS per band
+            else:  # weight gradient beside the backward-data (opt-in)
+                dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             dxp = conv_tile(g, wp, K, 1, cin_p, rules, xp.size(0), "subm_bwd_data",

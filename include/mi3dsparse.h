@@ -184,6 +184,26 @@ int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const i
                    const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
                    float* dw, msp_stream_t stream);
 
+/* Banded weight gradient for submanifold rules (pairs of each offset in
+ * ascending pair_out, as msp_pair_lists makes them): a block owns a 32 x 32
+ * dW tile and a group of 256-row bands of output rows, stages each band's dy
+ * rows and the x rows around it in LDS once and runs every offset's pairs of
+ * the band from there (instead of one global load per pair).  seg[K][n_sub+1]
+ * (msp_wgrad_band_segments, once per pair lists) = first pair of offset o
+ * with output row >= 256 s.  slab: msp_wgrad_band_groups(...) x K x c_in x
+ * c_out floats; the groups are reduced in order (deterministic).
+ * Requires K <= 32 and c_in, c_out multiples of 32.  msp_wgrad_band_ok says
+ * whether the library prefers it for a shape: not yet (measured slower than
+ * msp_conv_wgrad), so it answers 0. */
+int msp_wgrad_band_ok(int64_t n_rows, int K, int c_in, int c_out);
+int64_t msp_wgrad_band_groups(int64_t n_rows, int c_in, int c_out);
+int64_t msp_wgrad_band_seg_len(int64_t n_rows, int K);
+int msp_wgrad_band_segments(const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_rows, int64_t* seg,
+                            msp_stream_t stream);
+int msp_conv_wgrad_band(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
+                        const int32_t* pair_out, const int64_t* seg, int K, int64_t n_rows, float* slab, float* dw,
+                        msp_stream_t stream);
+
 /* ---------------- batch norm + (leaky) ReLU (replaces SCN BatchNormalization
  * with leakiness; scn.BatchNormReLU / BatchNormLeakyReLU).
  * Per-channel statistics are one float array stats[5][C]: mean_hi, mean_lo

@@ -21,7 +21,7 @@ BLOCKS = [int(v) for v in os.environ.get("BLOCKS", "0").split(",")]
 MODES = [int(v) for v in os.environ.get("MODES", "0,1").split(",")]
 lib.msp_debug_wgrad_abl(int(os.environ.get("ABL", "0")))
 for (L, size, ci, c), mode, nb in [(cs, m, nb) for cs in cases for m in MODES for nb in BLOCKS]:
-    lib.msp_debug_wgrad_f32(mode)
+    lib.msp_debug_wgrad_f32(1 if mode == 1 else 0)
     lib.msp_debug_wgrad_blocks(nb)
     rules = meta.level(size).subm_rules(3)
     p = rules.pairs
@@ -29,13 +29,16 @@ for (L, size, ci, c), mode, nb in [(cs, m, nb) for cs in cases for m in MODES fo
     torch.manual_seed(L)
     x = torch.randn(V, ci, device="cuda")
     dy = torch.randn(V, c, device="cuda")
+    # mode 2: banded form (msp_conv_wgrad_band), else the pair-list form (mode 1: f32 MFMA)
+    fw = (lambda: ops.conv_wgrad_band(x, dy, p, 27, V)) if mode == 2 else \
+        (lambda: ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27))
     for _ in range(2):
-        dw = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
+        dw = fw()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(10):
-        ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
+        fw()
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 10
@@ -47,6 +50,6 @@ for (L, size, ci, c), mode, nb in [(cs, m, nb) for cs in cases for m in MODES fo
         ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
         err = max(err, ((dw[o].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item())
     flops = 2.0 * rules.n_rules * ci * c
-    print(f"L{L} {ci:3d}->{c:3d} {'f32' if mode else 'x6 '} blocks~{nb or 4096} V={V} R={rules.n_rules} "
+    print(f"L{L} {ci:3d}->{c:3d} {['x6 ', 'f32', 'band'][mode]} blocks~{nb or 4096} V={V} R={rules.n_rules} "
           f"pieces={_lib.query('msp_wgrad_pieces', _lib.I64(p.total), 27, ci, c)}: {ms:.3f} ms "
           f"{flops / ms / 1e9:.1f} TF  max rel err {err:.2e}", flush=True)

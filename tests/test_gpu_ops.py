@@ -461,3 +461,42 @@ def test_weight_layout_flag(cin, cout, nbr_form):
                                    ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), None, 0,
                                    _lib.stream(x.device))
     assert rc != 0 and b"128-row" in _lib.load().msp_last_error()
+
+
+@pytest.mark.parametrize("cin,cout,size", [(32, 32, 4096), (64, 32, 4096), (32, 64, 64), (96, 96, 64),
+                                           (64, 128, 64), (160, 96, 64)])
+def test_conv_wgrad_band(cin, cout, size):
+    """msp_conv_wgrad_band (rows staged in LDS per 256-row band) against fp64
+    per-offset x^T dy sums and against the pair-list form: fp32-class error
+    (< 2e-6 of each offset's max), on a multi-band level with a partial last
+    band and pairs whose input row lies outside the staged halo."""
+    from sparseconvnet import ops, _lib
+    _lib.load().msp_debug_wgrad_band(1)
+    torch.manual_seed(cin + cout + size)
+    if size == 4096:
+        b = make_batch(1, 50, seed=9)
+        coords, feats = torch.from_numpy(b["coords"]), torch.from_numpy(b["feats"])
+    else:
+        coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, size, mode=4)([coords.to(DEV), feats.to(DEV)])
+    lvl = t.metadata.level(size)
+    V = lvl.n
+    p = lvl.subm_rules(3).pairs
+    x = torch.randn(V, cin, device=DEV)
+    dy = torch.randn(V, cout, device=DEV)
+    dw = ops.conv_wgrad_band(x, dy, p, 27, V)
+    dw2 = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
+    offs = p.off_start.cpu().tolist()
+    pin, pout = p.pair_in.long(), p.pair_out.long()
+    far = 0
+    for o in range(27):
+        s0, s1 = offs[o], offs[o + 1]
+        ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
+        scale = ref.abs().max().clamp_min(1e-30)
+        assert ((dw[o].double() - ref).abs().max() / scale).item() < 2e-6, o
+        assert ((dw2[o].double() - ref).abs().max() / scale).item() < 2e-6, o
+        band0 = (pout[s0:s1] // 256) * 256
+        far += int(((pin[s0:s1] < band0 - 64) | (pin[s0:s1] >= band0 + 256 + 64)).sum())
+    if size == 4096:
+        assert V > 256 * 8 and V % 256 != 0 and far > 0, (V, far)
+    _lib.load().msp_debug_wgrad_band(0)
