@@ -43,10 +43,14 @@ struct BnStats {
 // Vector form (C % 4 == 0, C <= 1024): each thread owns 4 channels (one
 // float4 column) and strides over rows with 4 independent loads in flight;
 // R = 256 / (C/4) rows are covered per pass and folded in LDS in fixed order.
+// MODE 2: residual join fused with the statistics of its output: x = a,
+// dy = b, sum = a + b is written to sum_out and reduced as in MODE 0 (same
+// partition and order as msp_bn_stats on the sum: identical partials).
 template <int MODE>
 __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                         int64_t V, int C, const float* __restrict__ stats,
-                                                        float leak, double* __restrict__ partial) {
+                                                        float leak, double* __restrict__ partial,
+                                                        float* __restrict__ sum_out = nullptr) {
   __shared__ double red[kT][8];
   const int64_t P = gridDim.x;
   const int64_t per = (V + P - 1) / P;
@@ -73,7 +77,7 @@ __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict_
     const float gs[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (MODE == 0) {
+      if (MODE != 1) {
         s0[k] += xs[k];
         s1[k] += (double)xs[k] * xs[k];
       } else {
@@ -88,18 +92,38 @@ __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict_
   if (ro < R) {
     const float4* x4 = reinterpret_cast<const float4*>(x);
     const float4* g4 = reinterpret_cast<const float4*>(dy);
+    float4* s4 = reinterpret_cast<float4*>(sum_out);
+    auto join = [&](int64_t e, const float4& a, const float4& b) {  // MODE 2: the residual sum
+      const float4 sm = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      s4[e] = sm;
+      return sm;
+    };
     int64_t v = v0 + ro;
     for (; v + 3 * R < v1; v += 4 * R) {
       float4 xa[4], ga[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         xa[u] = x4[(v + u * R) * C4 + c4];
-        if (MODE == 1) ga[u] = g4[(v + u * R) * C4 + c4];
+        if (MODE != 0) ga[u] = g4[(v + u * R) * C4 + c4];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) term(xa[u], MODE == 1 ? ga[u] : xa[u]);
+      for (int u = 0; u < 4; ++u) {
+        if (MODE == 2) {
+          const float4 sm = join((v + u * R) * C4 + c4, xa[u], ga[u]);
+          term(sm, sm);
+        } else {
+          term(xa[u], MODE == 1 ? ga[u] : xa[u]);
+        }
+      }
     }
-    for (; v < v1; v += R) term(x4[v * C4 + c4], MODE == 1 ? g4[v * C4 + c4] : x4[v * C4 + c4]);
+    for (; v < v1; v += R) {
+      if (MODE == 2) {
+        const float4 sm = join(v * C4 + c4, x4[v * C4 + c4], g4[v * C4 + c4]);
+        term(sm, sm);
+      } else {
+        term(x4[v * C4 + c4], MODE == 1 ? g4[v * C4 + c4] : x4[v * C4 + c4]);
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -294,7 +318,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
                                                           int64_t V, const double* __restrict__ sums,
                                                           const float* __restrict__ stats,
                                                           const float* __restrict__ weight, float leak, int train,
-                                                          float* __restrict__ dx) {
+                                                          const float* __restrict__ addend, float* __restrict__ dx) {
   const int64_t stride = (int64_t)gridDim.x * kT;
   const double invV = V > 0 ? 1.0 / (double)V : 0.0;
   const BnStats st(stats, C);
@@ -306,9 +330,11 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
     if (train) {
       const float xh = st.centred(xv, c) * st.is[c];
       const float mdz = (float)(sums[c] * invV), mdzx = (float)(sums[C + c] * invV);
-      dx[i] = w * st.is[c] * (dz - mdz - xh * mdzx);
+      const float d = w * st.is[c] * (dz - mdz - xh * mdzx);
+      dx[i] = addend ? d + addend[i] : d;
     } else {
-      dx[i] = w * st.is[c] * dz;
+      const float d = w * st.is[c] * dz;
+      dx[i] = addend ? d + addend[i] : d;
     }
   }
 }
@@ -319,7 +345,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply4_kernel(const float* __restri
                                                            const double* __restrict__ sums,
                                                            const float* __restrict__ stats,
                                                            const float* __restrict__ weight, float leak, int train,
-                                                           float* __restrict__ dx) {
+                                                           const float* __restrict__ addend, float* __restrict__ dx) {
   const int C4 = C >> 2, R = kT / C4;
   const int t = threadIdx.x, c4 = t % C4, ro = t / C4;
   if (ro >= R) return;
@@ -350,7 +376,12 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply4_kernel(const float* __restri
   };
   for (int64_t v = (int64_t)blockIdx.x * R + ro; v < V; v += step) {
     const float4 a = x4[v * C4 + c4], g = g4[v * C4 + c4];
-    d4[v * C4 + c4] = make_float4(f(a.x, g.x, 0), f(a.y, g.y, 1), f(a.z, g.z, 2), f(a.w, g.w, 3));
+    float4 d = make_float4(f(a.x, g.x, 0), f(a.y, g.y, 1), f(a.z, g.z, 2), f(a.w, g.w, 3));
+    if (addend) {  // uniform: the other consumer's gradient of x (residual fork), one add as autograd's
+      const float4 e = reinterpret_cast<const float4*>(addend)[v * C4 + c4];
+      d = make_float4(d.x + e.x, d.y + e.y, d.z + e.z, d.w + e.w);
+    }
+    d4[v * C4 + c4] = d;
   }
 }
 
@@ -362,6 +393,12 @@ inline unsigned rows_grid(int64_t V, int C) {
   int64_t g = (V + R - 1) / R;
   if (g > 4096) g = 4096;
   return (unsigned)(g < 1 ? 1 : g);
+}
+
+__global__ __launch_bounds__(kT) void add_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                                                 float* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * kT;
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) out[i] = a[i] + b[i];
 }
 
 inline unsigned ew_grid(int64_t n) {
@@ -421,9 +458,10 @@ int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const fl
   return check_launch("msp_bn_bwd_stats");
 }
 
-int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,
-                     const float* weight, float leak, int train, float* dx, float* dweight, float* dbias,
-                     msp_stream_t stream) {
+int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, const double* partial,
+                         const float* stats, const float* weight, float leak, int train, const float* addend,
+                         float* dx, float* dweight, float* dbias, msp_stream_t stream) {
+  MSP_REQUIRE(addend == nullptr || addend != dx || V * C == 0, "msp_bn_bwd_apply_add: addend must not alias dx");
   hipStream_t s = as_stream(stream);
   // The combined per-channel sums go to the extra 2*C doubles at the tail of
   // the partial buffer (it holds (P + 1) * 2 * C doubles, see the header).
@@ -431,12 +469,36 @@ int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const do
   bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V), C, dweight, dbias, sums);
   const int64_t n = V * C;
   if (n > 0) {
-    if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx))
-      bn_bwd_apply4_kernel<<<rows_grid(V, C), kT, 0, s>>>(x, dy, V, C, sums, stats, weight, leak, train, dx);
+    if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx) &&
+        (addend == nullptr || aligned16(addend)))
+      bn_bwd_apply4_kernel<<<rows_grid(V, C), kT, 0, s>>>(x, dy, V, C, sums, stats, weight, leak, train, addend,
+                                                          dx);
     else
-      bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, dx);
+      bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, addend, dx);
   }
   return check_launch("msp_bn_bwd_apply");
+}
+
+int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,
+                     const float* weight, float leak, int train, float* dx, float* dweight, float* dbias,
+                     msp_stream_t stream) {
+  return msp_bn_bwd_apply_add(x, dy, V, C, partial, stats, weight, leak, train, nullptr, dx, dweight, dbias,
+                              stream);
+}
+
+int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,
+                     msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_add_bn_stats: bad shape");
+  MSP_REQUIRE((sum != a && sum != b) || V * C == 0, "msp_add_bn_stats: sum must not alias an input");
+  hipStream_t s = as_stream(stream);
+  if (C % 4 == 0 && C <= 4 * kT && aligned16(a) && aligned16(b) && aligned16(sum)) {
+    bn_reduce4_kernel<2><<<(unsigned)bn_parts(V), kT, 0, s>>>(a, b, V, C, nullptr, 0.f, partial, sum);
+  } else {
+    const int64_t n = V * C;
+    if (n > 0) add_kernel<<<ew_grid(n), kT, 0, s>>>(a, b, n, sum);
+    bn_reduce_kernel<0><<<(unsigned)bn_parts(V), kT, 0, s>>>(sum, nullptr, V, C, nullptr, 0.f, partial);
+  }
+  return check_launch("msp_add_bn_stats");
 }
 
 }  // extern "C"

@@ -237,9 +237,32 @@ class BatchNormalization(nn.Module):
     def forward(self, input):
         if input.features.size(1) != self.nPlanes:
             raise ValueError(f"BatchNormalization({self.nPlanes}) got {input.features.size(1)} channels")
-        f = ops.BatchNormFunction.apply(input.features, self.weight, self.bias, self.running_mean, self.running_var,
-                                        self.eps, self.momentum, float(self.leakiness), self.training)
+        args = (self.weight, self.bias, self.running_mean, self.running_var, self.eps, self.momentum,
+                float(self.leakiness), self.training, self._joined_partial(input))
+        if self.__dict__.pop("_fork", False):
+            # residual fork requested by ConcatTable: x is handed on to the shortcut through the Function so
+            # the shortcut's gradient of x is added inside the BN backward (ops.BatchNormForkFunction)
+            f, xs = ops.BatchNormForkFunction.apply(input.features, *args)
+            self._fork_shortcut = SparseConvNetTensor(xs, input.metadata, input.spatial_size)
+        else:
+            f = ops.BatchNormFunction.apply(input.features, *args)
         return SparseConvNetTensor(f, input.metadata, input.spatial_size)
+
+    def _joined_partial(self, input):
+        """Batch-statistic partials a residual join left on its output (AddTable), if they are for exactly
+        these features and this pass needs batch statistics."""
+        jp = getattr(input, "_bn_partial", None)
+        return jp[1] if (jp is not None and self.training and jp[0] is input.features) else None
+
+    def forward_fork(self, input):
+        """(BN-ReLU(input), input) with the shortcut's gradient of input added inside the BN backward.  The
+        module is called normally (forward hooks see the usual input and output)."""
+        self._fork = True
+        try:
+            y = self(input)
+        finally:
+            self.__dict__.pop("_fork", None)
+        return y, self.__dict__.pop("_fork_shortcut")
 
     def extra_repr(self):
         return f"{self.nPlanes}, eps={self.eps}, momentum={self.momentum}, leakiness={self.leakiness}"
@@ -262,6 +285,11 @@ class Sequential(nn.Sequential):
         return self
 
 
+# Residual fork / join fusions (ops.BatchNormForkFunction, ops.ResidualJoinFunction); False = SCN's
+# one-module-at-a-time composition with torch adds (same results bit for bit, tests/test_gpu_ops.py).
+FUSE_RESIDUAL = True
+
+
 class ConcatTable(nn.Module):
     def __init__(self, *args):
         super().__init__()
@@ -273,11 +301,27 @@ class ConcatTable(nn.Module):
         return self
 
     def forward(self, input):
-        return [m(input) for m in self._modules.values()]
+        mods = list(self._modules.values())
+        # residual fork (shortcut, Sequential(BatchNorm..., ...)): the BN runs first and hands x on to the
+        # shortcut, so x's two gradients are summed inside the BN backward (ops.BatchNormForkFunction)
+        if FUSE_RESIDUAL and len(mods) == 2 and isinstance(mods[1], nn.Sequential) and len(mods[1]) > 0 \
+                and type(mods[1][0]).forward is BatchNormalization.forward and input.features.is_cuda:
+            y, xs = mods[1][0].forward_fork(input)
+            out = mods[0](xs)
+            for m in list(mods[1])[1:]:
+                y = m(y)
+            return [out, y]
+        return [m(input) for m in mods]
 
 
 class AddTable(nn.Module):
     def forward(self, input):
+        if FUSE_RESIDUAL and len(input) == 2 and input[0].features.is_cuda and input[0].features.shape == input[1].features.shape:
+            # residual join + the next BatchNormalization's statistics in one pass (ops.ResidualJoinFunction)
+            f, partial = ops.ResidualJoinFunction.apply(input[0].features, input[1].features)
+            out = SparseConvNetTensor(f, input[0].metadata, input[0].spatial_size)
+            out._bn_partial = (f, partial)
+            return out
         f = input[0].features
         for t in input[1:]:
             f = f + t.features

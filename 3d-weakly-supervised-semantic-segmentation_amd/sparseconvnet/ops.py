@@ -329,24 +329,53 @@ class NetworkInNetworkFunction(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------ batch norm
-class BatchNormFunction(torch.autograd.Function):
-    """BatchNormalization + (leaky) ReLU; stats[5][C] as in include/mi3dsparse.h."""
+def _bn_partial_buf(V, C, device):
+    P = int(_lib.query("msp_bn_partials", _lib.I64(V), C))
+    return torch.empty((P + 1) * 2 * C, dtype=torch.float64, device=device)
 
-    @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train):
-        _check_feats(x)
-        x = x.contiguous()
-        V, C = x.shape
-        s = _stream(x)
-        P = int(_lib.query("msp_bn_partials", _lib.I64(V), C))
-        stats = torch.empty((5, C), dtype=torch.float32, device=x.device)
-        partial = torch.empty((P + 1) * 2 * C, dtype=torch.float64, device=x.device)
+
+def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial):
+    """y, stats of BN + (leaky) ReLU; `partial` = the msp_bn_stats partials of
+    x when a residual join already produced them (msp_add_bn_stats), else None."""
+    V, C = x.shape
+    s = _stream(x)
+    stats = torch.empty((5, C), dtype=torch.float32, device=x.device)
+    if partial is None:
+        partial = _bn_partial_buf(V, C, x.device)
         if train:
             call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
-        call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
-             ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
-        y = torch.empty_like(x)
-        call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
+    call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
+         ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
+    y = torch.empty_like(x)
+    call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
+    return y, stats
+
+
+def _bn_bwd(x, weight, stats, cfg, gy, addend):
+    """dx (+ addend, fused), dweight, dbias."""
+    leak, train, has_w, has_b = cfg
+    gy = gy.contiguous()
+    V, C = x.shape
+    s = _stream(x)
+    partial = _bn_partial_buf(V, C, x.device)
+    call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
+    dx = torch.empty_like(x)
+    dw = torch.empty(C, dtype=torch.float32, device=x.device)
+    db = torch.empty(C, dtype=torch.float32, device=x.device)
+    call("msp_bn_bwd_apply_add", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats), ptr(weight) if has_w else None,
+         leak, train, ptr(addend) if addend is not None else None, ptr(dx), ptr(dw), ptr(db), s)
+    return dx, (dw if has_w else None), (db if has_b else None)
+
+
+class BatchNormFunction(torch.autograd.Function):
+    """BatchNormalization + (leaky) ReLU; stats[5][C] as in include/mi3dsparse.h.
+    `partial`: precomputed batch-statistic partials of x (ResidualJoinFunction)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial=None):
+        _check_feats(x)
+        x = x.contiguous()
+        y, stats = _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial)
         ctx.save_for_backward(x, weight, stats)
         ctx.cfg = (float(leak), int(train), weight is not None, bias is not None)
         return y
@@ -354,19 +383,59 @@ class BatchNormFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, weight, stats = ctx.saved_tensors
-        leak, train, has_w, has_b = ctx.cfg
-        gy = gy.contiguous()
-        V, C = x.shape
-        s = _stream(x)
-        P = int(_lib.query("msp_bn_partials", _lib.I64(V), C))
-        partial = torch.empty((P + 1) * 2 * C, dtype=torch.float64, device=x.device)
-        call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
-        dx = torch.empty_like(x)
-        dw = torch.empty(C, dtype=torch.float32, device=x.device)
-        db = torch.empty(C, dtype=torch.float32, device=x.device)
-        call("msp_bn_bwd_apply", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats), ptr(weight) if has_w else None,
-             leak, train, ptr(dx), ptr(dw), ptr(db), s)
-        return dx, (dw if has_w else None), (db if has_b else None), None, None, None, None, None, None
+        dx, dw, db = _bn_bwd(x, weight, stats, ctx.cfg, gy, None)
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+class BatchNormForkFunction(torch.autograd.Function):
+    """x -> (BN-ReLU(x), x): the residual fork of SCN's ConcatTable(shortcut,
+    Sequential(BatchNorm..., ...)) (networkArchitectures.py blocks, UNet skip
+    joins).  The second output is x itself (a view) for the shortcut; the
+    backward adds the shortcut's gradient of x inside the BN backward kernel
+    (msp_bn_bwd_apply_add) instead of autograd's separate accumulation add."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial=None):
+        _check_feats(x)
+        x = x.contiguous()
+        ctx.set_materialize_grads(False)
+        y, stats = _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial)
+        ctx.save_for_backward(x, weight, stats)
+        ctx.cfg = (float(leak), int(train), weight is not None, bias is not None)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gx):
+        x, weight, stats = ctx.saved_tensors
+        if gy is None:
+            return gx, None, None, None, None, None, None, None, None, None
+        if gx is not None:
+            gx = gx.contiguous()
+        dx, dw, db = _bn_bwd(x, weight, stats, ctx.cfg, gy, gx)
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+class ResidualJoinFunction(torch.autograd.Function):
+    """a + b (SCN AddTable of a residual block) fused with the batch-statistic
+    partials of the sum (msp_add_bn_stats): the next BatchNormalization, which
+    every residual join in the UNet/FCN builders feeds, skips its own pass
+    over the sum.  Returns (sum, partials); the partials carry no gradient."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        _check_feats(a)
+        _check_feats(b)
+        a, b = a.contiguous(), b.contiguous()
+        V, C = a.shape
+        out = torch.empty_like(a)
+        partial = _bn_partial_buf(V, C, a.device)
+        call("msp_add_bn_stats", ptr(a), ptr(b), V, C, ptr(out), ptr(partial), _stream(a))
+        ctx.mark_non_differentiable(partial)
+        return out, partial
+
+    @staticmethod
+    def backward(ctx, g, _gp):
+        return g, g
 
 
 # ------------------------------------------------------------------ input / output / pooling

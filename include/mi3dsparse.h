@@ -223,6 +223,18 @@ int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const fl
 int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,
                      const float* weight, float leak, int train, float* dx, float* dweight, float* dbias,
                      msp_stream_t stream);
+/* Residual fusions (SCN's ConcatTable(shortcut, BN...) / AddTable pair,
+ * networkArchitectures.py res blocks; the reference leaves these to autograd
+ * and a separate add).  msp_bn_bwd_apply_add: as msp_bn_bwd_apply, plus
+ * dx += addend (the shortcut's gradient of x, one fp32 add as autograd's
+ * accumulation would do); addend may be NULL, must not alias dx.
+ * msp_add_bn_stats: sum = a + b and the msp_bn_stats partials of sum in one
+ * pass (identical partials to msp_bn_stats on sum). */
+int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, const double* partial,
+                         const float* stats, const float* weight, float leak, int train, const float* addend,
+                         float* dx, float* dweight, float* dbias, msp_stream_t stream);
+int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,
+                     msp_stream_t stream);
 
 /* ---------------- input / output / pooling layers */
 /* mode-4 average: out[v] = mean of feats[perm[j]] for j in [vstart[v], vstart[v+1]) */

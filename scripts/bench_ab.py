@@ -2,18 +2,19 @@
 once per variant in one process (same box, same batches), prints ms/step.
 Variants (comma list in AB): tile (no dense row groups), nbr0 (dense groups in
 key order), nbr (production: mask-sorted order), g<N> (dense kernel variant N,
-msp_debug_conv_nbr_variant).  Usage: AB=tile,nbr python scripts/bench_ab.py"""
+msp_debug_conv_nbr_variant), fuse / nofuse (residual fork/join fusions on / off).  Usage: AB=tile,nbr python scripts/bench_ab.py"""
 import io, json, os, sys, contextlib
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
 import __graft_entry__ as g_; g_.add_path()
 import bench
-from sparseconvnet import _lib, metadata
+from sparseconvnet import _lib, metadata, modules
 lib = _lib.load()
 orig_query, orig_order = _lib.query, metadata.SubmRules.dense_order
 res = []
 for v in os.environ.get("AB", "tile,nbr").split(","):
     _lib.query, metadata.SubmRules.dense_order = orig_query, orig_order
     lib.msp_debug_conv_nbr_variant(0)
+    modules.FUSE_RESIDUAL = v != "nofuse"
     if v == "tile":
         _lib.query = lambda name, *a: 0 if name == "msp_conv_nbr_preferred" else orig_query(name, *a)
     elif v == "nbr0":

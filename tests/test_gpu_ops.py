@@ -500,3 +500,66 @@ def test_conv_wgrad_band(cin, cout, size):
     if size == 4096:
         assert V > 256 * 8 and V % 256 != 0 and far > 0, (V, far)
     _lib.load().msp_debug_wgrad_band(0)
+
+
+@pytest.mark.parametrize("V,C", [(5000, 32), (3001, 64), (777, 36), (1200, 6), (0, 32)])
+def test_residual_join_stats(V, C):
+    """msp_add_bn_stats: the sum bit-equal to a + b and its partials bit-equal
+    to msp_bn_stats on that sum (vector form; C = 6 takes the scalar form)."""
+    from sparseconvnet import _lib, ops
+    torch.manual_seed(V + C)
+    a = torch.randn(V, C, device=DEV) * 2 + 0.5
+    b = torch.randn(V, C, device=DEV)
+    f, part = ops.ResidualJoinFunction.apply(a, b)
+    assert torch.equal(f, a + b)
+    ref = ops._bn_partial_buf(V, C, a.device)
+    ref.zero_()
+    _lib.call("msp_bn_stats", _lib.ptr(a + b), V, C, _lib.ptr(ref), ops._stream(a))
+    P = int(_lib.query("msp_bn_partials", _lib.I64(V), C))
+    assert torch.equal(part[:P * 2 * C], ref[:P * 2 * C])
+
+
+@pytest.mark.parametrize("C,leak,nin", [(32, 0.0, False), (64, 0.333, True), (6, 0.0, False)])
+def test_residual_block_fused_matches_unfused(C, leak, nin):
+    """ConcatTable(shortcut, BN-SubM-BN-SubM) + AddTable + BN with the fork /
+    join fusions against the same modules run one by one with torch adds
+    (the unfused composition): outputs, input gradient and every parameter
+    gradient bit-equal, running statistics equal."""
+    torch.manual_seed(C)
+    coords, feats = _inputs(3000, 24, n_feat=C)
+    g, _ = _pair(coords, feats)
+    C2 = C + 16 if nin else C
+    def make():
+        torch.manual_seed(1)
+        blk = scn.Sequential().add(
+            scn.ConcatTable().add(scn.NetworkInNetwork(C, C2, False) if nin else scn.Identity()).add(
+                scn.Sequential().add(scn.BatchNormLeakyReLU(C, leakiness=leak))
+                .add(scn.SubmanifoldConvolution(3, C, C2, 3, False))
+                .add(scn.BatchNormLeakyReLU(C2, leakiness=leak))
+                .add(scn.SubmanifoldConvolution(3, C2, C2, 3, False)))).add(scn.AddTable()).add(
+            scn.BatchNormReLU(C2))
+        return blk.to(DEV)
+    fused, plain = make(), make()
+    def run_plain(x):
+        ct, _, bn = list(plain)
+        sc, br = list(ct._modules.values())
+        a = sc(x)
+        y = x
+        for m in br:
+            y = m(y)
+        s = type(x)(a.features + y.features, x.metadata, x.spatial_size)
+        return bn(s)
+    outs = []
+    for run in (fused, run_plain):
+        x = g.features.detach().clone().requires_grad_(True)
+        t = type(g)(x, g.metadata, g.spatial_size)
+        y = run(t)
+        w = torch.linspace(-1, 1, y.features.numel(), device=DEV).view_as(y.features)
+        (y.features * w).square().sum().backward()
+        outs.append((y.features.detach(), x.grad))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    for (n1, p1), (n2, p2) in zip(fused.named_parameters(), plain.named_parameters()):
+        assert n1 == n2 and torch.equal(p1.grad, p2.grad), n1
+    for (n1, b1), (n2, b2) in zip(fused.named_buffers(), plain.named_buffers()):
+        assert torch.equal(b1, b2), n1
