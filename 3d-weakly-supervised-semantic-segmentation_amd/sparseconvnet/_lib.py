@@ -57,6 +57,9 @@ PROTOTYPES = {
     "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),
+    "msp_nin_gemm_ok": (I, [I64, I, I]),
+    "msp_nin_gemm_preferred": (I, [I64, I, I]),
+    "msp_nin_gemm": (I, [P, I64, I, P, I, P, P]),
     "msp_input_avg_fwd": (I, [P, I, P, P, I64, P, P]),
     "msp_input_avg_bwd": (I, [P, I, P, P, I64, P, P]),
     "msp_output_fwd": (I, [P, I, P, I64, P, P]),

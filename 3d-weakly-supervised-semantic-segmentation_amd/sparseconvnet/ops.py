@@ -300,6 +300,19 @@ class _IdentityPairs:
         self.pair = torch.arange(max(n, 1), dtype=torch.int32, device=device)
 
 
+def nin_gemm(a, b, force=False):
+    """a[M][K] @ b[K][N] on msp_nin_gemm (HBM-bound tall-skinny product) where the library prefers it
+    (msp_nin_gemm_preferred: >= 2^18 rows); other shapes run torch's device GEMM (hipBLASLt)."""
+    M, K = a.shape
+    N = b.size(1)
+    q = "msp_nin_gemm_ok" if force else "msp_nin_gemm_preferred"
+    if not _lib.query(q, _lib.I64(M), K, N) or a.data_ptr() % 16 or b.data_ptr() % 16:
+        return a @ b
+    out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    call("msp_nin_gemm", ptr(a), M, K, ptr(b), N, ptr(out), _stream(a))
+    return out
+
+
 class NetworkInNetworkFunction(torch.autograd.Function):
     """out = x W (§8(a) a11).  Forward and backward-data are dense GEMMs on
     hipBLASLt through torch; the weight gradient x^T dy (contraction over all
@@ -311,7 +324,7 @@ class NetworkInNetworkFunction(torch.autograd.Function):
         _check_feats(x)
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
-        return x @ weight
+        return nin_gemm(x, weight.contiguous())
 
     @staticmethod
     def backward(ctx, gout):
@@ -319,7 +332,7 @@ class NetworkInNetworkFunction(torch.autograd.Function):
         g = gout.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = g @ weight.t()
+            dx = nin_gemm(g, weight.t().contiguous())
         if ctx.needs_input_grad[1]:
             cin, cout = weight.shape
             cin_p, cout_p = _pad16(cin), _pad16(cout)

@@ -236,6 +236,17 @@ int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, cons
 int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,
                      msp_stream_t stream);
 
+/* ---------------- NetworkInNetwork products (replaces SCN's NetworkInNetwork
+ * forward / backward-data, scn.NetworkInNetwork in the UNet/FCN residual
+ * shortcuts): C[M][N] = A[M][K] B[K][N], row-major fp32,
+ * fp32 products and accumulation (f32 MFMA).  Forward: A = x, B = W[c_in][c_out];
+ * backward-data: A = dy, B = W^T.  msp_nin_gemm_ok says whether the shape is
+ * supported (K % 16 == 0, N % 16 == 0, K <= 1024); A and B 16-byte aligned. */
+int msp_nin_gemm_ok(int64_t M, int K, int N);
+/* whether msp_nin_gemm beats the library GEMM for this shape (measured: M >= 2^18 rows) */
+int msp_nin_gemm_preferred(int64_t M, int K, int N);
+int msp_nin_gemm(const float* A, int64_t M, int K, const float* B, int N, float* C, msp_stream_t stream);
+
 /* ---------------- input / output / pooling layers */
 /* mode-4 average: out[v] = mean of feats[perm[j]] for j in [vstart[v], vstart[v+1]) */
 int msp_input_avg_fwd(const float* feats, int C, const int32_t* perm, const int32_t* vstart, int64_t V,

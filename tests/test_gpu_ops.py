@@ -563,3 +563,35 @@ def test_residual_block_fused_matches_unfused(C, leak, nin):
         assert n1 == n2 and torch.equal(p1.grad, p2.grad), n1
     for (n1, b1), (n2, b2) in zip(fused.named_buffers(), plain.named_buffers()):
         assert torch.equal(b1, b2), n1
+
+
+@pytest.mark.parametrize("M,K,N", [(300007, 64, 32), (40000, 128, 64), (9001, 192, 96), (5000, 320, 160),
+                                   (777, 48, 48), (130, 448, 224), (1, 32, 16), (0, 64, 32), (270001, 32, 64),
+                                   (30000, 64, 128), (20000, 96, 192)])
+def test_nin_gemm(M, K, N):
+    """msp_nin_gemm (NetworkInNetwork forward / backward-data) against an fp64
+    product: fp32 products and accumulation, tolerance 1e-5 of max |ref|
+    (ragged last row group, 1-8 column tiles, several column chunks, the
+    headline UNet's forward and backward-data shapes)."""
+    from sparseconvnet import ops
+    torch.manual_seed(M + K + N)
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV) / K ** 0.5
+    out = ops.nin_gemm(a, b, force=True)
+    close(out, a.double() @ b.double(), 1e-5, "nin_gemm")
+
+
+def test_nin_layer_grad():
+    """NetworkInNetwork fwd + bwd (dx via msp_nin_gemm on W^T, dW via msp_conv_wgrad) against fp64 torch."""
+    torch.manual_seed(3)
+    coords, feats = _inputs(4000, 24, n_feat=64)  # below the preferred size: checks the routing too
+    g, _ = _pair(coords, feats)
+    nin = scn.NetworkInNetwork(64, 32, False).to(DEV)
+    x = g.features.detach().clone().requires_grad_(True)
+    y = nin(type(g)(x, g.metadata, g.spatial_size))
+    gy = torch.randn_like(y.features)
+    y.features.backward(gy)
+    xd, wd = x.detach().double(), nin.weight.detach().double()
+    close(y.features, xd @ wd, 1e-5, "nin fwd")
+    close(x.grad, gy.double() @ wd.t(), 1e-5, "nin dx")
+    close(nin.weight.grad, xd.t() @ gy.double(), 1e-5, "nin dW")
