@@ -986,7 +986,7 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   // profiles/r01/kbench_nbr_r01v.log; g = 2: the base form (all fragments
   // first, two staging slots)
   if (nt <= 0) nt = n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1));
-  if (g <= 0) g = 132;
+  if (g <= 0) g = 141;
   if (n16 % nt != 0) {
     set_error("msp_conv_nbr: nt %d does not divide c_out/16 = %d", nt, n16);
     return MSP_EINVAL;
@@ -1014,10 +1014,13 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
                                                            n_y, out);                                         \
     launched = true;                                                                                          \
   }
-  // production (g = 0 -> 132): column-group-outer MFMAs, one staging slot, a 3-waves-per-SIMD register
-  // budget (156 / 142 VGPRs, no spills): 5-12 % over the G = 2 base form within one run
-  // (profiles/r01/kbench_nbr_lr_r01w.log); g = 100 + G + 10 * waves per SIMD selects others
+  // production (g = 0 -> 141): column-group-outer MFMAs, one staging slot, ONE 16-row group per wave at a
+  // 4-waves-per-SIMD budget (108 / 94 VGPRs, no spills): conv family +1.5 % TF/s over 132 (G = 2, 3 waves,
+  // 156 / 142 VGPRs) in three same-process A/B pairs (profiles/r01/bench_ab_g1_r01.log); 132 was 5-12 %
+  // over the G = 2 base form (profiles/r01/kbench_nbr_lr_r01w.log); g = 100 + G + 10 * waves per SIMD
+  // selects others
   LL(4, 2, 3) LL(3, 2, 3) LL(2, 2, 3) LL(1, 2, 3) LL(4, 2, 1) LL(3, 2, 1)
+  LL(4, 1, 4) LL(3, 1, 4) LL(2, 1, 4) LL(1, 1, 4)  // G = 1: 108 / 94 VGPRs, 4-5 waves per SIMD (G = 2 at 4 waves spills)
 #undef LL
   if (!launched) {
     set_error("msp_conv_nbr: no dense-group kernel for nt=%d g=%d", nt, g);
