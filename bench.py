@@ -168,9 +168,8 @@ def main():
     from wsss3d.synthetic import make_batch
 
     _lib.load()
-    if args.concurrent_wgrad:
-        from sparseconvnet import ops as scn_ops
-        scn_ops.WGRAD_CONCURRENT = True
+    from sparseconvnet import ops as scn_ops
+    scn_ops.WGRAD_CONCURRENT = bool(args.concurrent_wgrad)  # set both ways (scripts/bench_ab.py reruns main)
     # two distinct batches per rank, alternated step to step
     host_batches = [make_batch(args.batch, args.scale, seed=1000 * rank + k) for k in range(2)]
     contrastive = args.workload == "contrastive"

@@ -3,7 +3,7 @@ once per variant in one process (same box, same batches), prints ms/step.
 Variants (comma list in AB): tile (no dense row groups), nbr0 (dense groups in
 key order), nbr (production: mask-sorted order), g<N> (dense kernel variant N,
 msp_debug_conv_nbr_variant), fuse / nofuse (residual fork/join fusions on / off),
-fused / foreach (Adam implementation).  Usage: AB=tile,nbr python scripts/bench_ab.py"""
+fused / foreach (Adam implementation), cw (weight gradients on a side stream).  Usage: AB=tile,nbr python scripts/bench_ab.py"""
 import io, json, os, sys, contextlib
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
 import __graft_entry__ as g_; g_.add_path()
@@ -23,7 +23,7 @@ for v in os.environ.get("AB", "tile,nbr").split(","):
     elif v.startswith("g"):
         lib.msp_debug_conv_nbr_variant(int(v[1:]))
     sys.argv = ["bench.py", "--steps", os.environ.get("STEPS", "10"), "--warmup", "2", "--no-cpu"] + \
-        (["--foreach-adam"] if v == "foreach" else [])
+        (["--foreach-adam"] if v == "foreach" else []) + (["--concurrent-wgrad"] if v == "cw" else [])
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         bench.main()
