@@ -960,7 +960,15 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   if (e < cc) {
     const float* p = slab + (int64_t)o * cc + e;
     const int64_t stride = (int64_t)K * cc;
-    for (int64_t j = j0; j < j1; ++j) s += p[j * stride];
+    int64_t j = j0;
+    for (; j + 8 <= j1; j += 8) {  // eight loads in flight, added in piece order (same sum as one at a time)
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = p[(j + k) * stride];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    for (; j < j1; ++j) s += p[j * stride];
   }
   part[seg][el] = s;
   __syncthreads();
