@@ -1425,10 +1425,14 @@ int launch_wgrad_band_seg(const int32_t* pout, const int64_t* off_start, int K, 
 
 // dW tile of the x6 weight gradient: WA in {4, 3, 2, 1} (largest dividing
 // c_in / 16), WB in {2, 1} (registers: two value sets of 8 pairs each).
+static int g_wgrad_wa = 0, g_wgrad_wb = 0;  // msp_debug_wgrad_tile: forced tile (experiments)
+
 void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb) {
   const int a = c_in / 16, bb = c_out / 16;
   wa = a % 4 == 0 ? 4 : (a % 3 == 0 ? 3 : (a % 2 == 0 ? 2 : 1));
   wb = bb % 2 == 0 ? 2 : 1;
+  if (g_wgrad_wa > 0 && a % g_wgrad_wa == 0) wa = g_wgrad_wa;
+  if (g_wgrad_wb > 0 && bb % g_wgrad_wb == 0) wb = g_wgrad_wb;
 }
 
 static int g_wgrad_abl = 0;  // msp_debug_wgrad_abl: ablation variants of the x6 weight gradient
@@ -1463,6 +1467,12 @@ int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const 
 }
 
 }  // namespace msp
+
+extern "C" int msp_debug_wgrad_tile(int wa, int wb) {
+  msp::g_wgrad_wa = wa;
+  msp::g_wgrad_wb = wb;
+  return MSP_OK;
+}
 
 extern "C" int msp_debug_wgrad_abl(int abl) {
   msp::g_wgrad_abl = abl;

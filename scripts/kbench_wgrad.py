@@ -20,6 +20,7 @@ lib.msp_debug_wgrad_blocks.argtypes = [_lib.I64]
 BLOCKS = [int(v) for v in os.environ.get("BLOCKS", "0").split(",")]
 MODES = [int(v) for v in os.environ.get("MODES", "0,1").split(",")]
 lib.msp_debug_wgrad_abl(int(os.environ.get("ABL", "0")))
+lib.msp_debug_wgrad_tile(int(os.environ.get("WA", "0")), int(os.environ.get("WB", "0")))  # forced dW tile
 for (L, size, ci, c), mode, nb in [(cs, m, nb) for cs in cases for m in MODES for nb in BLOCKS]:
     lib.msp_debug_wgrad_f32(1 if mode == 1 else 0)
     lib.msp_debug_wgrad_blocks(nb)
