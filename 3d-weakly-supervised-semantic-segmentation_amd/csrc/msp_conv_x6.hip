@@ -790,22 +790,23 @@ size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c
 // registers loaded two steps ahead) instead of reloading it per wave.
 // Gathered values run two steps ahead, neighbour indices four; each step's six
 // piece products are summed in a zeroed accumulator and added once.
-template <int NT, int G, int OCC = 1, int LR = 0>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_x6g_kernel(
+template <int NT, int G, int OCC = 1, int LR = 0, int NW = kWaves>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_x6g_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const int32_t* __restrict__ nbr, const int32_t* __restrict__ perm, int64_t n_rows, int n_y,
     float* __restrict__ out) {
   constexpr int NC = 16 * NT;
   constexpr int WU = 3 * 4 * NC;  // 16-byte units of one step's split weight slice
   constexpr int TRW = 16 * G;     // rows per wave
-  constexpr int WPT = (WU + kThreads - 1) / kThreads;
+  constexpr int NTH = 64 * NW;    // threads per block (NW waves share each step's weight slice)
+  constexpr int WPT = (WU + NTH - 1) / NTH;
   __shared__ u32x4 wl[2][WU];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 15, q = lane >> 4;
   const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
   const int cy = (int)(lb % n_y);
-  const int64_t row0 = (lb / n_y) * (int64_t)(kWaves * TRW) + wave * TRW;
+  const int64_t row0 = (lb / n_y) * (int64_t)(NW * TRW) + wave * TRW;
   const int nks = (c_in + 31) / 32;
   const int n_steps = K * nks;
   uint32_t rowok = 0;  // lane's rows inside the level
@@ -829,15 +830,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(OCC)))
     const u32x4* src = wimg + ((int64_t)(ow * n_y + cy) * nks + ks) * WU;
 #pragma unroll
     for (int i = 0; i < WPT; ++i) {
-      const int u = tid + i * kThreads;
+      const int u = tid + i * NTH;
       w.u[i] = src[u < WU ? u : WU - 1];
     }
   };
   auto st_wst = [&](const Wst& w, int buf) {
 #pragma unroll
     for (int i = 0; i < WPT; ++i) {
-      const int u = tid + i * kThreads;
-      if (WU % kThreads == 0 || u < WU) wl[buf][u] = w.u[i];
+      const int u = tid + i * NTH;
+      if (WU % NTH == 0 || u < WU) wl[buf][u] = w.u[i];
     }
   };
   auto ld_ix = [&](int s, Ix& d) {
@@ -998,7 +999,8 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * nt, 32, wimg,
                                                                        (flip >> 1) & 1);
   flip &= 1;
-  const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)kWaves * 16 * (g % 10)) * n_y);
+  const int nw = g >= 1000 ? 8 : kWaves;  // g = 1000 + ...: 8-wave blocks
+  const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)nw * 16 * (g % 10)) * n_y);
   bool launched = false;
 #define LG(N, GG)                                                                                             \
   if (!launched && nt == N && g == GG) {                                                                      \
@@ -1020,7 +1022,15 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   // over the G = 2 base form (profiles/r01/kbench_nbr_lr_r01w.log); g = 100 + G + 10 * waves per SIMD
   // selects others
   LL(4, 2, 3) LL(3, 2, 3) LL(2, 2, 3) LL(1, 2, 3) LL(4, 2, 1) LL(3, 2, 1)
-  LL(4, 1, 4) LL(3, 1, 4) LL(2, 1, 4) LL(1, 1, 4)  // G = 1: 108 / 94 VGPRs, 4-5 waves per SIMD (G = 2 at 4 waves spills)
+  LL(4, 1, 4) LL(3, 1, 4) LL(2, 1, 4) LL(1, 1, 4)
+#define L8(N, GG, O)                                                                                          \
+  if (!launched && nt == N && g == 1000 + GG + 10 * O + 100) {                                                \
+    conv_x6g_kernel<N, GG, O, 1, 8><<<grid, 512, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, perm, n_rows,    \
+                                                         n_y, out);                                           \
+    launched = true;                                                                                          \
+  }
+  L8(4, 1, 4) L8(3, 1, 4)  // 8-wave blocks (128 rows share each step's weight slice)
+#undef L8  // G = 1: 108 / 94 VGPRs, 4-5 waves per SIMD (G = 2 at 4 waves spills)
 #undef LL
   if (!launched) {
     set_error("msp_conv_nbr: no dense-group kernel for nt=%d g=%d", nt, g);
