@@ -26,8 +26,14 @@ namespace msp {
 constexpr int kT = 256;
 constexpr int64_t kMaxParts = 1024;
 
-__host__ __device__ inline int64_t bn_parts(int64_t V) {
-  int64_t p = (V + 255) / 256;
+// Partial-sum blocks: two 4-deep passes of the vector form per block (R = 1024 / C rows per pass, so
+// 8 R rows per block, 16..256), at most kMaxParts.  Sized by C so the small levels (C up to 448, a few
+// hundred to a few thousand rows) get enough blocks: 256 rows per block there meant 16-64 serial passes
+// per thread (20-26 us per reduction, profiles/r01/kernel_stats_r01final2_bench_steps3.csv).
+__host__ __device__ inline int64_t bn_parts(int64_t V, int C) {
+  int64_t rpb = (C > 0 && C <= 1024) ? 8 * (1024 / C) : 256;
+  rpb = rpb > 256 ? 256 : (rpb < 16 ? 16 : rpb);
+  const int64_t p = (V + rpb - 1) / rpb;
   return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
 }
 
@@ -415,16 +421,16 @@ extern "C" {
 
 int64_t msp_bn_partials(int64_t V, int C) {
   (void)C;
-  return bn_parts(V);
+  return bn_parts(V, C);
 }
 
 int msp_bn_stats(const float* x, int64_t V, int C, double* partial, msp_stream_t stream) {
   MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_stats: bad shape");
   if (C % 4 == 0 && C <= 4 * kT && aligned16(x))
-    bn_reduce4_kernel<0><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
+    bn_reduce4_kernel<0><<<(unsigned)bn_parts(V, C), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
                                                                               partial);
   else
-    bn_reduce_kernel<0><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
+    bn_reduce_kernel<0><<<(unsigned)bn_parts(V, C), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
                                                                              partial);
   return check_launch("msp_bn_stats");
 }
@@ -434,7 +440,7 @@ int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double 
                     msp_stream_t stream) {
   MSP_REQUIRE(C > 0, "msp_bn_finalize: bad C");
   bn_finalize_kernel<<<(unsigned)C, kT, 0, as_stream(stream)>>>(
-      partial, bn_parts(V), C, V, eps, momentum, train, running_mean, running_var, weight, bias, stats);
+      partial, bn_parts(V, C), C, V, eps, momentum, train, running_mean, running_var, weight, bias, stats);
   return check_launch("msp_bn_finalize");
 }
 
@@ -452,9 +458,9 @@ int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const fl
                      double* partial, msp_stream_t stream) {
   MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_bwd_stats: bad shape");
   if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy))
-    bn_reduce4_kernel<1><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
+    bn_reduce4_kernel<1><<<(unsigned)bn_parts(V, C), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
   else
-    bn_reduce_kernel<1><<<(unsigned)bn_parts(V), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
+    bn_reduce_kernel<1><<<(unsigned)bn_parts(V, C), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial);
   return check_launch("msp_bn_bwd_stats");
 }
 
@@ -465,8 +471,8 @@ int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, cons
   hipStream_t s = as_stream(stream);
   // The combined per-channel sums go to the extra 2*C doubles at the tail of
   // the partial buffer (it holds (P + 1) * 2 * C doubles, see the header).
-  double* sums = const_cast<double*>(partial) + bn_parts(V) * 2 * C;
-  bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V), C, dweight, dbias, sums);
+  double* sums = const_cast<double*>(partial) + bn_parts(V, C) * 2 * C;
+  bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V, C), C, dweight, dbias, sums);
   const int64_t n = V * C;
   if (n > 0) {
     if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx) &&
@@ -492,11 +498,11 @@ int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* su
   MSP_REQUIRE((sum != a && sum != b) || V * C == 0, "msp_add_bn_stats: sum must not alias an input");
   hipStream_t s = as_stream(stream);
   if (C % 4 == 0 && C <= 4 * kT && aligned16(a) && aligned16(b) && aligned16(sum)) {
-    bn_reduce4_kernel<2><<<(unsigned)bn_parts(V), kT, 0, s>>>(a, b, V, C, nullptr, 0.f, partial, sum);
+    bn_reduce4_kernel<2><<<(unsigned)bn_parts(V, C), kT, 0, s>>>(a, b, V, C, nullptr, 0.f, partial, sum);
   } else {
     const int64_t n = V * C;
     if (n > 0) add_kernel<<<ew_grid(n), kT, 0, s>>>(a, b, n, sum);
-    bn_reduce_kernel<0><<<(unsigned)bn_parts(V), kT, 0, s>>>(sum, nullptr, V, C, nullptr, 0.f, partial);
+    bn_reduce_kernel<0><<<(unsigned)bn_parts(V, C), kT, 0, s>>>(sum, nullptr, V, C, nullptr, 0.f, partial);
   }
   return check_launch("msp_add_bn_stats");
 }
