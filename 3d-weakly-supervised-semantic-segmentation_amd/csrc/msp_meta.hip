@@ -62,6 +62,22 @@ __global__ __launch_bounds__(kThreads) void point_keys_kernel(const int64_t* __r
   }
 }
 
+// starts[b] = first row whose batch id is >= b (lower bound over a non-decreasing
+// batch column), b = 0..n_batch; one thread per entry, a binary search each.
+__global__ __launch_bounds__(kThreads) void batch_starts_kernel(const int64_t* __restrict__ coords, int64_t n,
+                                                                int64_t stride, int64_t n_batch,
+                                                                int64_t* __restrict__ starts) {
+  const int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (b > n_batch) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (coords[mid * stride + 3] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  starts[b] = lo;
+}
+
 // ---------------------------------------------------------------- segment
 constexpr int kSegItems = 8;
 constexpr int kSegTile = kThreads * kSegItems;
@@ -388,6 +404,16 @@ int msp_point_keys(const int64_t* coords, int64_t n, int64_t row_stride, int log
   point_keys_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(coords, n, row_stride, log2_size,
                                                                    spatial_size, keys, vals, stats);
   return check_launch("msp_point_keys");
+}
+
+int msp_batch_starts(const int64_t* coords, int64_t n, int64_t row_stride, int64_t n_batch, int64_t* starts,
+                     msp_stream_t stream) {
+  MSP_REQUIRE(n >= 0 && row_stride >= 4 && n_batch >= 0, "msp_batch_starts: bad n/row_stride/n_batch");
+  MSP_REQUIRE(starts != nullptr, "msp_batch_starts: starts is NULL");
+  MSP_REQUIRE(n == 0 || coords != nullptr, "msp_batch_starts: coords is NULL");
+  batch_starts_kernel<<<grid1(n_batch + 1), kThreads, 0, as_stream(stream)>>>(coords, n, row_stride, n_batch,
+                                                                              starts);
+  return check_launch("msp_batch_starts");
 }
 
 size_t msp_sort_workspace_size(int64_t n, int end_bit) {

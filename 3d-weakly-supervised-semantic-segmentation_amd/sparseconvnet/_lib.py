@@ -22,6 +22,7 @@ PROTOTYPES = {
     "msp_abi_version": (I, []),
     "msp_last_error": (ctypes.c_char_p, []),
     "msp_point_keys": (I, [P, I64, I64, I, I64, P, P, P, P]),
+    "msp_batch_starts": (I, [P, I64, I64, I64, P, P]),
     "msp_sort_workspace_size": (SZ, [I64, I]),
     "msp_sort_pairs": (I, [P, P, P, P, I64, I, P, SZ, P]),
     "msp_scan_workspace_size": (SZ, [I64]),

@@ -188,6 +188,17 @@ class InputRules:
     def __init__(self, n_points, perm, p2v, vstart, batch_size):
         self.n_points, self.perm, self.p2v, self.vstart, self.batch_size = n_points, perm, p2v, vstart, batch_size
         self.batch_monotonic = False  # batch column non-decreasing along the points
+        self.scene_starts = None      # host list: first point of batch id b, b = 0..batch_size (monotonic only)
+
+    def scene_ranges_match(self, batch_offsets):
+        """True when scene b of `batch_offsets` (dataset/data.py:142,209) is exactly the points of batch id b
+        (decided on the host from the counts read back with the voxel count; no device read)."""
+        off = [int(o) for o in batch_offsets]
+        B = len(off) - 1
+        if B < 1 or not self.batch_monotonic or self.scene_starts is None or self.batch_size > B:
+            return False
+        st = self.scene_starts + [self.n_points] * (B + 1 - len(self.scene_starts))
+        return st[:B + 1] == off
 
 
 class Metadata:
@@ -230,15 +241,22 @@ class Metadata:
         p2v = torch.empty_like(vals)
         uniq = torch.empty_like(keys)
         vstart = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        nu = torch.zeros(1, dtype=torch.int64, device=dev)
+        n_batch = int(max_b) + 1 if n else 0
+        monotonic = n_desc == 0
+        # one read-back: [voxel count, scene starts of a non-decreasing batch column (msp_batch_starts)]
+        tail = torch.zeros(2 + (n_batch if monotonic else 0), dtype=torch.int64, device=dev)
         ws = _ws(((n + 2047) // 2048 + 1) * 8, dev)
-        call("msp_segment", ptr(skeys), n, 0, ptr(perm), ptr(seg_of), ptr(p2v), ptr(uniq), ptr(vstart), ptr(nu),
+        call("msp_segment", ptr(skeys), n, 0, ptr(perm), ptr(seg_of), ptr(p2v), ptr(uniq), ptr(vstart), ptr(tail),
              ptr(ws), ws.numel(), s)
-        V = int(nu.item())
+        if monotonic:
+            call("msp_batch_starts", ptr(coords), n, 4, n_batch, ptr(tail[1:]), s)
+        got = tail.tolist()
+        V = int(got[0])
         lvl = Level(size, log2, uniq[:max(V, 1)], V, dev, self.plan)
         self.levels[size] = lvl
-        self.input = InputRules(n, perm[:n], p2v[:n], vstart[:V + 1], int(max_b) + 1 if n else 0)
-        self.input.batch_monotonic = n_desc == 0
+        self.input = InputRules(n, perm[:n], p2v[:n], vstart[:V + 1], n_batch)
+        self.input.batch_monotonic = monotonic
+        self.input.scene_starts = [int(v) for v in got[1:]] if monotonic else None
         return lvl
 
     def level(self, size):
@@ -353,6 +371,10 @@ class Metadata:
 # InputLayer forward then finds it ready (its stream waits on an event) and
 # the forward issues no device-to-host reads at all.  Nothing is skipped:
 # each batch's metadata is still built once, inside the step before it.
+# device index -> (coords tensor, its key, Metadata, event): at most one pending
+# entry per device; the entry holds the coords tensor itself and a hit needs the
+# very same tensor object (not just the same address), so freed coords whose
+# memory was handed to a new tensor can never pick up another batch's rulebooks.
 _PREFETCHED = {}
 _SIDE = {}
 
@@ -369,6 +391,7 @@ def prefetch(coords, spatial_size, plan, wait_for_producer=True):
     dev = coords.device
     if dev.type != "cuda":
         raise RuntimeError("sparseconvnet.prefetch: coords must be on a HIP device")
+    _PREFETCHED.pop(dev.index, None)  # an unconsumed older entry is dropped (its memory goes back)
     side = _SIDE.get(dev.index)
     if side is None:
         side = _SIDE[dev.index] = torch.cuda.Stream(dev)
@@ -381,20 +404,21 @@ def prefetch(coords, spatial_size, plan, wait_for_producer=True):
         m.replay(plan)
         ev = torch.cuda.Event()
         ev.record(side)
-    _PREFETCHED[_coords_key(coords, spatial_size)] = (m, ev)
+    _PREFETCHED[dev.index] = (coords, _coords_key(coords, spatial_size), m, ev)
     return m
 
 
 def take_prefetched(coords, spatial_size):
-    """The Metadata prefetched for these coords (popped), with the current
-    stream ordered after its build and its tensors marked as used by the
-    current stream; None if there is none."""
+    """The Metadata prefetched for this very coords tensor (popped), with the
+    current stream ordered after its build and its tensors marked as used by
+    the current stream; None if there is none."""
     if not _PREFETCHED:
         return None
-    hit = _PREFETCHED.pop(_coords_key(coords, spatial_size), None)
-    if hit is None:
+    hit = _PREFETCHED.get(coords.device.index)
+    if hit is None or hit[0] is not coords or hit[1] != _coords_key(coords, spatial_size):
         return None
-    m, ev = hit
+    del _PREFETCHED[coords.device.index]
+    _, _, m, ev = hit
     cur = torch.cuda.current_stream(coords.device)
     cur.wait_event(ev)
     for t in m.tensors():

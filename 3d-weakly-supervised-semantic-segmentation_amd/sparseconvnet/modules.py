@@ -365,7 +365,16 @@ def prefetch_metadata(model, coords, wait_for_producer=True):
     rulebook the model's last forward requested -- on a side stream now
     (typically right after the current step's backward/optimizer calls were
     queued), so the next forward on these coords starts with it ready.
-    Returns the Metadata, or None before the model's first forward."""
+    Returns the Metadata, or None before the model's first forward.
+
+    wait_for_producer=True (the safe default) orders the side stream after
+    everything already queued on the current stream, in case kernels queued
+    there still write `coords`; the build's count reads then wait for the
+    queued backward/optimizer too, so there is no overlap.  Pass False for
+    coords that are already complete on the device (a resident batch, or one
+    whose producer was synchronised): the build then runs beside the queued
+    work.  The entry is keyed on the coords tensor object itself and only the
+    latest prefetch per device is kept."""
     for m in model.modules():
         if isinstance(m, InputLayer):
             plan = getattr(m, "last_plan", None)

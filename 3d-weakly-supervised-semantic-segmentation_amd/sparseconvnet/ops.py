@@ -83,11 +83,15 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     return out[:n_rows]
 
 
-def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out):
+def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out, kind="pairs", flops=0):
     out = torch.empty((max(n_out, 1), c_out), dtype=torch.float32, device=x.device)
     if pairs.n_chunks:
-        call("msp_conv_pairs", ptr(x), x.size(1), ptr(wt), K, c_out, ptr(pin), ptr(pout), ptr(pairs.off_start),
-             ptr(pairs.chunk_start), pairs.n_chunks, ptr(out), _stream(x))
+        c_in = x.size(1)
+        # compulsory bytes: source rows, output rows, weights, the pair lists
+        nbytes = 4 * (x.size(0) * c_in + n_out * c_out + K * c_in * c_out) + 8 * pairs.total
+        _record(kind + "/f32", flops, lambda: call(
+            "msp_conv_pairs", ptr(x), c_in, ptr(wt), K, c_out, ptr(pin), ptr(pout), ptr(pairs.off_start),
+            ptr(pairs.chunk_start), pairs.n_chunks, ptr(out), _stream(x)), nbytes)
     return out[:n_out]
 
 
@@ -98,7 +102,7 @@ _WGRAD_SIDE = {}
 WGRAD_CONCURRENT = False
 
 
-def conv_wgrad_async(x, dy, pairs, pin, pout, K):
+def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None):
     """conv_wgrad on a side stream, ordered after the work already queued on
     the current stream, so it runs concurrently with the backward-data
     launched next on the current stream (both are latency-bound gathers at
@@ -107,7 +111,7 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K):
     backward returns, so everything after this autograd node is ordered
     after the weight gradient as well."""
     if not WGRAD_CONCURRENT:
-        return conv_wgrad(x, dy, pairs, pin, pout, K), lambda: None
+        return conv_wgrad(x, dy, pairs, pin, pout, K, flops=flops), lambda: None
     dev = x.device
     cur = torch.cuda.current_stream(dev)
     side = _WGRAD_SIDE.get(dev.index)
@@ -115,7 +119,7 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K):
         side = _WGRAD_SIDE[dev.index] = torch.cuda.Stream(dev)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
-        dw = conv_wgrad(x, dy, pairs, pin, pout, K)
+        dw = conv_wgrad(x, dy, pairs, pin, pout, K, flops=flops)
         ev = torch.cuda.Event()
         ev.record(side)
 
@@ -144,13 +148,18 @@ def conv_wgrad_band(x, dy, pairs, K, n_rows):
     return dw
 
 
-def conv_wgrad(x, dy, pairs, pin, pout, K):
+def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
     c_in, c_out = x.size(1), dy.size(1)
     dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
     n_pieces = int(_lib.query("msp_wgrad_pieces", _lib.I64(pairs.total), K, c_in, c_out))
     slab = torch.empty((n_pieces, K, c_in, c_out), dtype=torch.float32, device=x.device)
-    call("msp_conv_wgrad", ptr(x), c_in, ptr(dy), c_out, ptr(pin), ptr(pout), ptr(pairs.off_start), K,
-         n_pieces, ptr(slab), ptr(dw), _stream(x))
+    if flops is None:
+        flops = 2.0 * pairs.total * c_in * c_out
+    # compulsory bytes: x and dy rows, the pair lists, dW
+    nbytes = 4 * (x.size(0) * c_in + dy.size(0) * c_out + K * c_in * c_out) + 8 * pairs.total
+    _record(kind + "/x6", flops, lambda: call(
+        "msp_conv_wgrad", ptr(x), c_in, ptr(dy), c_out, ptr(pin), ptr(pout), ptr(pairs.off_start), K,
+        n_pieces, ptr(slab), ptr(dw), _stream(x)), nbytes)
     return dw
 
 
@@ -203,7 +212,7 @@ class SubmanifoldConvFunction(torch.autograd.Function):
             if int(_lib.query("msp_wgrad_band_ok", _lib.I64(V), K, cin_p, cout_p)):
                 dwp = conv_wgrad_band(xp, g, p, K, V)  # rows staged in LDS per band
             else:  # weight gradient beside the backward-data (opt-in)
-                dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K)
+                dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             dxp = conv_tile(g, wp, K, 1, cin_p, rules, xp.size(0), "subm_bwd_data",
@@ -240,11 +249,12 @@ class ConvolutionFunction(torch.autograd.Function):
         dx = dw = None
         join = None
         if ctx.needs_input_grad[1]:
-            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K)
+            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             # dx[fine] = W[o] g[parent]: src = coarse (pair_out), dst = fine (pair_in)
-            dxp = conv_pairs(g, wp, K, cin_p, p, p.pair_out, p.pair_in, xp.size(0))
+            dxp = conv_pairs(g, wp, K, cin_p, p, p.pair_out, p.pair_in, xp.size(0), "conv_bwd_data",
+                             2.0 * p.total * cin * cout)
             dx = dxp if cin_p == cin else dxp[:, :cin]
         if join is not None:
             join()
@@ -264,7 +274,7 @@ class DeconvolutionFunction(torch.autograd.Function):
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
         wt = wp.transpose(1, 2).contiguous()
         p = rules.pairs
-        out = conv_pairs(xp, wt, K, cout_p, p, p.pair_out, p.pair_in, n_fine)
+        out = conv_pairs(xp, wt, K, cout_p, p, p.pair_out, p.pair_in, n_fine, "deconv_fwd", 2.0 * p.total * cin * cout)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims = rules, (cin, cout)
         return out if cout_p == cout else out[:, :cout].contiguous()
@@ -279,7 +289,7 @@ class DeconvolutionFunction(torch.autograd.Function):
         dx = dw = None
         join = None
         if ctx.needs_input_grad[1]:
-            dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K)
+            dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K, 2.0 * p.total * cin * cout)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             dxp = conv_tile(g, wp, K, 0, cin_p, rules, xp.size(0), "deconv_bwd_data",
@@ -291,25 +301,35 @@ class DeconvolutionFunction(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------ network-in-network
+_ARANGE = {}  # device index -> int32 arange, grown on demand (identity pair lists)
+
+
 class _IdentityPairs:
-    """Pair lists of the per-site linear map: row i -> row i (one 'offset')."""
+    """Pair lists of the per-site linear map: row i -> row i (one 'offset').
+    Built with device fills only (no host-to-device copy that would
+    synchronise the host inside backward)."""
 
     def __init__(self, n, device):
         self.total = int(n)
-        self.off_start = torch.tensor([0, n], dtype=torch.int64, device=device)
-        self.pair = torch.arange(max(n, 1), dtype=torch.int32, device=device)
+        self.off_start = torch.zeros(2, dtype=torch.int64, device=device)
+        self.off_start[1:].fill_(self.total)
+        ar = _ARANGE.get(device.index)
+        if ar is None or ar.numel() < max(n, 1):
+            ar = _ARANGE[device.index] = torch.arange(max(n, 1 << 16), dtype=torch.int32, device=device)
+        self.pair = ar[:max(n, 1)]
 
 
-def nin_gemm(a, b, force=False):
+def nin_gemm(a, b, force=False, kind="nin"):
     """a[M][K] @ b[K][N] on msp_nin_gemm (HBM-bound tall-skinny product) where the library prefers it
     (msp_nin_gemm_preferred: >= 2^18 rows); other shapes run torch's device GEMM (hipBLASLt)."""
     M, K = a.shape
     N = b.size(1)
+    flops, nbytes = 2.0 * M * K * N, 4 * (M * K + M * N + K * N)
     q = "msp_nin_gemm_ok" if force else "msp_nin_gemm_preferred"
     if not _lib.query(q, _lib.I64(M), K, N) or a.data_ptr() % 16 or b.data_ptr() % 16:
-        return a @ b
+        return _record(kind + "/blas", flops, lambda: a @ b, nbytes)
     out = torch.empty((M, N), dtype=torch.float32, device=a.device)
-    call("msp_nin_gemm", ptr(a), M, K, ptr(b), N, ptr(out), _stream(a))
+    _record(kind + "/hip", flops, lambda: call("msp_nin_gemm", ptr(a), M, K, ptr(b), N, ptr(out), _stream(a)), nbytes)
     return out
 
 
@@ -324,7 +344,7 @@ class NetworkInNetworkFunction(torch.autograd.Function):
         _check_feats(x)
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
-        return nin_gemm(x, weight.contiguous())
+        return nin_gemm(x, weight.contiguous(), kind="nin_fwd")
 
     @staticmethod
     def backward(ctx, gout):
@@ -332,12 +352,13 @@ class NetworkInNetworkFunction(torch.autograd.Function):
         g = gout.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = nin_gemm(g, weight.t().contiguous())
+            dx = nin_gemm(g, weight.t().contiguous(), kind="nin_bwd_data")
         if ctx.needs_input_grad[1]:
             cin, cout = weight.shape
             cin_p, cout_p = _pad16(cin), _pad16(cout)
             p = _IdentityPairs(x.size(0), x.device)
-            dw = conv_wgrad(_pad_cols(x, cin_p), _pad_cols(g, cout_p), p, p.pair, p.pair, 1)[0, :cin, :cout]
+            dw = conv_wgrad(_pad_cols(x, cin_p), _pad_cols(g, cout_p), p, p.pair, p.pair, 1, "nin_wgrad",
+                            2.0 * p.total * cin * cout)[0, :cin, :cout]
         return dx, dw
 
 
@@ -353,14 +374,18 @@ def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, tra
     V, C = x.shape
     s = _stream(x)
     stats = torch.empty((5, C), dtype=torch.float32, device=x.device)
-    if partial is None:
-        partial = _bn_partial_buf(V, C, x.device)
-        if train:
-            call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
-    call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
-         ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
     y = torch.empty_like(x)
-    call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
+
+    def run(partial=partial):
+        if partial is None:
+            partial = _bn_partial_buf(V, C, x.device)
+            if train:
+                call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
+        call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
+             ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
+        call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
+    # compulsory bytes: statistics pass (read x) unless a join produced them, apply (read x, write y)
+    _record("bn_fwd/hbm", 0, run, 4 * V * C * (3 if (partial is None and train) else 2))
     return y, stats
 
 
@@ -371,12 +396,17 @@ def _bn_bwd(x, weight, stats, cfg, gy, addend):
     V, C = x.shape
     s = _stream(x)
     partial = _bn_partial_buf(V, C, x.device)
-    call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
     dx = torch.empty_like(x)
     dw = torch.empty(C, dtype=torch.float32, device=x.device)
     db = torch.empty(C, dtype=torch.float32, device=x.device)
-    call("msp_bn_bwd_apply_add", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats), ptr(weight) if has_w else None,
-         leak, train, ptr(addend) if addend is not None else None, ptr(dx), ptr(dw), ptr(db), s)
+
+    def run():
+        call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
+        call("msp_bn_bwd_apply_add", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats),
+             ptr(weight) if has_w else None, leak, train, ptr(addend) if addend is not None else None, ptr(dx),
+             ptr(dw), ptr(db), s)
+    # compulsory bytes: statistics pass (read x, dy), apply (read x, dy [, shortcut grad], write dx)
+    _record("bn_bwd/hbm", 0, run, 4 * V * C * (5 + (addend is not None)))
     return dx, (dw if has_w else None), (db if has_b else None)
 
 
@@ -442,7 +472,8 @@ class ResidualJoinFunction(torch.autograd.Function):
         V, C = a.shape
         out = torch.empty_like(a)
         partial = _bn_partial_buf(V, C, a.device)
-        call("msp_add_bn_stats", ptr(a), ptr(b), V, C, ptr(out), ptr(partial), _stream(a))
+        _record("bn_join/hbm", 0, lambda: call("msp_add_bn_stats", ptr(a), ptr(b), V, C, ptr(out), ptr(partial),
+                                                _stream(a)), 12 * V * C)
         ctx.mark_non_differentiable(partial)
         return out, partial
 

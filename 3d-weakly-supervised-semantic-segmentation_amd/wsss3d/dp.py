@@ -25,22 +25,27 @@ import torch
 import torch.distributed as dist
 
 
-def init_from_env(device_type: str = "cuda"):
-    """Returns (rank, world, local_rank, device)."""
+def init_from_env(device_type: str = "cuda", backend: str | None = None, device_index: int | None = None):
+    """Returns (rank, world, local_rank, device).  backend: "nccl" (RCCL, the
+    default on GPUs) or "gloo" (the default on CPU; also lets several ranks
+    share one GPU in tests, which RCCL refuses).  device_index overrides
+    LOCAL_RANK as the GPU this rank uses."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if device_type == "cuda":
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        idx = local if device_index is None else int(device_index)
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if device_type == "cuda":
+        backend = backend or ("nccl" if device_type == "cuda" else "gloo")
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group(backend)
     return rank, world, local, device
 
 

@@ -75,22 +75,14 @@ class SparseConvBase_(nn.Module):
         """Per-scene means straight from the level-0 voxel rows
         (ops.SceneMeanFunction).  Valid when scene b is exactly the points of
         batch id b: batch column non-decreasing and the first/last point of
-        every range carrying its index; otherwise the per-point path runs."""
-        off = [int(o) for o in batch_offsets]
-        B = len(off) - 1
+        every range carrying its index; otherwise the per-point path runs.
+        The check compares the offsets with the scene starts the InputLayer
+        read back together with its voxel count (InputRules.scene_ranges_match),
+        so this path issues no device-to-host read of its own."""
+        B = len(batch_offsets) - 1
         t = self.encoder[:-1]([coords, feats])
         rules = t.metadata.input
-        ok = B >= 1 and rules.batch_monotonic and rules.batch_size <= B and off[0] == 0 and off[-1] == coords.size(0)
-        if ok:
-            idx, want = [], []
-            for b in range(B):
-                if off[b + 1] > off[b]:
-                    idx += [off[b], off[b + 1] - 1]
-                    want += [b, b]
-            if idx:
-                got = coords[torch.tensor(idx, device=coords.device), -1].tolist()
-                ok = [int(v) for v in got] == want
-        if not ok:
+        if not rules.scene_ranges_match(batch_offsets):
             return self.postProcessing(self.encoder[-1](t), batch_offsets)
         lvl = t.metadata.level(int(t.spatial_size[0]))
         out, _ = SceneMeanFunction.apply(t.features, lvl, rules, B)

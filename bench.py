@@ -6,21 +6,34 @@ ScanNet-shaped scenes per GPU, MultiLabel head + multilabel soft-margin loss.
 A step = zero_grad -> forward (metadata built on the device from raw coords)
 -> loss -> backward -> Adam step, on batches already resident in HBM.
 value = sum over ranks of level-0 active voxels per step x steps / max-over-
-ranks wall time.  N>1: one process per GPU (torchrun), each rank its own
-scenes (weak scaling), DDP gradient all-reduce over RCCL.
+ranks wall time.  N>1: one process per GPU, each rank its own scenes (weak
+scaling), DDP gradient all-reduce over RCCL.  `python bench.py --gpus N`
+without torchrun's environment starts the N ranks itself (a torch.distributed.run
+child, launched before this process touches the GPU) and passes rank 0's line
+through.  --preset c2/c3/c4/c5 selects BASELINE.json configs[1..4] (c4 =
+the headline network at 5 scenes per GPU).
 
-Also reported: roofline of the dominant kernel (msp_conv_tile / msp_conv_nbr: bf16 MFMA on
-exact three-piece splits -- six bf16 products per fp32 multiply-add -- so the
-peak is 2500/6 TF/s fp32-equivalent; a call on the f32-MFMA forms would be
-priced at 157.3 and the peak reported is the FLOP-weighted mix)
-timed live with HIP events on its launch stream during the timed steps, and
-the CPU oracle path (fp32, torch threads) on a bounded sample on rank 0.
+Also reported: roofline of the dominant kernel family (msp_conv_tile /
+msp_conv_nbr: bf16 MFMA on exact three-piece splits -- six bf16 products per
+fp32 multiply-add -- so the peak is 2500/6 TF/s fp32-equivalent; a call on the
+f32-MFMA forms would be priced at 157.3 and the peak reported is the
+FLOP-weighted mix) and of every other recorded family (weight gradients,
+one-contribution convolutions, NetworkInNetwork, BatchNorm), each call timed
+live with HIP events on its launch stream during the timed steps; the
+step-level roofline of SURVEY.md §8(d) (t_roof = max(B_alg / 8 TB/s,
+F_alg / peak), F_alg = 6 x the forward multiply-add counter); and the CPU
+oracle path (fp32, all host cores available to the process) on a bounded
+sample on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -38,24 +51,44 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md chip table (f32 MFMA = f32 
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # same table, dense
 # split-bf16 ("x6") convolutions: six bf16 MFMA products per fp32 multiply-add
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6.0
+HBM_PEAK_GBS = 8000.0
+
+# recorded kinds (sparseconvnet/ops.py _record) -> family
+CONV_KINDS = ("subm_fwd", "conv_fwd", "subm_bwd_data", "deconv_bwd_data")
+FAMILIES = {"wgrad": "wgrad", "nin_wgrad": "wgrad", "conv_bwd_data": "pairs", "deconv_fwd": "pairs",
+            "nin_fwd": "nin", "nin_bwd_data": "nin", "bn_fwd": "bn", "bn_bwd": "bn", "bn_join": "bn"}
+
+
+def family(kind):
+    base = kind.split("/")[0]
+    return "conv" if base in CONV_KINDS else FAMILIES.get(base, base)
 
 
 def kind_peak(kind):
     return X6_PEAK_TFLOPS if kind.endswith("/x6") or kind.endswith("/x6g") else FP32_MFMA_PEAK_TFLOPS
-HBM_PEAK_GBS = 8000.0
+
+
+PRESETS = {  # BASELINE.json configs[1..4]
+    "c2": dict(workload="unet", m=16, reps=1, residual=0, scale=50, batch=4),
+    "c3": dict(workload="unet", m=32, reps=2, residual=1, scale=50, batch=8),
+    "c4": dict(workload="unet", m=32, reps=2, residual=1, scale=50, batch=5),
+    "c5": dict(workload="contrastive", m=32, reps=1, residual=0, scale=20, batch=8),
+}
 
 
 class KernelRecorder:
-    """Brackets every msp_conv_tile / msp_conv_nbr launch with torch.cuda.Events on the
-    current stream (the stream the kernel is launched on) and accumulates the
-    algorithmic FLOPs (2 * rules * c_in * c_out) per launch."""
+    """Brackets every recorded library call (sparseconvnet/ops.py _record: the conv family, weight
+    gradients, one-contribution convolutions, NetworkInNetwork, BatchNorm) with torch.cuda.Events on the
+    current stream -- the stream the kernels are launched on -- and accumulates each call's algorithmic
+    FLOPs and compulsory bytes.  mode "conv" records the conv family only."""
 
-    def __init__(self):
+    def __init__(self, mode="all"):
         self.events = []
         self.active = False
+        self.mode = mode
 
     def run(self, kind, flops, fn, nbytes=0):
-        if not self.active:
+        if not self.active or (self.mode == "conv" and family(kind) != "conv"):
             return fn()
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
@@ -66,20 +99,42 @@ class KernelRecorder:
         return r
 
     def summary(self):
+        """family -> {achieved, peak, frac, bound, unit, ms, launches, bytes, gbs, per_kind}."""
         torch.cuda.synchronize()
-        tot_f, tot_b, tot_ms, n = 0.0, 0.0, 0.0, 0
         per = {}
         for kind, f, nb, s, e in self.events:
-            ms = s.elapsed_time(e)
-            tot_f += f
-            tot_b += nb
-            tot_ms += ms
-            n += 1
-            k = per.setdefault(kind, [0, 0.0, 0.0])
+            k = per.setdefault(kind, [0, 0.0, 0.0, 0.0])
             k[0] += 1
             k[1] += f
-            k[2] += ms
-        return tot_f, tot_b, tot_ms, n, per
+            k[2] += nb
+            k[3] += s.elapsed_time(e)
+        fams = {}
+        for kind, (n, f, nb, ms) in per.items():
+            d = fams.setdefault(family(kind), {"launches": 0, "flops": 0.0, "bytes": 0.0, "ms": 0.0,
+                                               "t_peak": 0.0, "per_kind": {}})
+            d["launches"] += n
+            d["flops"] += f
+            d["bytes"] += nb
+            d["ms"] += ms
+            d["t_peak"] += f / (kind_peak(kind) * 1e12)
+            sec = ms * 1e-3
+            d["per_kind"][kind] = {"launches": n, "ms": ms,
+                                   "tflops": f / sec / 1e12 if sec and f else 0.0,
+                                   "gbs": nb / sec / 1e9 if sec else 0.0}
+        out = {}
+        for fam, d in fams.items():
+            sec = d["ms"] * 1e-3
+            gbs = d["bytes"] / sec / 1e9 if sec else 0.0
+            if d["flops"] > 0:
+                achieved = d["flops"] / sec / 1e12 if sec else 0.0
+                peak = d["flops"] / d["t_peak"] / 1e12 if d["t_peak"] else FP32_MFMA_PEAK_TFLOPS
+                bound, unit = "mfma", "TFLOP/s"
+            else:
+                achieved, peak, bound, unit = gbs, HBM_PEAK_GBS, "hbm", "GB/s"
+            out[fam] = {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+                        "frac": achieved / peak if peak else 0.0, "ms": d["ms"], "launches": d["launches"],
+                        "bytes": d["bytes"], "gbs": gbs, "per_kind": d["per_kind"]}
+        return out
 
 
 def pmc_traffic():
@@ -102,13 +157,42 @@ def level_stats(meta):
     return out
 
 
-def cpu_baseline(args, batch):
-    """CPU oracle (fp32, SCN-CPU-structured gather -> mm -> scatter-add) on a
-    bounded sample: the first scene of the batch, one fwd+bwd."""
-    from oracle.encoders import OracleEncoder
-    from wsss3d.synthetic import train_merge  # noqa: F401
+def host_cores():
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota if one is set (on
+    the GPU box os.cpu_count() reports the whole machine while the job gets a share of it)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    cores = max(1, min(n, int(math.ceil(quota))) if quota else n)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return cores, {"affinity_cpus": n, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(),
+                   "cpu_model": model}
 
-    threads = int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+
+def cpu_baseline(args, batch, iters=3):
+    """CPU oracle (fp32, SCN-CPU-structured gather -> MKL mm -> scatter-add, torch threads = every core
+    available to the process) on a bounded sample: the first scene of the batch, one warm-up then the
+    median of `iters` fwd+bwd steps (each step rebuilds the voxelisation and rulebooks, as SCN's CPU
+    path does per forward)."""
+    from oracle.encoders import OracleEncoder
+
+    cores, info = host_cores()
+    threads = int(os.environ.get("BENCH_CPU_THREADS", cores))
+    prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     off = batch["batch_offsets"]
     n0 = off[1]
@@ -120,15 +204,38 @@ def cpu_baseline(args, batch):
     lin = torch.nn.Linear(args.m, 20)
     y = torch.from_numpy(batch["scene_labels"][:1])
     x = dict(coords=coords, feature=feats, batch_offsets=[0, n0])
-    t0 = time.perf_counter()
-    feats_out = ref(x, istrain=True)
-    loss = torch.nn.functional.multilabel_soft_margin_loss(lin(feats_out), y)
-    loss.backward()
-    dt = time.perf_counter() - t0
+    times = []
+    for it in range(iters + 1):
+        ref.zero_grad(set_to_none=True)
+        t0 = time.perf_counter()
+        feats_out = ref(x, istrain=True)
+        loss = torch.nn.functional.multilabel_soft_margin_loss(lin(feats_out), y)
+        loss.backward()
+        dt = time.perf_counter() - t0
+        if it:
+            times.append(dt)
+    torch.set_num_threads(prev)
+    med = statistics.median(times)
     V0 = len(np.unique(batch["coords"][:n0], axis=0))
-    return {"value": V0 / dt, "unit": "active-voxels/s", "cores": threads, "kind": "port",
-            "sample": f"1 scene of the workload ({n0} points, {V0} L0 voxels), 1 fwd+bwd step, fp32, "
-                      f"oracle/scn_oracle.py on {threads} torch threads ({dt:.2f} s)"}
+    return {"value": V0 / med, "unit": "active-voxels/s", "cores": threads, "kind": "port",
+            "cpu_model": info["cpu_model"], "host": info,
+            "sample": f"1 scene of the workload ({n0} points, {V0} L0 voxels), fwd+bwd, fp32, "
+                      f"oracle/scn_oracle.py on {threads} torch threads: 1 warm-up + median of {iters} "
+                      f"({', '.join(f'{t:.2f}' for t in times)} s)"}
+
+
+def launch_ranks(n):
+    """Start n ranks (torch.distributed.run child, one process per GPU) before this process touches the
+    GPU; rank 0 prints the JSON line.  Returns the child's exit code."""
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -136,31 +243,44 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="scenes per GPU")
-    ap.add_argument("--scale", type=float, default=50)
-    ap.add_argument("--m", type=int, default=32)
-    ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--residual", type=int, default=1)
+    ap.add_argument("--preset", choices=sorted(PRESETS), default=None,
+                    help="BASELINE.json configs[1..4]: c2 UNet m16 r1 VGG b4, c3 (default) UNet m32 r2 residual b8, "
+                         "c4 the same at 5 scenes per GPU, c5 MultiLabelContrastive FCNet m32 + text")
+    ap.add_argument("--batch", type=int, default=None, help="scenes per GPU (default 8)")
+    ap.add_argument("--scale", type=float, default=None)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--reps", type=int, default=None)
+    ap.add_argument("--residual", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-iters", type=int, default=3, help="timed cpu_baseline iterations (median)")
+    ap.add_argument("--record", choices=["all", "conv", "none"], default="all",
+                    help="HIP-event bracketing of the recorded calls in the timed steps (roofline): every "
+                         "recorded family, the conv family only, or none")
     ap.add_argument("--foreach-adam", action="store_true", help="torch's foreach Adam instead of the fused one")
     ap.add_argument("--concurrent-wgrad", action="store_true",
                     help="weight gradients on a side stream beside the backward-data (sparseconvnet.ops)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="build each batch's metadata inside its own forward (no side-stream input pipelining)")
-    ap.add_argument("--workload", choices=["unet", "contrastive"], default="unet",
+    ap.add_argument("--workload", choices=["unet", "contrastive"], default=None,
                     help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
                          "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
                          "(CLIP text-tower shape: width 512, 12 layers, context 120, vocab 49408), 10 texts per "
                          "scene, Classification + TextContrastive losses")
     args = ap.parse_args()
-    if args.workload == "contrastive":
-        if args.scale == 50:
-            args.scale = 20
-        args.reps, args.residual = 1, 0
+    preset = args.preset or ("c5" if args.workload == "contrastive" else "c3")
+    for k, v in PRESETS[preset].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     from wsss3d import dp
 
     rank, world, local, dev = dp.init_from_env("cuda")
+    if rank == 0 and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
+              file=sys.stderr)
 
     import sparseconvnet as scn
     from sparseconvnet import _lib
@@ -202,6 +322,7 @@ def main():
                       residual_blocks=bool(args.residual))
         cls, _ = MODEL_REGISTRY.get("MultiLabel")
         model = dp.wrap(cls(pc).to(dev), dev)
+    n_params = sum(p.numel() for p in model.parameters())
     # the reference's optimizer (train.py:39, Adam lr 1e-3); one fused multi-tensor kernel per step
     # (--foreach-adam: torch's default foreach form, ~21 launches per step)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else {"fused": True}))
@@ -225,8 +346,8 @@ def main():
 
     for i in range(args.warmup):
         step(i)
-    rec = KernelRecorder()
-    _lib.set_recorder(rec)
+    rec = KernelRecorder(args.record)
+    _lib.set_recorder(rec if args.record != "none" else None)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -241,9 +362,8 @@ def main():
     rec.active = False
     vox = sum(batches[i % len(batches)][2] for i in range(args.steps))
     dt_max, vox_all = dp.max_over_ranks(dt), dp.sum_over_ranks(float(vox))
-
-    flops, abytes, kms, nlaunch, per = rec.summary()
     _lib.set_recorder(None)
+    fams = rec.summary()
 
     # one untimed forward for the per-level statistics and the MAC counter
     scn.forward_pass_multiplyAdd_count = 0
@@ -259,11 +379,8 @@ def main():
     macs = scn.forward_pass_multiplyAdd_count
 
     if rank == 0:
-        achieved = flops / (kms * 1e-3) / 1e12 if kms > 0 else 0.0
-        # effective peak of the mix: the rate at which these FLOPs would run
-        # if every call ran at its own path's MFMA peak
-        t_peak = sum(v[1] / (kind_peak(k) * 1e12) for k, v in per.items())
-        peak = flops / t_peak / 1e12 if t_peak > 0 else FP32_MFMA_PEAK_TFLOPS
+        ms_step = dt_max / args.steps * 1e3
+        conv = fams.get("conv")
         traffic, traffic_src = pmc_traffic()
         if contrastive:
             workload = (f"MultiLabelContrastive: SparseConvFCNet m={args.m} block_reps={args.reps} scale="
@@ -282,7 +399,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": dt_max / args.steps * 1e3,
+            "ms_per_step": ms_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -291,6 +408,7 @@ def main():
                     "random-init weights",
             "config": {
                 "workload": workload,
+                "preset": preset,
                 "scenes_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world}",
@@ -299,30 +417,52 @@ def main():
                 "active_voxels_per_step_rank0": batches[0][2],
                 "levels": stats,
                 "fwd_multiply_adds": macs,
+                "parameters": n_params,
             },
-            "roofline": {
+        }
+        if conv is not None:
+            res["roofline"] = {
                 "kernel": "msp_conv_tile / msp_conv_nbr (submanifold fwd/bwd-data, strided conv fwd, deconv bwd-data)",
                 "bound": "mfma",
-                "achieved": achieved,
-                "peak": peak,
+                "achieved": conv["achieved"],
+                "peak": conv["peak"],
                 "peak_note": f"mix of f32 MFMA ({FP32_MFMA_PEAK_TFLOPS} TF/s) and split-bf16 MFMA "
                              f"({BF16_MFMA_PEAK_TFLOPS:g}/6 = {X6_PEAK_TFLOPS:.1f} TF/s fp32-equivalent) weighted by "
                              "each path's FLOPs",
                 "unit": "TFLOP/s",
-                "frac": achieved / peak,
+                "frac": conv["frac"],
                 "traffic": traffic,
                 "traffic_unit": "HBM bytes per msp_conv_tile / msp_conv_nbr call (PMC 2*FETCH_SIZE + WRITE_SIZE)",
                 "traffic_source": traffic_src,
-                "alg_bytes_per_call": abytes / max(nlaunch, 1),
-                "alg_bytes_gbs": abytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0,
-                "launches": nlaunch,
-                "avg_launch_us": kms / max(nlaunch, 1) * 1e3,
-                "per_kind": {k: {"launches": v[0], "tflops": v[1] / (v[2] * 1e-3) / 1e12 if v[2] else 0.0,
-                                 "ms": v[2]} for k, v in per.items()},
-            },
-        }
+                "alg_bytes_per_call": conv["bytes"] / max(conv["launches"], 1),
+                "alg_bytes_gbs": conv["gbs"],
+                "launches": conv["launches"],
+                "avg_launch_us": conv["ms"] / max(conv["launches"], 1) * 1e3,
+                "per_kind": conv["per_kind"],
+            }
+            res["roofline_families"] = {
+                f: {k: v for k, v in d.items() if k != "per_kind" and k != "bytes"} | {"per_kind": d["per_kind"]}
+                for f, d in fams.items() if f != "conv"}
+            # step level: F_alg = 6 x forward MACs (fwd, bwd-data, bwd-weight), B_alg = the
+            # compulsory bytes of every recorded call + the Adam step (param, grad, 2 moments read; 3 written)
+            f_alg = 6.0 * macs
+            b_rec = sum(d["bytes"] for d in fams.values()) / args.steps
+            b_alg = b_rec + 28.0 * n_params
+            t_hbm = b_alg / (HBM_PEAK_GBS * 1e9) * 1e3
+            t32 = f_alg / (FP32_MFMA_PEAK_TFLOPS * 1e12) * 1e3
+            tx6 = f_alg / (X6_PEAK_TFLOPS * 1e12) * 1e3
+            res["step_roofline"] = {
+                "F_alg_tflop": f_alg / 1e12, "B_alg_gb": b_alg / 1e9,
+                "t_roof_ms_fp32_peak": max(t_hbm, t32), "frac_fp32_peak": max(t_hbm, t32) / ms_step,
+                "t_roof_ms_x6_peak": max(t_hbm, tx6), "frac_x6_peak": max(t_hbm, tx6) / ms_step,
+                "hbm_frac": t_hbm / ms_step,
+                "recorded_ms_per_step": sum(d["ms"] for d in fams.values()) / args.steps,
+                "note": "t_roof = max(B_alg / 8 TB/s, F_alg / peak); fp32 peak = 157.3 TF/s (f32 MFMA, the "
+                        "arithmetic's native rate), x6 peak = 2500/6 TF/s (the split-bf16 path the convolutions "
+                        "take); frac = t_roof / measured ms_per_step",
+            }
         if world == 1 and not args.no_cpu and not contrastive:
-            res["cpu_baseline"] = cpu_baseline(args, host_batches[0])
+            res["cpu_baseline"] = cpu_baseline(args, host_batches[0], args.cpu_iters)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -61,6 +61,16 @@ const char* msp_last_error(void);
 int msp_point_keys(const int64_t* coords, int64_t n, int64_t row_stride, int log2_size, int64_t spatial_size,
                    uint64_t* keys, int32_t* vals, int64_t* stats, msp_stream_t stream);
 
+/* Scene boundaries of a non-decreasing batch column (msp_point_keys stats[2]
+ * == 0): starts[b] = first row whose batch id is >= b, for b = 0..n_batch
+ * (n_batch + 1 entries; starts[n_batch] = n when n_batch > max batch id).  The
+ * caller reads them back together with the voxel count, so checking that the
+ * reference's batch_offsets (dataset/data.py:142,209) are exactly the batch-id
+ * ranges (the fused per-scene mean, models/SparseConvNet.py:20-26) needs no
+ * extra device-to-host read. */
+int msp_batch_starts(const int64_t* coords, int64_t n, int64_t row_stride, int64_t n_batch, int64_t* starts,
+                     msp_stream_t stream);
+
 size_t msp_sort_workspace_size(int64_t n, int end_bit);
 /* Stable LSD radix sort of (key, value) pairs on bits [0, end_bit). */
 int msp_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* vals_in, int32_t* vals_out,

@@ -1,0 +1,107 @@
+"""Data parallelism around the HIP model: two ranks spawned on cuda:0 (gloo -- RCCL
+refuses two ranks on one device), each running the device SparseConvUNet + MultiLabel head under
+wsss3d.dp.wrap with the residual fork/join fusions on and the second step's metadata prefetched on the
+side stream, as bench.py runs it.  DDP's averaged gradients must equal the mean of the ranks' local
+gradients of an identical unwrapped model on the same batch, and the parameters must be identical on
+both ranks after the fused Adam step."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "3d-weakly-supervised-semantic-segmentation_amd"), root):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    import sparseconvnet as scn
+    from sparseconvnet import modules
+    from wsss3d import EasyDict, MODEL_REGISTRY, dp
+    from wsss3d.synthetic import make_batch
+
+    try:
+        r, w, _, dev = dp.init_from_env("cuda", backend="gloo", device_index=0)
+        assert modules.FUSE_RESIDUAL
+        pc = EasyDict(name="SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=2,
+                      residual_blocks=True)
+        cls, _ = MODEL_REGISTRY.get("MultiLabel")
+        torch.manual_seed(0)
+        local = cls(pc).to(dev)
+        torch.manual_seed(0)
+        model = dp.wrap(cls(pc).to(dev), dev)
+        assert isinstance(model, torch.nn.parallel.DistributedDataParallel)
+        bs = [make_batch(2, 20, seed=10 * r + k) for k in range(2)]
+        xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(dev), feature=torch.from_numpy(b["feats"]).to(dev),
+                       batch_offsets=b["batch_offsets"]) for b in bs]
+        ys = [torch.from_numpy(b["scene_labels"]).to(dev) for b in bs]
+
+        def loss_of(net, k):
+            logits, _ = net((xs[k], None), istrain=True)
+            return F.multilabel_soft_margin_loss(logits, ys[k])
+
+        # step 0 (records the rulebook plan), then the next batch's metadata on the side stream
+        loss_of(model, 0).backward()
+        model.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        assert scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False) is not None
+        loss_of(model, 1).backward()           # consumes the prefetched metadata
+        loss_of(local, 1).backward()
+        ok = True
+        inner = model.module
+        for (k, p), q in zip(inner.named_parameters(), local.parameters()):
+            g = q.grad.clone()
+            dist.all_reduce(g)
+            g /= w
+            if not torch.allclose(p.grad, g, rtol=1e-6, atol=1e-9):
+                ok = False
+                print(f"rank {r}: grad {k} differs by {(p.grad - g).abs().max().item():.3e}", flush=True)
+        # the two ranks' local gradients differ (different scenes), the averaged ones agree
+        opt = torch.optim.Adam(inner.parameters(), lr=1e-3, fused=True)
+        opt.step()
+        flat = torch.cat([p.detach().flatten() for p in inner.parameters()])
+        ref = flat.clone()
+        dist.broadcast(ref, 0)
+        ok &= torch.equal(flat, ref)
+        lg = torch.cat([q.grad.flatten() for q in local.parameters()])
+        other = lg.clone()
+        dist.broadcast(other, 1)
+        ok &= (r == 1) or not torch.equal(lg, other)
+        out[rank] = bool(ok)
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        out[rank] = f"{type(e).__name__}: {e}"
+        raise
+
+
+def test_ddp_world2_hip_model():
+    ctx = mp.get_context("spawn")
+    manager = ctx.Manager()
+    out = manager.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert dict(out) == {0: True, 1: True}, dict(out)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

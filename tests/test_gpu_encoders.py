@@ -190,3 +190,62 @@ def test_metadata_prefetch_matches_inline():
     assert torch.equal(out, ref_out)
     for a, b in zip(g, ref_g):
         assert torch.equal(a, b)
+
+
+def _prefetch_model():
+    from wsss3d import EasyDict
+    torch.manual_seed(0)
+    cls, _ = MODEL_REGISTRY.get("MultiLabel")
+    pc = EasyDict(name="SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=1, residual_blocks=True)
+    model = cls(pc).to(DEV)
+    bs = [make_batch(2, 20, seed=s) for s in (21, 22)]
+    xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(DEV), feature=torch.from_numpy(b["feats"]).to(DEV),
+                   batch_offsets=b["batch_offsets"]) for b in bs]
+    ys = [torch.from_numpy(b["scene_labels"]).to(DEV) for b in bs]
+    return model, xs, ys
+
+
+def test_prefetched_step_has_no_host_read():
+    """A training step whose metadata was prefetched (the bench loop: forward with the fused tail, loss,
+    backward, fused Adam) issues no device-to-host read or synchronising copy: torch's sync debug mode
+    raises on any (.item(), .tolist(), blocking copies)."""
+    import torch.nn.functional as F
+    model, xs, ys = _prefetch_model()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+
+    def step(k):
+        opt.zero_grad(set_to_none=True)
+        logits, _ = model((xs[k], None), istrain=True)
+        F.multilabel_soft_margin_loss(logits, ys[k]).backward()
+        opt.step()
+
+    step(0)                                   # records the plan, builds the optimizer state
+    torch.cuda.synchronize()
+    assert scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False) is not None
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        step(1)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(p).all() for p in model.parameters())
+
+
+def test_prefetch_entry_needs_the_same_tensor():
+    """The prefetched entry is found only through the very coords tensor it was built for (a copy at
+    another address, or a new tensor at a reused address, builds its own metadata), and a newer prefetch
+    drops an unconsumed older one."""
+    from sparseconvnet import metadata as md
+    model, xs, _ = _prefetch_model()
+    with torch.no_grad():
+        model(xs[0])                           # records the plan
+        m = scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False)
+        twin = xs[1].coords.clone()
+        assert md.take_prefetched(twin, 4096) is None
+        assert md._PREFETCHED                  # still pending for the original tensor
+        m2 = scn.prefetch_metadata(model, xs[0].coords, wait_for_producer=False)
+        assert len(md._PREFETCHED) == 1        # the older entry was dropped
+        assert md.take_prefetched(xs[1].coords, 4096) is None
+        assert md.take_prefetched(xs[0].coords, 4096) is m2 and m2 is not m
+        assert not md._PREFETCHED

@@ -199,3 +199,30 @@ def test_reference_model_file_runs_on_this_package():
                                            residual_blocks=res)
         a, b = ref_enc.state_dict(), ours.state_dict()
         assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a), name
+
+
+def test_scene_ranges_match_host_logic():
+    """The fused tail's validity check (InputRules.scene_ranges_match): scene b of batch_offsets must be
+    exactly the points of batch id b, decided from the scene starts read back with the voxel count."""
+    from sparseconvnet.metadata import InputRules
+    r = InputRules(10, None, None, None, 3)
+    r.batch_monotonic, r.scene_starts = True, [0, 4, 4, 10]     # ids 0..2, id 1 empty
+    assert r.scene_ranges_match([0, 4, 4, 10])
+    assert r.scene_ranges_match([0, 4, 4, 10, 10])              # a trailing empty scene
+    assert not r.scene_ranges_match([0, 3, 4, 10])
+    assert not r.scene_ranges_match([0, 4, 10])                 # fewer scenes than batch ids
+    assert not r.scene_ranges_match([0, 10])
+    r.batch_monotonic = False
+    assert not r.scene_ranges_match([0, 4, 4, 10])
+    r.batch_monotonic, r.scene_starts = True, None
+    assert not r.scene_ranges_match([0, 4, 4, 10])
+
+
+def test_bench_presets_and_host_cores():
+    import bench
+    assert bench.PRESETS["c3"]["batch"] == 8 and bench.PRESETS["c4"]["batch"] == 5
+    assert bench.PRESETS["c2"]["m"] == 16 and bench.PRESETS["c2"]["residual"] == 0
+    cores, info = bench.host_cores()
+    assert 1 <= cores <= (os.cpu_count() or cores) and info["cpu_model"]
+    assert bench.family("subm_fwd/x6g") == "conv" and bench.family("wgrad/x6") == "wgrad"
+    assert bench.family("bn_fwd/hbm") == "bn" and bench.family("deconv_fwd/f32") == "pairs"
