@@ -1029,6 +1029,12 @@ int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out) {
   return 128;
 }
 
+int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows) {
+  if (n_rows <= 0 || c_in <= 0 || c_out <= 0) return 0;
+  if (tile_rows != 128) return 3;
+  return (c_out <= 32 && c_in <= 64) ? 1 : 2;
+}
+
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows) {
   if (tile_rows != 128 || n_rows <= 0 || c_out <= 0 || K <= 0) return 0;
   if (c_out <= 32 && c_in <= 64) return x6p_ws_bytes(K, c_in, c_out);

@@ -35,6 +35,7 @@ PROTOTYPES = {
     "msp_tile_rulebook": (I, [P, I, I64, I, P, P, P, P, I64, P, SZ, P]),
     "msp_decode_keys": (I, [P, I64, I, P, P]),
     "msp_conv_tile_rows": (I, [I64, I, I]),
+    "msp_conv_tile_form": (I, [I64, I, I, I]),
     "msp_conv_tile_workspace_size": (SZ, [I64, I, I, I, I]),
     "msp_conv_tile": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_nbr_preferred": (I, [I64, I, I]),

@@ -69,7 +69,8 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     if n_rows:
         # the contraction msp_conv_tile runs on 128-row tiles: bf16 MFMA over
         # exact three-piece operand splits (per-wave tiles for narrow outputs)
-        kind += "/x6" if tr == 128 else "/f32"
+        form = int(_lib.query("msp_conv_tile_form", _lib.I64(n_rows), c_in, c_out, tr))
+        kind += {1: "/x6r", 2: "/x6d"}.get(form, "/f32")
         wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(n_rows), K, c_in, c_out, tr))
         ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
         # compulsory bytes: input rows, output rows, weights, rulebook (chunk

@@ -11,10 +11,11 @@ instead of `nn.MultiheadAttention` with an additive -inf mask (same math:
 the reference mask is exactly the causal one, `build_attention_mask`).
 
 Inputs are token ids (B, L) with the end-of-text token the largest id of each
-row (`text.argmax(-1)` picks its position, `:117`).  The reference tokenizer
-(`clip`, `dataset/dataset_utils/text_transform_builder.py`) is not available
-here; callers pass ids.  context_length must equal the padded sequence
-length (the reference's 3DUNetWithText configs pad to max_seq_len = 120).
+row (`text.argmax(-1)` picks its position, `:117`), as produced by
+`wsss3d.tokenizer.text_transform(max_seq_len, cropped_texts)` (the reference's
+fixed-shape tokenizer, `dataset/dataset_utils/text_transform_builder.py:33-76`).
+context_length must equal the padded sequence length (the reference's
+3DUNetWithText configs pad to max_seq_len = 120).
 """
 from __future__ import annotations
 

@@ -65,7 +65,7 @@ def family(kind):
 
 
 def kind_peak(kind):
-    return X6_PEAK_TFLOPS if kind.endswith("/x6") or kind.endswith("/x6g") else FP32_MFMA_PEAK_TFLOPS
+    return X6_PEAK_TFLOPS if "/x6" in kind else FP32_MFMA_PEAK_TFLOPS
 
 
 PRESETS = {  # BASELINE.json configs[1..4]
@@ -277,7 +277,10 @@ def main():
 
     from wsss3d import dp
 
-    rank, world, local, dev = dp.init_from_env("cuda")
+    # BENCH_BACKEND=gloo BENCH_SHARE_DEVICE=1: rehearse N ranks on a one-GPU box (RCCL refuses two ranks on
+    # one device); the measured configuration is RCCL with one GPU per rank
+    rank, world, local, dev = dp.init_from_env("cuda", backend=os.environ.get("BENCH_BACKEND") or None,
+                                               device_index=0 if os.environ.get("BENCH_SHARE_DEVICE") else None)
     if rank == 0 and world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
               file=sys.stderr)
@@ -412,6 +415,7 @@ def main():
                 "scenes_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world}",
+                "comm_backend": dist.get_backend() if world > 1 else None,
                 "input_pipeline": "none" if args.no_prefetch else
                 "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step",
                 "active_voxels_per_step_rank0": batches[0][2],

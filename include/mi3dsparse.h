@@ -145,6 +145,11 @@ int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coo
  * c_out, tile_rows).  msp_conv_tile_rows gives the tile height the library
  * is tuned for. */
 int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out);
+/* Contraction form msp_conv_tile runs for these sizes: 1 = per-wave split-bf16
+ * tile (conv_x6r: c_out <= 32, c_in <= 64), 2 = shared split-bf16 tile (conv_x6d,
+ * split over offsets on small grids), 3 = f32-MFMA tile forms (tile_rows 64 /
+ * 256), 0 = nothing to do. */
+int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows);
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows);
 int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,

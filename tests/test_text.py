@@ -6,6 +6,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 import torch
 
 from wsss3d import EasyDict, LOSS_REGISTRY, MODEL_REGISTRY
@@ -67,3 +68,39 @@ def test_contrastive_head_and_loss_cpu_text():
     assert torch.allclose(loss, want)
     loss.backward()
     assert tm.token_embedding.weight.grad is not None
+
+
+def test_tokenizer_matches_reference_fixture():
+    """wsss3d.tokenizer restates the reference's CLIP BPE + fixed-shape text_transform
+    (dataset/dataset_utils/tokenizer.py, text_transform_builder.py:33-76); token ids are bit-exact
+    against ids the reference tokenizer produced (tests/golden/make_token_golden.py)."""
+    import json
+    import os
+    from wsss3d.tokenizer import SimpleTokenizer, text_transform
+    with open(os.path.join(os.path.dirname(__file__), "golden", "tokens.json")) as f:
+        gold = json.load(f)
+    tok = SimpleTokenizer()
+    assert tok.encoder["<|startoftext|>"] == gold["specials"]["sot"]
+    assert tok.encoder["<|endoftext|>"] == gold["specials"]["eot"]
+    assert len(tok.encoder) == gold["specials"]["vocab"]
+    for e in gold["encode"]:
+        assert tok.encode(e["text"]) == e["ids"], e["text"]
+    for c in gold["text_transform"]:
+        ids = text_transform(c["max_seq_len"], c["cropped_texts"])(c["texts"])
+        assert ids.dtype == torch.long
+        assert ids.tolist() == c["ids"]
+        # end-of-text is each row's largest id (TextTransformer reads the feature at argmax)
+        assert (ids.argmax(-1) == (ids == gold["specials"]["eot"]).long().argmax(-1)).all()
+
+
+def test_tokenizer_roundtrip_and_truncation():
+    from wsss3d.tokenizer import Tokenize, default_tokenizer
+    tok = default_tokenizer()
+    text = "a grey office chair beside the desk"
+    assert tok.decode(tok.encode(text)).strip() == text
+    t = Tokenize(tok, 8)
+    row = t("the sofa is in front of the television and the coffee table")
+    assert row.shape == (8,) and row[0] == 49406 and row[-1] == 49407
+    with pytest.raises(RuntimeError):
+        Tokenize(tok, 8, truncate=False)(["the sofa is in front of the television and the coffee table"])
+    assert Tokenize(tok, 8)([]).shape == (0, 8)
