@@ -1,0 +1,559 @@
+// Tile-local submanifold convolution: the input rows a tile of output rows
+// needs are staged in LDS once, split into bf16 pieces once, and every rule of
+// the tile reads them from there.
+//
+// Why: in Morton order the 128 output rows of a tile are a small surface patch,
+// and their 27-neighbourhoods overlap heavily.  On the headline batch a 128-row
+// tile touches 1.6-2.0 x 128 distinct input rows for 7.8-14.9 rules per row
+// (scripts/tile_stats.py), so each distinct input row serves 5-7 rules.  The
+// gather forms (msp_conv_tile / msp_conv_nbr) fetch and split every rule's row
+// from L2/MALL; here a tile fetches each distinct row once, with all its loads
+// in flight together, and the rule loop touches only LDS.
+//
+// Metadata (msp_tile_local, built once per level and reused by the forward and
+// the backward-data pass):
+//   u_start[t]..u_start[t+1]  the tile's distinct input rows u_rows[], sorted;
+//   lidx[o][t*T + i]          position in that list of the neighbour at offset
+//                             o of the tile's i-th row (0xFFFF: none);
+//   perm[t*T + i]             the tile's i-th row: rows are ordered inside the
+//                             tile by their 27-bit neighbour mask, so 16-row
+//                             groups share offsets (-1: padding past n).
+//
+// Kernel (conv_x6s): block = 4 waves on one T-row tile and one 16 NT-wide
+// output column slice.  Each wave owns a quarter of the filter offsets
+// (o = wave, wave + 4, ...) for ALL the tile's rows, keeping G = T / 16 row
+// groups x NT column tiles of accumulators in registers, and loads its own
+// weight fragments straight into registers (lane-ordered weight image, two
+// steps ahead): no barrier inside the offset loop.  Per (offset, group) the
+// wave reads the group's 16 local indices, skips the group when none has the
+// offset (wave-uniform ballot), reads the three pre-split pieces of each row
+// from LDS and issues 6 NT bf16 MFMAs over the exact splits (the x6 form of
+// msp_conv_x6.hip, six piece products summed in a zeroed accumulator and added
+// once).  The four waves' partial sums are added in wave order through LDS at
+// the end (deterministic).  Input channels are staged 32 at a time.
+#include "msp_x6.h"
+
+namespace msp {
+
+constexpr int kLT = 256;          // threads of the metadata kernels
+constexpr uint16_t kAbsent = 0xFFFF;
+constexpr int kXR = 384;          // LDS rows of a staged 32-channel input slice (last = zero row)
+constexpr int kUCap = kXR - 1;    // distinct input rows a tile can stage; more are read from global
+constexpr int kXU = 12;           // 16-byte units per staged row: 3 pieces x 4 k-octets
+constexpr int kKMax = 27;         // filter volume of the kernel's LDS index tile
+
+// ---------------------------------------------------------------- metadata
+template <int N2>
+__device__ void bitonic_i32(int32_t* a) {
+  for (int k = 2; k <= N2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < N2; i += kLT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const int32_t u = a[i], v = a[ixj];
+          if ((u > v) == ((i & k) == 0)) {
+            a[i] = v;
+            a[ixj] = u;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int N>
+__device__ void bitonic_u64(uint64_t* a) {
+  for (int k = 2; k <= N; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < N; i += kLT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t u = a[i], v = a[ixj];
+          if ((u > v) == ((i & k) == 0)) {
+            a[i] = v;
+            a[ixj] = u;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// the tile's K x T neighbour entries (absent -> INT32_MAX, sorted last), padded to N2
+template <int T, int N2>
+__device__ void load_tile_entries(const int32_t* __restrict__ nbr, int K, int64_t n, int64_t t, int32_t* a) {
+  for (int i = threadIdx.x; i < N2; i += kLT) {
+    int32_t v = INT32_MAX;
+    if (i < K * T) {
+      const int o = i / T, p = i - o * T;
+      const int64_t row = t * T + p;
+      if (row < n) {
+        const int32_t m = nbr[(int64_t)o * n + row];
+        if (m >= 0) v = m;
+      }
+    }
+    a[i] = v;
+  }
+  __syncthreads();
+}
+
+template <int T, int N2>
+__global__ __launch_bounds__(kLT) void local_count_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
+                                                          int64_t* __restrict__ cnt,
+                                                          unsigned long long* __restrict__ mx) {
+  __shared__ int32_t a[N2];
+  __shared__ int wsum[kLT / 64];
+  const int64_t t = blockIdx.x;
+  load_tile_entries<T, N2>(nbr, K, n, t, a);
+  bitonic_i32<N2>(a);
+  int c = 0;
+  for (int i = threadIdx.x; i < N2; i += kLT) c += a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1]);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < kLT / 64; ++w) tot += wsum[w];
+    cnt[t] = tot;
+    atomicMax(mx, (unsigned long long)tot);
+  }
+}
+
+template <int T, int N2>
+__global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
+                                                         int64_t n_pad, const int64_t* __restrict__ u_start,
+                                                         int32_t* __restrict__ u_rows, uint16_t* __restrict__ lidx,
+                                                         int32_t* __restrict__ perm, int order) {
+  constexpr int PER = N2 / kLT;
+  __shared__ int32_t a[N2];
+  __shared__ int32_t uq[N2];
+  __shared__ uint64_t mk[T];
+  const int64_t t = blockIdx.x;
+  load_tile_entries<T, N2>(nbr, K, n, t, a);
+  bitonic_i32<N2>(a);
+  // distinct rows, in order: per-thread runs of PER entries + a block scan
+  const int base = threadIdx.x * PER;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = base + j;
+    c += a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1]);
+  }
+  int tot;
+  int off = block_excl_scan<kLT>(c, &tot);
+  const int64_t u0 = u_start[t];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = base + j;
+    if (a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1])) {
+      uq[off] = a[i];
+      u_rows[u0 + off] = a[i];
+      ++off;
+    }
+  }
+  // rows of the tile ordered by neighbour mask (padding rows last)
+  for (int p = threadIdx.x; p < T; p += kLT) {
+    const int64_t row = t * T + p;
+    uint64_t m = ~0ull >> 8;
+    if (row < n) {
+      m = 0;
+      if (order)
+        for (int o = 0; o < K; ++o) m |= (uint64_t)(nbr[(int64_t)o * n + row] >= 0) << o;
+    }
+    mk[p] = (m << 8) | (uint64_t)p;
+  }
+  __syncthreads();
+  bitonic_u64<T>(mk);
+  for (int i = threadIdx.x; i < T; i += kLT) {
+    const int64_t row = t * T + (int)(mk[i] & 0xFF);
+    perm[t * T + i] = row < n ? (int32_t)row : -1;
+  }
+  // local index of every (offset, ordered row): binary search in the distinct list
+  for (int idx = threadIdx.x; idx < K * T; idx += kLT) {
+    const int o = idx / T, i = idx - o * T;
+    const int64_t row = t * T + (int)(mk[i] & 0xFF);
+    const int32_t v = row < n ? nbr[(int64_t)o * n + row] : -1;
+    uint16_t li = kAbsent;
+    if (v >= 0) {
+      int lo = 0, hi = tot;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (uq[mid] < v) lo = mid + 1;
+        else hi = mid;
+      }
+      li = (uint16_t)lo;
+    }
+    lidx[(int64_t)o * n_pad + t * T + i] = li;
+  }
+}
+
+// ---------------------------------------------------------------- weights
+// wt -> lane-ordered split image: unit ((((o * n_y + cy) * nks + ks) * NT + t) * 3 + p) * 64 + lane holds
+// piece p of W^T[out 16 (cy NT + t) + r][k 32 ks + 8 q .. + 7] for lane = 16 q + r (zero past c_in), so a
+// wave loads its fragments of one step as 3 NT coalesced 1 KiB rows.  wlay 1: wt is [K][c_in][c_out]
+// (the module's layout), else [K][c_out][c_in].
+__global__ __launch_bounds__(256) void split_weights_lane_kernel(const float* __restrict__ wt, int K, int c_out,
+                                                                 int c_in, int NT, u32x4* __restrict__ img,
+                                                                 int wlay) {
+  const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (o, cy, ks, t, lane)
+  if (g >= (int64_t)K * n_y * nks * NT * 64) return;
+  const int lane = (int)(g & 63), r = lane & 15, q = lane >> 4;
+  int64_t rest = g >> 6;
+  const int t = (int)(rest % NT);
+  rest /= NT;
+  const int ks = (int)(rest % nks);
+  rest /= nks;
+  const int cy = (int)(rest % n_y);
+  const int64_t o = rest / n_y;
+  const int oc = 16 * (cy * NT + t) + r, k = 32 * ks + 8 * q;
+  u32x4 pc[3] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+  if (k < c_in) {  // c_in % 16 == 0: an octet is all data or all padding
+    if (wlay) {
+      const float* src = wt + (o * c_in + k) * c_out + oc;
+      split8(floatx4{src[0], src[c_out], src[2 * c_out], src[3 * c_out]},
+             floatx4{src[4 * c_out], src[5 * c_out], src[6 * c_out], src[7 * c_out]}, pc);
+    } else {
+      const floatx4* src = reinterpret_cast<const floatx4*>(wt + (o * c_out + oc) * c_in + k);
+      split8(src[0], src[1], pc);
+    }
+  }
+  u32x4* dst = img + ((g >> 6) * 3) * 64 + lane;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) dst[p * 64] = pc[p];
+}
+
+// ---------------------------------------------------------------- convolution
+// staged row j of the 32-channel slice: 12 units (piece p, k-octet qq) at p * 4 + (qq ^ ((j >> 2) & 3)):
+// the 16 lanes of one ds_read_b128 lane group read 16 rows at their own octet, and the swizzle spreads rows
+// j mod 16 over the 16 bank quads
+__device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + p * 4 + (qq ^ ((j >> 2) & 3)); }
+
+// ABL (timing experiments only, wrong results): bit 1 no weight loads, 2 no LDS input reads, 4 no staging,
+// 8 no MFMAs, 16 no index reads (every group active)
+template <int NT, int T, int D, int WR, int ABL = 0>
+__global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
+    const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
+    const int32_t* __restrict__ perm, int64_t n_pad, int n_y, float* __restrict__ out) {
+  constexpr int NTH = 256 * WR;    // 4 offset classes x WR row parts
+  constexpr int G = T / 16 / WR;   // row groups per wave
+  constexpr int NC = 16 * NT;
+  static_assert(4 * T * NC * 4 <= kXR * kXU * 16, "partial sums must fit the staging area");
+  __shared__ u32x4 xs[kXR * kXU];
+  __shared__ uint16_t ls[kKMax * T];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int oc = wave & 3, rp = wave >> 2;  // offset class, row part (rows 16 G rp ..)
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int cy = (int)(lb % n_y);
+  const int64_t tile = lb / n_y;
+  const int64_t u0 = u_start[tile];
+  const int U = (int)(u_start[tile + 1] - u0);
+  const int Us = U < kUCap ? U : kUCap;
+  const int nks = (c_in + 31) / 32;
+  for (int i = tid; i < K * T; i += NTH) {
+    const int o = i / T, p = i - o * T;
+    ls[i] = lidx[(int64_t)o * n_pad + tile * T + p];
+  }
+  if (tid < kXU) xs[kUCap * kXU + tid] = u32x4{0u, 0u, 0u, 0u};
+
+  // this wave's offsets o = oc + 4 j, j < kNJ (slots past K are empty steps), kNJ per input-channel slice
+  constexpr int kNJ = 8;
+  const int n_steps = nks * kNJ;
+  floatx4 acc[G][NT];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto ld_w = [&](int s, u32x4 (&w)[NT][3]) {
+    const int sc = s < n_steps ? s : n_steps - 1;
+    const int ks = sc / kNJ, j = sc - ks * kNJ;
+    const int o = oc + 4 * j < K ? oc + 4 * j : oc;
+    const int ow = flip ? K - 1 - o : o;
+    const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * 3 * 64 + lane;
+    if (ABL & 1) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) w[t][p] = u32x4{(uint32_t)(s + t), (uint32_t)p, 0u, 1u};
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[t][p] = src[(t * 3 + p) * 64];
+  };
+  constexpr int SB = WR == 1 ? 3 : 2;  // staging loads in flight per thread
+  auto stage = [&](int ks) {
+    if (ABL & 4) return;
+    const int k0 = 32 * ks;
+    const int items = Us * 4;
+    for (int i0 = tid; i0 < items; i0 += NTH * SB) {
+      int32_t rows[SB];
+      floatx4 v[SB][2];
+#pragma unroll
+      for (int b = 0; b < SB; ++b) {
+        const int i = i0 + NTH * b;
+        rows[b] = i < items ? u_rows[u0 + (i >> 2)] : 0;
+      }
+#pragma unroll
+      for (int b = 0; b < SB; ++b) {
+        const int i = i0 + NTH * b;
+        const int k = k0 + 8 * (i & 3);
+        v[b][0] = v[b][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (i < items && k < c_in) {
+          const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)rows[b] * c_in + k);
+          v[b][0] = src[0];
+          v[b][1] = src[1];
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < SB; ++b) {
+        const int i = i0 + NTH * b;
+        if (i < items) {
+          u32x4 pc[3];
+          split8(v[b][0], v[b][1], pc);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) xs[xs_unit(i >> 2, p, i & 3)] = pc[p];
+        }
+      }
+    }
+  };
+  // one (k-slice, offset) step of this wave over the tile's row groups: the 16 local indices of every group
+  // first (one LDS wait), the wave-uniform masks of groups with the offset and with rows past the staged
+  // capacity, then the groups in order with the next group's three pieces read from LDS before the current
+  // group's MFMAs (absent rows read the zero row; inactive groups are read and skipped)
+  auto xload = [&](int li, u32x4 (&xp)[3]) {
+    const int jr = li < kUCap ? li : kUCap;  // absent (0xFFFF) and far rows -> zero row
+    if (ABL & 2) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) xp[p] = u32x4{(uint32_t)jr, (uint32_t)p, 7u, 9u};
+      return;
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) xp[p] = xs[xs_unit(jr, p, q)];
+  };
+  auto run = [&](int s, const u32x4 (&w)[NT][3]) {
+    const int ks = s / kNJ, j = s - ks * kNJ;
+    const int o = oc + 4 * j;
+    if (o >= K) return;  // empty slot (wave-uniform)
+    const uint16_t* lo = ls + o * T + 16 * G * rp + r;
+    int li[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) li[g] = (ABL & 16) ? (r + 7 * g + o) : lo[16 * g];
+    uint32_t act = 0, far = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const bool pres = li[g] != kAbsent;
+      act |= (ballot64(pres) != 0 ? 1u : 0u) << g;
+      far |= (ballot64(pres && li[g] >= kUCap) != 0 ? 1u : 0u) << g;
+    }
+    u32x4 xa[3], xb[3];
+    xload(li[0], xa);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      u32x4(&cur)[3] = (g & 1) ? xb : xa;
+      u32x4(&nxt)[3] = (g & 1) ? xa : xb;
+      if (g + 1 < G) xload(li[g + 1], nxt);
+      if ((act >> g) & 1) {  // wave-uniform
+        if ((far >> g) & 1) {  // rows past the staged capacity: straight from global memory (rare)
+          const bool f = li[g] != kAbsent && li[g] >= kUCap;
+          const int k = 32 * ks + 8 * q;
+          floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+          if (f && k < c_in) {
+            const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)u_rows[u0 + li[g]] * c_in + k);
+            a = src[0];
+            b = src[1];
+          }
+          u32x4 fp[3];
+          split8(a, b, fp);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) cur[p] = f ? fp[p] : cur[p];
+        }
+        floatx4 c[NT];
+        if (ABL & 8) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[g][t] += __builtin_bit_cast(floatx4, cur[0] ^ cur[1] ^ cur[2] ^ w[t][0] ^ w[t][1] ^ w[t][2]);
+          continue;
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][2], cur[0], floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[1], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[2], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[0], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[1], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[0], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] += c[t];
+      }
+    }
+  };
+
+  static_assert(kNJ % D == 0, "steps per slice must be a multiple of the weight register sets");
+  u32x4 wf[D][NT][3];
+#pragma unroll
+  for (int d = 0; d < D; ++d) ld_w(d, wf[d]);
+  for (int ks = 0; ks < nks; ++ks) {
+    __syncthreads();  // previous slice's readers done (and the index tile / zero row written)
+    stage(ks);
+    __syncthreads();
+    for (int j = 0; j < kNJ; j += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int st = ks * kNJ + j + d;
+        run(st, wf[d]);
+        ld_w(st + D, wf[d]);
+      }
+    }
+  }
+  // the four offset classes' partial sums, added in class order
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs);
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      *reinterpret_cast<floatx4*>(red + ((int64_t)(oc * T + 16 * (G * rp + g) + r)) * NC + 16 * t + 4 * q) =
+          acc[g][t];
+  __syncthreads();
+  constexpr int QPR = NC / 4;  // float4 quads per row
+  for (int i = tid; i < T * QPR; i += NTH) {
+    const int row = i / QPR, cq = i - row * QPR;
+    const float* pr = red + row * NC + 4 * cq;
+    floatx4 v = *reinterpret_cast<const floatx4*>(pr);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const floatx4*>(pr + w * T * NC);
+    const int32_t dst = perm[tile * T + row];
+    if (dst >= 0) *reinterpret_cast<floatx4*>(out + (int64_t)dst * c_out + cy * NC + 4 * cq) = v;
+  }
+}
+
+inline int local_nt(int c_out) { return (c_out / 16) % 2 == 0 ? 2 : 1; }
+
+static int g_local_wr = 2;     // row parts per block (waves = 4 x wr); msp_debug_conv_local (experiments)
+static int g_local_order = 1;  // msp_tile_local: order rows inside a tile by neighbour mask
+static int g_local_nt = 0;     // forced column tiles per wave (0: local_nt)
+static int g_local_abl = 0;    // ablation variant (timing only; msp_debug_conv_local_abl)
+
+}  // namespace msp
+
+using namespace msp;
+
+extern "C" {
+
+size_t msp_tile_local_workspace_size(int64_t n, int tile_rows) {
+  const int64_t n_tiles = ceil_div(n > 0 ? n : 1, tile_rows > 0 ? tile_rows : 1);
+  return (size_t)(n_tiles + 1) * sizeof(int64_t) + scan_ws_bytes(n_tiles);
+}
+
+int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t* u_start, int32_t* u_rows,
+                   int64_t u_cap, uint16_t* lidx, int32_t* perm, void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && K <= 32 && n >= 0, "msp_tile_local: K must be in [1, 32] (got %d)", K);
+  MSP_REQUIRE(tile_rows == 64 || tile_rows == 128 || tile_rows == 256,
+              "msp_tile_local: tile_rows must be 64, 128 or 256 (got %d)", tile_rows);
+  MSP_REQUIRE(n < (1ll << 31), "msp_tile_local: too many rows");
+  hipStream_t s = as_stream(stream);
+  const int64_t n_tiles = ceil_div(n, tile_rows);
+  const size_t need = msp_tile_local_workspace_size(n, tile_rows);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_tile_local: workspace too small (%zu < %zu)", ws_bytes, need);
+  if (n_tiles == 0) {
+    MSP_HIP(hipMemsetAsync(u_start, 0, 2 * sizeof(int64_t), s), "msp_tile_local");
+    return MSP_OK;
+  }
+  const int64_t n_pad = n_tiles * tile_rows;
+  int64_t* cnt = reinterpret_cast<int64_t*>(ws);
+  void* sws = cnt + n_tiles + 1;
+  const unsigned grid = (unsigned)n_tiles;
+  if (u_cap <= 0) {  // counting call: u_start[0..n_tiles] = exclusive scan, u_start[n_tiles + 1] = largest tile
+    MSP_HIP(hipMemsetAsync(u_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_tile_local");
+    auto* mx = reinterpret_cast<unsigned long long*>(u_start + n_tiles + 1);
+    if (tile_rows == 64) local_count_kernel<64, 2048><<<grid, kLT, 0, s>>>(nbr, K, n, cnt, mx);
+    else if (tile_rows == 128) local_count_kernel<128, 4096><<<grid, kLT, 0, s>>>(nbr, K, n, cnt, mx);
+    else local_count_kernel<256, 8192><<<grid, kLT, 0, s>>>(nbr, K, n, cnt, mx);
+    const int rc = scan_exclusive_i64(cnt, u_start, n_tiles, u_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
+    if (rc) return rc;
+  } else {
+    MSP_REQUIRE(u_rows && lidx && perm, "msp_tile_local: NULL output");
+    if (tile_rows == 64)
+      local_fill_kernel<64, 2048><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm, g_local_order);
+    else if (tile_rows == 128)
+      local_fill_kernel<128, 4096><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm, g_local_order);
+    else
+      local_fill_kernel<256, 8192><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm, g_local_order);
+  }
+  return check_launch("msp_tile_local");
+}
+
+// Experiment hook (not part of the public ABI; scripts/kbench_local.py): wr = row parts per block (1 or 2),
+// order = 1 to order rows inside a tile by neighbour mask (0: key order), nt = forced column tiles per wave
+// (0: automatic); negative = keep.
+int msp_debug_conv_local(int wr, int order, int nt) {
+  if (wr == 1 || wr == 2) g_local_wr = wr;
+  if (nt >= 0) g_local_nt = nt;
+  if (order >= 0) g_local_order = order ? 1 : 0;
+  return MSP_OK;
+}
+
+int msp_debug_conv_local_abl(int abl) {
+  g_local_abl = abl;
+  return MSP_OK;
+}
+
+// Measured against the gather forms on the headline batch's rulebooks (scripts/kbench_local.py,
+// profiles/r02/kbench_local_r02_levels.log): ahead from 64 channels on both sides and 4096 rows up (levels
+// 1-4 of m = 32: 0-34 % less time), behind on the 32-channel level 0 (the per-wave tile form x6r and the
+// dense row groups) and on the few-tile levels 5-6 (grids of 16 / 4 tiles).
+int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {
+  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 64 && c_out >= 64 && n_rows >= 4096) ? 1 : 0;
+}
+
+size_t msp_conv_local_workspace_size(int K, int c_in, int c_out) {
+  return (size_t)K * c_out * ((c_in + 31) / 32) * 32 * 6;
+}
+
+int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                   const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
+                   int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
+              "msp_conv_local: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
+  MSP_REQUIRE(K >= 1 && K <= kKMax, "msp_conv_local: K must be in [1, %d] (got %d)", kKMax, K);
+  MSP_REQUIRE(tile_rows == 128, "msp_conv_local: tile_rows must be 128 (got %d)", tile_rows);
+  MSP_REQUIRE(flip >= 0 && flip <= 3, "msp_conv_local: flip must be 0..3 (got %d)", flip);
+  const size_t need = msp_conv_local_workspace_size(K, c_in, c_out);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_local: workspace too small (%zu < %zu)", ws_bytes, need);
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
+  if (n_tiles == 0) return MSP_OK;
+  hipStream_t s = as_stream(stream);
+  const int NT = (g_local_nt == 1 || (g_local_nt == 2 && c_out % 32 == 0)) ? g_local_nt : local_nt(c_out);
+  const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
+  u32x4* img = static_cast<u32x4*>(ws);
+  const int64_t lanes = (int64_t)K * n_y * nks * NT * 64;
+  split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                             (flip >> 1) & 1);
+  const int64_t n_pad = n_tiles * tile_rows;
+  const unsigned grid = (unsigned)(n_tiles * n_y);
+  const int wr = g_local_wr;
+#define LX(N, W, A)                                                                                           \
+  if (NT == N && wr == W && g_local_abl == A)                                                                 \
+    conv_x6s_kernel<N, 128, 2, W, A><<<grid, 256 * W, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, \
+                                                              u_rows, perm, n_pad, n_y, out);
+  LX(2, 1, 0) LX(1, 1, 0) LX(2, 2, 0) LX(1, 2, 0)
+  LX(2, 2, 1) LX(2, 2, 2) LX(2, 2, 4) LX(2, 2, 8) LX(2, 2, 16) LX(2, 2, 15) LX(2, 2, 31)
+#undef LX
+  return check_launch("msp_conv_local");
+}
+
+}  // extern "C"

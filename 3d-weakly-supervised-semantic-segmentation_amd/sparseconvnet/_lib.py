@@ -34,6 +34,11 @@ PROTOTYPES = {
     "msp_pair_lists": (I, [P, I, I64, P, P, I64, P, P, SZ, P]),
     "msp_tile_rulebook": (I, [P, I, I64, I, P, P, P, P, I64, P, SZ, P]),
     "msp_decode_keys": (I, [P, I64, I, P, P]),
+    "msp_tile_local_workspace_size": (SZ, [I64, I]),
+    "msp_tile_local": (I, [P, I, I64, I, P, P, I64, P, P, P, SZ, P]),
+    "msp_conv_local_preferred": (I, [I64, I, I]),
+    "msp_conv_local_workspace_size": (SZ, [I, I, I]),
+    "msp_conv_local": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_tile_rows": (I, [I64, I, I]),
     "msp_conv_tile_form": (I, [I64, I, I, I]),
     "msp_conv_tile_workspace_size": (SZ, [I64, I, I, I, I]),

@@ -58,6 +58,27 @@ def tile_rulebook(m, K, n, device, s, tile_rows=64):
                 n_chunks=n_chunks, tile_rows=tr, max_chunks=max_chunks)
 
 
+LOCAL_TILE_ROWS = 128
+
+
+def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS):
+    """msp_tile_local: count (one host read of the total), then fill."""
+    T = int(tile_rows)
+    n_tiles = (n + T - 1) // T
+    u_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=device)
+    ws = _ws(query("msp_tile_local_workspace_size", I64(n), T), device)
+    call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), None, 0, None, None, ptr(ws), ws.numel(), s)
+    total, max_u = (int(v) for v in u_start[n_tiles:].tolist()) if n_tiles else (0, 0)
+    u_rows = torch.empty(max(total, 1), dtype=torch.int32, device=device)
+    lidx = torch.empty((K, max(n_tiles * T, 1)), dtype=torch.int16, device=device)  # uint16 bits
+    perm = torch.empty(max(n_tiles * T, 1), dtype=torch.int32, device=device)
+    if n_tiles:
+        call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), ptr(u_rows), max(total, 1), ptr(lidx), ptr(perm),
+             ptr(ws), ws.numel(), s)
+    return dict(u_start=u_start, u_rows=u_rows, lidx=lidx, perm=perm, tile_rows=T, n_tiles=n_tiles, total=total,
+                max_u=max_u)
+
+
 class PairLists:
     """Per-offset (in, out) pair lists of an offset-major map, plus the chunk
     and block partitions used by msp_conv_pairs / msp_conv_wgrad."""
@@ -101,6 +122,7 @@ class SubmRules:
             call("msp_subm_map", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(table), cap,
                  ptr(self.nbr), s)
         self._tiles = {}
+        self._locals = {}
         self._dense = None
         self._map, self._n = self.nbr, V
         self.pairs = PairLists(self.nbr, K, V, dev, s)
@@ -125,6 +147,16 @@ class SubmRules:
                      s)
                 self._dense = (perm, nbr_p)
         return self._dense
+
+    def local(self, tile_rows=LOCAL_TILE_ROWS):
+        """Tile-local rulebook (msp_tile_local) for msp_conv_local, built on first use: per tile the sorted
+        distinct input rows, the rows' order inside the tile and the local index of every neighbour."""
+        t = self._locals.get(tile_rows)
+        if t is None:
+            self._plan.append(("local", self._key, tile_rows))
+            t = self._locals[tile_rows] = local_rulebook(self.nbr, self.K, self._n, self.nbr.device,
+                                                         _lib.stream(self.nbr.device), tile_rows)
+        return t
 
     def tiles_for(self, tile_rows):
         """Tile rulebook with tile_rows-row tiles, built on first use."""
@@ -333,6 +365,8 @@ class Metadata:
                 self._rules(entry[1]).tiles_for(entry[2])
             elif entry[0] == "dense":
                 self._rules(entry[1]).dense_order()
+            elif entry[0] == "local":
+                self._rules(entry[1]).local(entry[2])
 
     def tensors(self):
         """Every device tensor this metadata holds (for stream bookkeeping)."""

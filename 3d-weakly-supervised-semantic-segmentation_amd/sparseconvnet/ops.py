@@ -60,6 +60,9 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     counts (msp_conv_tile_rows)."""
     c_in = x.size(1)
     nbr = getattr(rules, "nbr", None)  # submanifold rules carry the neighbour map
+    if nbr is not None and n_rows and K <= 27 and CONV_LOCAL and \
+            int(_lib.query("msp_conv_local_preferred", _lib.I64(n_rows), c_in, c_out)):
+        return conv_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
     if nbr is not None and n_rows and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(n_rows), c_in, c_out)):
         perm, nbr_p = rules.dense_order()
         return conv_nbr(x, wt, K, flip, c_out, nbr_p, n_rows, kind, flops, perm)
@@ -81,6 +84,28 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
             "msp_conv_tile", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tr, ptr(tiles["tile_start"]),
             ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), n_rows, ptr(out),
             ptr(ws), wsb, _stream(x)), nbytes)
+    return out[:n_rows]
+
+
+# tile-local submanifold convolution (msp_conv_local) where the library prefers it; False: the gather forms
+CONV_LOCAL = True
+
+
+def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0):
+    """Submanifold convolution over the tile-local rulebook (SubmRules.local): each 128-row tile's distinct
+    input rows staged in LDS and split once (msp_conv_local)."""
+    c_in = x.size(1)
+    loc = rules.local()
+    out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
+    wsb = int(_lib.query("msp_conv_local_workspace_size", K, c_in, c_out))
+    ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
+    # compulsory bytes: input rows, output rows, weights, the tile-local rulebook
+    nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
+        4 * loc["total"] + 2 * K * loc["n_tiles"] * loc["tile_rows"] + 4 * loc["n_tiles"] * loc["tile_rows"]
+    _record(kind + "/x6s", flops, lambda: call(
+        "msp_conv_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
+        ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), n_rows, ptr(out), ptr(ws), wsb, _stream(x)),
+        nbytes)
     return out[:n_rows]
 
 

@@ -121,6 +121,20 @@ int msp_pair_lists(const int32_t* map, int K, int64_t n, int32_t* pair_in, int32
 int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64_t* tile_start,
                       uint8_t* chunk_off, int32_t* chunk_src, uint16_t* chunk_row, int64_t chunk_cap, void* ws,
                       size_t ws_bytes, msp_stream_t stream);
+/* Tile-local rulebook of a submanifold neighbour map (msp_conv_local):
+ * rows are cut into tiles of tile_rows (64, 128 or 256); per tile t the
+ * distinct input rows its neighbour entries name are listed in ascending order
+ * at u_rows[u_start[t] .. u_start[t+1]); perm[t*T + i] is the tile's i-th row
+ * (rows ordered inside the tile by their neighbour mask, so 16-row groups share
+ * offsets; -1 past n) and lidx[o][t*T + i] (uint16, [K][n_tiles*T]) the
+ * position in the tile's list of that row's neighbour at offset o (0xFFFF:
+ * none).  K <= 32.  Count-then-fill like msp_pair_lists: the counting call
+ * (u_cap = 0) writes u_start[0..n_tiles] (u_start[n_tiles] = total) and
+ * u_start[n_tiles+1] = the largest tile's count; the filling call (u_cap >=
+ * total) reuses u_start.  Workspace: msp_tile_local_workspace_size. */
+size_t msp_tile_local_workspace_size(int64_t n, int tile_rows);
+int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t* u_start, int32_t* u_rows,
+                   int64_t u_cap, uint16_t* lidx, int32_t* perm, void* ws, size_t ws_bytes, msp_stream_t stream);
 /* Decode keys back to (x, y, z, batch) int64 rows (SparseToDense, locations). */
 int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coords, msp_stream_t stream);
 
@@ -150,6 +164,20 @@ int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out);
  * split over offsets on small grids), 3 = f32-MFMA tile forms (tile_rows 64 /
  * 256), 0 = nothing to do. */
 int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows);
+
+/* Tile-local submanifold convolution (replaces the gather forms where
+ * msp_conv_local_preferred says so): out[perm row] = sum_o W'[o]^T x[nbr(row, o)]
+ * over a msp_tile_local rulebook with tile_rows = 128 (K <= 27).  Each tile's
+ * distinct input rows are staged in LDS once per 32 input channels and split
+ * into exact bf16 pieces once; the rules read them from LDS.  flip and the
+ * weight layouts as msp_conv_tile (bit 0: offset K-1-o, bit 1: wt is
+ * [K][c_in][c_out], else [K][c_out][c_in]).  Workspace:
+ * msp_conv_local_workspace_size (the split weight image). */
+int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out);
+size_t msp_conv_local_workspace_size(int K, int c_in, int c_out);
+int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                   const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
+                   int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows);
 int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,

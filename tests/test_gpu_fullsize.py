@@ -1,8 +1,9 @@
 """Full-size parity of the benchmarked networks (BASELINE.json configs[1] and configs[2] shapes at 2 cm,
 whole synthetic scenes): the HIP path against the fp64 CPU oracle with shared ReLU decisions
 (oracle/parity.py), at the sizes where the production kernel selections take over -- the dense row-group
-convolution (msp_conv_nbr, >= 1e5 rows and c_out >= 64), the NetworkInNetwork kernel (msp_nin_gemm,
->= 2^18 rows) and the per-wave split-bf16 tile at level 0 (conv_x6r).  The test records which forms ran
+convolution (msp_conv_nbr, >= 1e5 rows and c_out >= 64: level 0's 32 -> 64 backward-data), the tile-local
+convolution (msp_conv_local, 64+ channels from 4096 rows: levels 1-4), the NetworkInNetwork kernel
+(msp_nin_gemm, >= 2^18 rows) and the per-wave split-bf16 tile at level 0 (conv_x6r).  The test records which forms ran
 (through the same hook bench.py times them with) and requires each to have fired.
 
 Bars (tests/test_gpu_encoders.py explains them): per-point and scene features within 1e-4 of
@@ -89,9 +90,10 @@ def test_headline_unet_full_size_parity():
     """configs[2] network (SparseConvUNet m=32, block_reps=2, residual) on two whole scenes at 2 cm:
     level 0 >= 2^18 voxels (NIN kernel), level 1 >= 1e5 (dense row groups)."""
     kinds = _run("SparseConvUNet", 32, 2, True, 2,
-                 need=["subm_fwd/x6r", "subm_fwd/x6g", "subm_bwd_data/x6g", "subm_fwd/x6d", "nin_fwd/hip",
-                       "nin_bwd_data/hip", "wgrad/x6", "nin_wgrad/x6", "conv_fwd/x6d", "deconv_fwd/f32"])
-    assert kinds["subm_fwd/x6g"] >= 4
+                 need=["subm_fwd/x6r", "subm_fwd/x6s", "subm_bwd_data/x6s", "subm_bwd_data/x6g", "subm_fwd/x6d",
+                       "nin_fwd/hip", "nin_bwd_data/hip", "wgrad/x6", "nin_wgrad/x6", "conv_fwd/x6d",
+                       "deconv_fwd/f32"])
+    assert kinds["subm_fwd/x6s"] >= 4
 
 
 def test_c2_unet_full_size_parity():

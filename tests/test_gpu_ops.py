@@ -595,3 +595,115 @@ def test_nin_layer_grad():
     close(y.features, xd @ wd, 1e-5, "nin fwd")
     close(x.grad, gy.double() @ wd.t(), 1e-5, "nin dx")
     close(nin.weight.grad, xd.t() @ gy.double(), 1e-5, "nin dW")
+
+
+def _local_ref(x, wt, nbr, flip):
+    V = nbr.size(1)
+    x64 = torch.cat([x.double(), torch.zeros(1, x.size(1), dtype=torch.float64, device=DEV)])
+    w64 = wt.double().flip(0) if flip else wt.double()
+    nb = nbr.long()
+    ref = torch.zeros(V, wt.size(1), dtype=torch.float64, device=DEV)
+    for o in range(nbr.size(0)):
+        ref += x64[torch.where(nb[o] >= 0, nb[o], x.size(0))] @ w64[o].t()
+    return ref
+
+
+def _check_local_rulebook(nbr, loc, n):
+    K = nbr.size(0)
+    T, nt = loc["tile_rows"], loc["n_tiles"]
+    us = loc["u_start"][:nt + 1].cpu()
+    u_rows = loc["u_rows"].cpu()
+    perm = loc["perm"][:nt * T].view(nt, T).cpu()
+    lidx = loc["lidx"][:, :nt * T].cpu().to(torch.int64) & 0xFFFF  # uint16 bits in an int16 tensor
+    nb = nbr.cpu()
+    assert loc["total"] == int(us[-1]) and loc["max_u"] == int((us[1:] - us[:-1]).max())
+    for t in range(nt):
+        rows = perm[t]
+        valid = rows >= 0
+        assert int(valid.sum()) == min(T, n - t * T)
+        assert bool((~valid[int(valid.sum()):]).all())  # padding last
+        assert sorted(rows[valid].tolist()) == list(range(t * T, t * T + int(valid.sum())))
+        u = u_rows[int(us[t]):int(us[t + 1])]
+        assert bool((u[1:] > u[:-1]).all())
+        ent = nb[:, rows[valid].long()]
+        assert sorted(set(ent[ent >= 0].tolist())) == u.tolist()
+        li = lidx[:, t * T:(t + 1) * T][:, :int(valid.sum())]
+        absent = ent < 0
+        assert bool((li[absent] == 0xFFFF).all())
+        assert torch.equal(u[li[~absent]], ent[~absent])
+
+
+@pytest.mark.parametrize("order", [1, 0])
+def test_tile_local_rulebook(order):
+    """msp_tile_local: per 128-row tile the sorted distinct input rows, the rows' order inside the tile
+    (by neighbour mask, or key order) and the local index of every neighbour, checked entry by entry."""
+    import ctypes
+    from sparseconvnet import _lib, metadata
+    lib = _lib.load()
+    lib.msp_debug_conv_local.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    lvl = t.metadata.level(64)
+    rules = lvl.subm_rules(3)
+    try:
+        lib.msp_debug_conv_local(-1, order, -1)
+        loc = metadata.local_rulebook(rules.nbr, 27, lvl.n, rules.nbr.device, _lib.stream(), 128)
+    finally:
+        lib.msp_debug_conv_local(-1, 1, -1)
+    assert lvl.n % 128 != 0
+    _check_local_rulebook(rules.nbr, loc, lvl.n)
+
+
+@pytest.mark.parametrize("cin,cout,flip", [(64, 64, 2), (64, 64, 1), (96, 96, 2), (192, 96, 1), (48, 64, 2),
+                                           (64, 48, 1), (128, 16, 2), (32, 160, 1)])
+def test_conv_local_accuracy(cin, cout, flip):
+    """msp_conv_local (tile-local staging, split-bf16 MFMA) against an fp64 evaluation: below 1e-6 of the
+    output scale (the x6 forms' bar), and against the production gather form.  flip 2 = forward with the
+    module's [K][c_in][c_out] weights, 1 = backward-data ([K][c_out][c_in], offsets mirrored); c_in 48 has a
+    half-empty 32-channel slice, c_out 48 / 16 / 160 run one 16-column tile per wave."""
+    from sparseconvnet import ops
+    torch.manual_seed(cin * 7 + cout + flip)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    lvl = t.metadata.level(64)
+    rules = lvl.subm_rules(3)
+    V = lvl.n
+    x = torch.randn(V, cin, device=DEV)
+    w = torch.randn(27, cin, cout, device=DEV) / (27 * cin) ** 0.5
+    wt = w if flip == 2 else w.transpose(1, 2).contiguous()
+    y = ops.conv_local(x, wt, 27, flip, cout, rules, V)
+    ref = _local_ref(x, w.transpose(1, 2), rules.nbr, flip & 1)  # [K][c_out][c_in], offsets mirrored for flip 1
+    scale = ref.abs().max().item()
+    err = (y.double() - ref).abs().max().item() / scale
+    assert err < 1e-6, err
+    ops.CONV_LOCAL = False
+    try:
+        yg = ops.conv_tile(x, wt, 27, flip, cout, rules, V)
+    finally:
+        ops.CONV_LOCAL = True
+    assert (y - yg).abs().max().item() / scale < 2e-6
+
+
+def test_conv_local_overflow_rows():
+    """Tiles naming more distinct input rows than the LDS stage holds (383): a random neighbour map over a
+    large input (about 1700 distinct rows per tile) sends most rows down the global-memory path; results
+    still match fp64, and the metadata is exact."""
+    from sparseconvnet import _lib, metadata, ops
+
+    class R:  # a SubmRules stand-in over an arbitrary map
+        pass
+    torch.manual_seed(5)
+    V, n_in, K = 1000, 50000, 27
+    nbr = torch.randint(0, n_in, (K, V), dtype=torch.int32, device=DEV)
+    nbr[torch.rand(K, V, device=DEV) < 0.5] = -1
+    r = R()
+    r.nbr, r.K = nbr, K
+    loc = metadata.local_rulebook(nbr, K, V, nbr.device, _lib.stream(), 128)
+    assert loc["max_u"] > 1000
+    _check_local_rulebook(nbr, loc, V)
+    r.local = lambda tile_rows=128: loc
+    x = torch.randn(n_in, 64, device=DEV)
+    w = torch.randn(K, 64, 32, device=DEV) / (K * 64) ** 0.5
+    y = ops.conv_local(x, w, K, 2, 32, r, V)
+    ref = _local_ref(x, w.transpose(1, 2), nbr, 0)
+    assert (y.double() - ref).abs().max().item() / ref.abs().max().item() < 1e-6
