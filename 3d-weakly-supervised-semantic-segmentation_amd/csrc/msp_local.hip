@@ -441,12 +441,267 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
   }
 }
 
+// ---------------------------------------------------------------- persistent pipelined form
+// conv_x6l: one block of 8 waves per CU (all of its LDS), looping over a contiguous range of work items
+// (tile, output column slice); a work item is nks units (32-input-channel slices).  The staging area is
+// double buffered: while the waves compute unit u from buffer u & 1, every thread has the next unit's row
+// indices, input values and index tile in flight in registers (issued at the start / after the second
+// step of unit u) and writes them, split into bf16 pieces, into the other buffer at its end -- the
+// staging latency and the per-tile start-up leave the critical path.  Waves = 4 offset classes x 2 column
+// halves of the block's 32 NT columns: each wave keeps all 8 row groups of its 16 NT columns in registers
+// and loads only its own weight fragments (two steps ahead, across units).  At the end of a work item the
+// four offset classes' partial sums meet in LDS in class order (deterministic) and the rows are written
+// through the tile's row order.
+template <int NT>
+__global__ __launch_bounds__(512, 2) void conv_x6l_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
+    const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
+    const int32_t* __restrict__ perm, int64_t n_pad, int n_y, int64_t n_items, float* __restrict__ out) {
+  constexpr int T = 128, G = 8, NTH = 512, NCW = 16 * NT, NCB = 2 * NCW;
+  constexpr int kNJ = 8;                 // offset slots per wave and unit (o = oc + 4 j; slots past K empty)
+  constexpr int SI = (kUCap * 4 + NTH - 1) / NTH;  // staging items (row, k-octet) per thread
+  constexpr int LW = (kKMax * T / 2 + NTH - 1) / NTH;  // index-tile words (2 x uint16) per thread
+  static_assert(T * NCB * 4 <= kXR * kXU * 16, "the item's sums must fit one staging buffer");
+  __shared__ u32x4 xs[2][kXR * kXU];
+  __shared__ uint32_t ls[2][kKMax * T / 2];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int oc = wave & 3, ch = wave >> 2;  // offset class, column half
+  const int r = lane & 15, q = lane >> 4;
+  const int nks = (c_in + 31) / 32;
+  // contiguous work items per block (neighbouring tiles share input rows: keep them on one XCD's L2)
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int64_t it0 = lb * n_items / gridDim.x, it1 = (lb + 1) * n_items / gridDim.x;
+  const int64_t n_units = (it1 - it0) * nks;
+  if (n_units == 0) return;
+  auto unit_of = [&](int64_t u, int64_t& tile, int& cy, int& ks) {
+    const int64_t it = it0 + u / nks;
+    ks = (int)(u % nks);
+    cy = (int)(it % n_y);
+    tile = it / n_y;
+  };
+
+  // ---- staging of a unit: row indices -> values -> split into LDS
+  int32_t srow[SI];
+  floatx4 sv[SI][2];
+  uint32_t slw[LW];
+  int s_us = 0;
+  int64_t s_u0 = 0;
+  auto stage_issue_rows = [&](int64_t u) {  // row indices and the index tile of unit u
+    int64_t tile;
+    int cy, ks;
+    unit_of(u, tile, cy, ks);
+    s_u0 = u_start[tile];
+    const int U = (int)(u_start[tile + 1] - s_u0);
+    s_us = U < kUCap ? U : kUCap;
+#pragma unroll
+    for (int b = 0; b < SI; ++b) {
+      const int i = tid + NTH * b;
+      srow[b] = i < s_us * 4 ? u_rows[s_u0 + (i >> 2)] : 0;
+    }
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lidx);
+#pragma unroll
+    for (int b = 0; b < LW; ++b) {
+      const int i = tid + NTH * b;  // word i = entries 2i, 2i + 1 of the [K][T] tile
+      if (i < K * T / 2) {
+        const int e = 2 * i, o = e / T, pp = e - o * T;
+        slw[b] = lw[((int64_t)o * n_pad + tile * T + pp) >> 1];
+      }
+    }
+  };
+  auto stage_issue_values = [&](int64_t u) {
+    int64_t tile;
+    int cy, ks;
+    unit_of(u, tile, cy, ks);
+#pragma unroll
+    for (int b = 0; b < SI; ++b) {
+      const int i = tid + NTH * b;
+      const int k = 32 * ks + 8 * (i & 3);
+      sv[b][0] = sv[b][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (i < s_us * 4 && k < c_in) {
+        const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + k);
+        sv[b][0] = src[0];
+        sv[b][1] = src[1];
+      }
+    }
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int b = 0; b < SI; ++b) {
+      const int i = tid + NTH * b;
+      if (i < s_us * 4) {
+        u32x4 pc[3];
+        split8(sv[b][0], sv[b][1], pc);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) xs[buf][xs_unit(i >> 2, p, i & 3)] = pc[p];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < LW; ++b) {
+      const int i = tid + NTH * b;
+      if (i < K * T / 2) ls[buf][i] = slw[b];
+    }
+  };
+
+  // ---- weights: step (u, j) -> fragments of offset oc + 4 j, slice ks, columns of this wave
+  auto ld_w = [&](int64_t u, int j, u32x4 (&w)[NT][3]) {
+    if (u >= n_units) u = n_units - 1;
+    int64_t tile;
+    int cy, ks;
+    unit_of(u, tile, cy, ks);
+    const int o = oc + 4 * j < K ? oc + 4 * j : oc;
+    const int ow = flip ? K - 1 - o : o;
+    const int cw = 2 * cy + ch;  // this wave's 16 NT-column slice
+    const u32x4* src = wimg + ((((int64_t)ow * (2 * n_y) + cw) * nks + ks) * NT) * 3 * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[t][p] = src[(t * 3 + p) * 64];
+  };
+
+  floatx4 acc[G][NT];
+  int64_t cur_u0 = 0;  // u_start of the unit being computed (rows past the staged capacity)
+  auto xload = [&](int buf, int li, u32x4 (&xp)[3]) {
+    const int jr = li < kUCap ? li : kUCap;  // absent (0xFFFF) and far rows -> zero row
+#pragma unroll
+    for (int p = 0; p < 3; ++p) xp[p] = xs[buf][xs_unit(jr, p, q)];
+  };
+  auto run = [&](int buf, int ks, int j, const u32x4 (&w)[NT][3]) {
+    const int o = oc + 4 * j;
+    if (o >= K) return;  // empty slot (wave-uniform)
+    const uint16_t* lo = reinterpret_cast<const uint16_t*>(ls[buf]) + o * T + r;
+    int li[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) li[g] = lo[16 * g];
+    uint32_t act = 0, far = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const bool pres = li[g] != kAbsent;
+      act |= (ballot64(pres) != 0 ? 1u : 0u) << g;
+      far |= (ballot64(pres && li[g] >= kUCap) != 0 ? 1u : 0u) << g;
+    }
+    u32x4 xa[3], xb[3];
+    xload(buf, li[0], xa);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      u32x4(&cur)[3] = (g & 1) ? xb : xa;
+      u32x4(&nxt)[3] = (g & 1) ? xa : xb;
+      if (g + 1 < G) xload(buf, li[g + 1], nxt);
+      if ((act >> g) & 1) {  // wave-uniform
+        if ((far >> g) & 1) {  // rows past the staged capacity: straight from global memory (rare)
+          const bool f = li[g] != kAbsent && li[g] >= kUCap;
+          const int k = 32 * ks + 8 * q;
+          floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+          if (f && k < c_in) {
+            const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)u_rows[cur_u0 + li[g]] * c_in + k);
+            a = src[0];
+            b = src[1];
+          }
+          u32x4 fp[3];
+          split8(a, b, fp);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) cur[p] = f ? fp[p] : cur[p];
+        }
+        floatx4 c[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][2], cur[0], floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[1], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[2], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[0], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[1], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[0], c[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] += c[t];
+      }
+    }
+  };
+
+  // ---- prologue: unit 0 staged synchronously, zero rows of both buffers
+  stage_issue_rows(0);
+  stage_issue_values(0);
+  stage_store(0);
+  if (tid < 2 * kXU) xs[tid / kXU][kUCap * kXU + tid % kXU] = u32x4{0u, 0u, 0u, 0u};
+  u32x4 wf[2][NT][3];
+  ld_w(0, 0, wf[0]);
+  ld_w(0, 1, wf[1]);
+  __syncthreads();
+
+  for (int64_t u = 0; u < n_units; ++u) {
+    const int buf = (int)(u & 1);
+    int64_t tile;
+    int cy, ks;
+    unit_of(u, tile, cy, ks);
+    cur_u0 = u_start[tile];
+    const bool more = u + 1 < n_units;
+    if (more) stage_issue_rows(u + 1);
+    if (ks == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < kNJ; j += 2) {
+      run(buf, ks, j, wf[0]);
+      ld_w(j + 2 < kNJ ? u : u + 1, (j + 2) % kNJ, wf[0]);
+      run(buf, ks, j + 1, wf[1]);
+      ld_w(j + 3 < kNJ ? u : u + 1, (j + 3) % kNJ, wf[1]);
+      if (j == 2 && more) stage_issue_values(u + 1);
+    }
+    if (more) stage_store(buf ^ 1);
+    __syncthreads();  // unit u's reads of buffer buf done; unit u + 1 staged in buf ^ 1
+    if (ks == nks - 1) {
+      // the item's sums: offset classes 0..3 add into buffer buf in order, then rows are written out
+      float* red = reinterpret_cast<float*>(xs[buf]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (oc == c) {
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              floatx4* dst = reinterpret_cast<floatx4*>(red + (16 * g + r) * NCB + ch * NCW + 16 * t + 4 * q);
+              *dst = c == 0 ? acc[g][t] : *dst + acc[g][t];
+            }
+        }
+        __syncthreads();
+      }
+      constexpr int QPR = NCB / 4;
+      for (int i = tid; i < T * QPR; i += NTH) {
+        const int row = i / QPR, cq = i - row * QPR;
+        const int32_t dst = perm[tile * T + row];
+        if (dst >= 0)
+          *reinterpret_cast<floatx4*>(out + (int64_t)dst * c_out + cy * NCB + 4 * cq) =
+              *reinterpret_cast<const floatx4*>(red + row * NCB + 4 * cq);
+      }
+      __syncthreads();  // buffer buf is free for the unit after next
+    }
+  }
+}
+
 inline int local_nt(int c_out) { return (c_out / 16) % 2 == 0 ? 2 : 1; }
 
 static int g_local_wr = 2;     // row parts per block (waves = 4 x wr); msp_debug_conv_local (experiments)
 static int g_local_order = 1;  // msp_tile_local: order rows inside a tile by neighbour mask
 static int g_local_nt = 0;     // forced column tiles per wave (0: local_nt)
 static int g_local_abl = 0;    // ablation variant (timing only; msp_debug_conv_local_abl)
+static int g_local_form = 2;   // 2: conv_x6l for 64 output channels, 1: wherever it applies, 0: conv_x6s
+
+inline int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
 
 }  // namespace msp
 
@@ -508,6 +763,10 @@ int msp_debug_conv_local(int wr, int order, int nt) {
 }
 
 int msp_debug_conv_local_abl(int abl) {
+  if (abl < 0) {  // -1 / -2 / -3: persistent form off / wherever it applies / 64 output channels only
+    g_local_form = abl == -2 ? 1 : (abl == -3 ? 2 : 0);
+    return MSP_OK;
+  }
   g_local_abl = abl;
   return MSP_OK;
 }
@@ -537,6 +796,24 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
+  if (((g_local_form == 1 && c_out % 32 == 0) || (g_local_form == 2 && c_out == 64)) && g_local_abl == 0) {
+    // persistent pipelined form: 16 NT columns per wave, two column halves per block
+    const int NT = c_out % 96 == 0 ? 3 : (c_out % 64 == 0 ? 2 : 1);
+    const int n_y = c_out / (32 * NT), nks = (c_in + 31) / 32;
+    u32x4* img = static_cast<u32x4*>(ws);
+    const int64_t lanes = (int64_t)K * (2 * n_y) * nks * NT * 64;
+    split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                               (flip >> 1) & 1);
+    const int64_t n_pad = n_tiles * tile_rows, n_items = n_tiles * n_y;
+    const unsigned grid = (unsigned)(n_items < cu_count() ? n_items : cu_count());
+#define LP(N)                                                                                                   \
+  if (NT == N)                                                                                                \
+    conv_x6l_kernel<N><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad, \
+                                            n_y, n_items, out);
+    LP(1) LP(2) LP(3)
+#undef LP
+    return check_launch("msp_conv_local");
+  }
   const int NT = (g_local_nt == 1 || (g_local_nt == 2 && c_out % 32 == 0)) ? g_local_nt : local_nt(c_out);
   const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
   u32x4* img = static_cast<u32x4*>(ws);

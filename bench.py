@@ -82,16 +82,23 @@ class KernelRecorder:
     current stream -- the stream the kernels are launched on -- and accumulates each call's algorithmic
     FLOPs and compulsory bytes.  mode "conv" records the conv family only."""
 
-    def __init__(self, mode="all"):
+    def __init__(self, mode="all", pool=8192):
         self.events = []
         self.active = False
         self.mode = mode
+        # events created up front and reused: creating two per call inside the timed steps cost ~3 ms of host
+        # time per step (scripts/bench_ab.py norec vs rec)
+        self.pool = [torch.cuda.Event(enable_timing=True) for _ in range(pool if mode != "none" else 0)]
+        self.used = 0
 
     def run(self, kind, flops, fn, nbytes=0):
         if not self.active or (self.mode == "conv" and family(kind) != "conv"):
             return fn()
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
+        if self.used + 2 <= len(self.pool):
+            s, e = self.pool[self.used], self.pool[self.used + 1]
+            self.used += 2
+        else:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         r = fn()
         e.record()
@@ -253,9 +260,14 @@ def main():
     ap.add_argument("--residual", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-iters", type=int, default=3, help="timed cpu_baseline iterations (median)")
-    ap.add_argument("--record", choices=["all", "conv", "none"], default="all",
-                    help="HIP-event bracketing of the recorded calls in the timed steps (roofline): every "
-                         "recorded family, the conv family only, or none")
+    ap.add_argument("--record", choices=["all", "conv", "none"], default="conv",
+                    help="HIP-event bracketing of the recorded calls in the timed steps (roofline): the conv "
+                         "family only (default), every recorded family, or none.  Every bracketed call costs "
+                         "about 2.5 us of stream time (all families: ~3 ms per step), so the other families' "
+                         "rooflines come from --family-steps extra recorded steps after the timed region")
+    ap.add_argument("--family-steps", type=int, default=5,
+                    help="untimed steps after the timed region with every family recorded (per-family rooflines "
+                         "and the step-level compulsory bytes); 0 = none")
     ap.add_argument("--foreach-adam", action="store_true", help="torch's foreach Adam instead of the fused one")
     ap.add_argument("--concurrent-wgrad", action="store_true",
                     help="weight gradients on a side stream beside the backward-data (sparseconvnet.ops)")
@@ -349,7 +361,7 @@ def main():
 
     for i in range(args.warmup):
         step(i)
-    rec = KernelRecorder(args.record)
+    rec = KernelRecorder(args.record, pool=2 * 700 * args.steps)
     _lib.set_recorder(rec if args.record != "none" else None)
     if world > 1:
         dist.barrier()
@@ -367,6 +379,20 @@ def main():
     dt_max, vox_all = dp.max_over_ranks(dt), dp.sum_over_ranks(float(vox))
     _lib.set_recorder(None)
     fams = rec.summary()
+    fam_steps = args.family_steps if args.record != "all" else 0
+    if fam_steps:
+        # every family bracketed, outside the timed region (see --record)
+        rec_all = KernelRecorder("all", pool=2 * 700 * fam_steps)
+        _lib.set_recorder(rec_all)
+        rec_all.active = True
+        for i in range(fam_steps):
+            step(args.steps + i)
+        rec_all.active = False
+        _lib.set_recorder(None)
+        fams_all = rec_all.summary()
+    else:
+        fams_all = fams
+        fam_steps = args.steps
 
     # one untimed forward for the per-level statistics and the MAC counter
     scn.forward_pass_multiplyAdd_count = 0
@@ -446,11 +472,14 @@ def main():
             }
             res["roofline_families"] = {
                 f: {k: v for k, v in d.items() if k != "per_kind" and k != "bytes"} | {"per_kind": d["per_kind"]}
-                for f, d in fams.items() if f != "conv"}
+                for f, d in fams_all.items()}
+            res["roofline_families"]["source"] = (
+                f"{fam_steps} recorded steps after the timed region (every family bracketed with HIP events)"
+                if fams_all is not fams else "the timed steps")
             # step level: F_alg = 6 x forward MACs (fwd, bwd-data, bwd-weight), B_alg = the
             # compulsory bytes of every recorded call + the Adam step (param, grad, 2 moments read; 3 written)
             f_alg = 6.0 * macs
-            b_rec = sum(d["bytes"] for d in fams.values()) / args.steps
+            b_rec = sum(d["bytes"] for d in fams_all.values()) / fam_steps
             b_alg = b_rec + 28.0 * n_params
             t_hbm = b_alg / (HBM_PEAK_GBS * 1e9) * 1e3
             t32 = f_alg / (FP32_MFMA_PEAK_TFLOPS * 1e12) * 1e3
@@ -460,7 +489,7 @@ def main():
                 "t_roof_ms_fp32_peak": max(t_hbm, t32), "frac_fp32_peak": max(t_hbm, t32) / ms_step,
                 "t_roof_ms_x6_peak": max(t_hbm, tx6), "frac_x6_peak": max(t_hbm, tx6) / ms_step,
                 "hbm_frac": t_hbm / ms_step,
-                "recorded_ms_per_step": sum(d["ms"] for d in fams.values()) / args.steps,
+                "recorded_ms_per_step": sum(d["ms"] for d in fams_all.values()) / fam_steps,
                 "note": "t_roof = max(B_alg / 8 TB/s, F_alg / peak); fp32 peak = 157.3 TF/s (f32 MFMA, the "
                         "arithmetic's native rate), x6 peak = 2500/6 TF/s (the split-bf16 path the convolutions "
                         "take); frac = t_roof / measured ms_per_step",

@@ -81,6 +81,7 @@ for L, size in enumerate(sizes):
             ops.CONV_LOCAL = var is not None
             if var is not None:
                 lib.msp_debug_conv_local(var[0], -1, var[2])
+                lib.msp_debug_conv_local_abl(-2 if len(var) > 3 and var[3] else -1)
                 rules._locals[128] = loc_sorted if var[1] else loc_key
             f = lambda: ops.conv_tile(x, wt, 27, flip, cout, rules, V)
             ms = timeit(f)
@@ -90,6 +91,7 @@ for L, size in enumerate(sizes):
         for abl in ABLS:
             lib.msp_debug_conv_local(2, -1, 0)
             rules._locals[128] = loc_sorted
+            lib.msp_debug_conv_local_abl(-1)
             lib.msp_debug_conv_local_abl(abl)
             ops.CONV_LOCAL = True
             ms = timeit(lambda: ops.conv_tile(x, wt, 27, flip, cout, rules, V))
@@ -97,5 +99,6 @@ for L, size in enumerate(sizes):
             lib.msp_debug_conv_local_abl(0)
         print(f"   {cin:3d}->{cout:3d}  " + "  ".join(res), flush=True)
         lib.msp_debug_conv_local(2, 1, 0)
+        lib.msp_debug_conv_local_abl(-2)
         rules._locals[128] = loc_sorted
 ops.CONV_LOCAL = True

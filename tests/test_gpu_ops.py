@@ -654,14 +654,18 @@ def test_tile_local_rulebook(order):
     _check_local_rulebook(rules.nbr, loc, lvl.n)
 
 
+@pytest.mark.parametrize("form", [-1, -2], ids=["x6s", "x6l"])
 @pytest.mark.parametrize("cin,cout,flip", [(64, 64, 2), (64, 64, 1), (96, 96, 2), (192, 96, 1), (48, 64, 2),
                                            (64, 48, 1), (128, 16, 2), (32, 160, 1)])
-def test_conv_local_accuracy(cin, cout, flip):
+def test_conv_local_accuracy(cin, cout, flip, form):
     """msp_conv_local (tile-local staging, split-bf16 MFMA) against an fp64 evaluation: below 1e-6 of the
     output scale (the x6 forms' bar), and against the production gather form.  flip 2 = forward with the
     module's [K][c_in][c_out] weights, 1 = backward-data ([K][c_out][c_in], offsets mirrored); c_in 48 has a
     half-empty 32-channel slice, c_out 48 / 16 / 160 run one 16-column tile per wave."""
-    from sparseconvnet import ops
+    import ctypes
+    from sparseconvnet import _lib, ops
+    lib = _lib.load()
+    lib.msp_debug_conv_local_abl.argtypes = [ctypes.c_int]
     torch.manual_seed(cin * 7 + cout + flip)
     coords, feats = _inputs(20000, 40, n_batch=2)
     t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
@@ -671,7 +675,11 @@ def test_conv_local_accuracy(cin, cout, flip):
     x = torch.randn(V, cin, device=DEV)
     w = torch.randn(27, cin, cout, device=DEV) / (27 * cin) ** 0.5
     wt = w if flip == 2 else w.transpose(1, 2).contiguous()
-    y = ops.conv_local(x, wt, 27, flip, cout, rules, V)
+    lib.msp_debug_conv_local_abl(form)  # -1: tile-per-block form (x6s), -2: persistent form (x6l) where it applies
+    try:
+        y = ops.conv_local(x, wt, 27, flip, cout, rules, V)
+    finally:
+        lib.msp_debug_conv_local_abl(-3)
     ref = _local_ref(x, w.transpose(1, 2), rules.nbr, flip & 1)  # [K][c_out][c_in], offsets mirrored for flip 1
     scale = ref.abs().max().item()
     err = (y.double() - ref).abs().max().item() / scale
