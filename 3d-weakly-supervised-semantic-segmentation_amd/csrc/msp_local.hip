@@ -684,6 +684,243 @@ __global__ __launch_bounds__(512, 2) void conv_x6l_kernel(
   }
 }
 
+// ---------------------------------------------------------------- tile-local weight gradient
+// dW[o][ci][co] = sum over rows i of x[nbr(i, o)][ci] dy[i][co] (submanifold, the forward's [K][c_in][c_out]
+// layout), over the same tile-local rulebook.  The pair-list form (msp_conv_wgrad) gathers x and dy per
+// rule from global memory and, at levels 0-1, refetches them 7-8x from past L2 (profiles/r01/
+// pmc_wgrad_pieces_r01zz.txt); here each tile's distinct x rows and its 128 dy rows are staged in LDS once
+// (split into bf16 pieces once) and every offset's rules read them from there.
+// Block = 8 waves, persistent over a contiguous range of tiles for one 32 x 32 (input x output channel)
+// slice of dW; wave w owns offsets w, w + 8, w + 16, w + 24 (< K) and keeps their 32 x 32 slices in
+// registers over the whole range.  MFMA k = 32 tile rows: lane (r, q) reads, for rows 8q .. 8q+7 of the
+// step, the bf16 pair (channels 2r, 2r+1) of each piece -- the 16 lanes of a row read 64 contiguous bytes --
+// and assembles the A (x, m-tile sa = channel parity) and B (dy, n-tile sb) fragments with byte permutes;
+// accumulator [o][sa][sb] register jj holds dW[o][ci0 + 2 (4q + jj) + sa][co0 + 2 r + sb].  The next tile's
+// rows are loaded into registers while the current one is computed.  Per range a slab of partial dW is
+// written; msp_conv_wgrad_local adds the ranges in order (deterministic).
+__device__ __forceinline__ uint32_t lo16x2(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
+__device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
+__global__ __launch_bounds__(512, 2) void wgrad_x6t_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, const uint16_t* __restrict__ lidx,
+    const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows, const int32_t* __restrict__ perm,
+    int K, int64_t n_tiles, int64_t n_pad, int n_ranges, float* __restrict__ slab) {
+  constexpr int T = 128, NTH = 512, NOW = 4;  // offsets per wave (K <= 32 over 8 waves)
+  constexpr int SI = (kUCap * 4 + NTH - 1) / NTH;
+  constexpr int LW = (kKMax * T / 2 + NTH - 1) / NTH;
+  constexpr int DYU = T * kXU;  // dy stage: T rows x 12 units
+  __shared__ u32x4 xs[kXR * kXU];
+  __shared__ u32x4 ds[DYU];
+  __shared__ uint32_t ls[kKMax * T / 2];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int n_sl_o = c_out / 32;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int slice = (int)(lb % ((c_in / 32) * n_sl_o));
+  const int range = (int)(lb / ((c_in / 32) * n_sl_o));
+  const int ci0 = 32 * (slice / n_sl_o), co0 = 32 * (slice % n_sl_o);
+  const int64_t t0 = (int64_t)range * n_tiles / n_ranges, t1 = (int64_t)(range + 1) * n_tiles / n_ranges;
+
+  floatx4 acc[NOW][2][2];
+#pragma unroll
+  for (int a = 0; a < NOW; ++a)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[a][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // staging registers of one tile: x rows (SI items of 8 channels), dy row (1 item), index-tile words
+  int32_t srow[SI];
+  floatx4 sv[SI][2], dv[2];
+  uint32_t slw[LW];
+  int s_us = 0;
+  auto issue_rows = [&](int64_t t) {
+    const int64_t u0 = u_start[t];
+    const int U = (int)(u_start[t + 1] - u0);
+    s_us = U < kUCap ? U : kUCap;
+#pragma unroll
+    for (int b = 0; b < SI; ++b) {
+      const int i = tid + NTH * b;
+      srow[b] = i < s_us * 4 ? u_rows[u0 + (i >> 2)] : 0;
+    }
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lidx);
+#pragma unroll
+    for (int b = 0; b < LW; ++b) {
+      const int i = tid + NTH * b;
+      if (i < K * T / 2) {
+        const int e = 2 * i, o = e / T, pp = e - o * T;
+        slw[b] = lw[((int64_t)o * n_pad + t * T + pp) >> 1];
+      }
+    }
+  };
+  auto issue_values = [&](int64_t t) {
+#pragma unroll
+    for (int b = 0; b < SI; ++b) {
+      const int i = tid + NTH * b;
+      sv[b][0] = sv[b][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (i < s_us * 4) {
+        const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + ci0 + 8 * (i & 3));
+        sv[b][0] = src[0];
+        sv[b][1] = src[1];
+      }
+    }
+    // dy: ordered row tid >> 2 of the tile, channel octet tid & 3 (T * 4 = NTH items)
+    const int32_t dr = perm[t * T + (tid >> 2)];
+    dv[0] = dv[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (dr >= 0) {
+      const floatx4* src = reinterpret_cast<const floatx4*>(dy + (int64_t)dr * c_out + co0 + 8 * (tid & 3));
+      dv[0] = src[0];
+      dv[1] = src[1];
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int b = 0; b < SI; ++b) {
+      const int i = tid + NTH * b;
+      if (i < s_us * 4) {
+        u32x4 pc[3];
+        split8(sv[b][0], sv[b][1], pc);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) xs[xs_unit(i >> 2, p, i & 3)] = pc[p];
+      }
+    }
+    {
+      u32x4 pc[3];
+      split8(dv[0], dv[1], pc);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) ds[xs_unit(tid >> 2, p, tid & 3)] = pc[p];
+    }
+#pragma unroll
+    for (int b = 0; b < LW; ++b) {
+      const int i = tid + NTH * b;
+      if (i < K * T / 2) ls[i] = slw[b];
+    }
+  };
+  // the bf16 pair (channels 2r, 2r+1) of piece p of staged row j
+  const uint32_t* xw = reinterpret_cast<const uint32_t*>(xs);
+  const uint32_t* dw = reinterpret_cast<const uint32_t*>(ds);
+  auto word = [&](const uint32_t* base, int j, int p) {
+    return base[xs_unit(j, p, r >> 2) * 4 + (r & 3)];
+  };
+  // fragments of 8 rows: f[s][p] = channel parity s of piece p over the rows, packed as 8 bf16
+  auto frags = [&](const uint32_t (&w)[8][3], u32x4 (&f)[2][3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        f[0][p][h] = lo16x2(w[2 * h][p], w[2 * h + 1][p]);
+        f[1][p][h] = hi16x2(w[2 * h][p], w[2 * h + 1][p]);
+      }
+  };
+
+  if (t0 < t1) {
+    issue_rows(t0);
+    issue_values(t0);
+    if (tid < kXU) xs[kUCap * kXU + tid] = u32x4{0u, 0u, 0u, 0u};
+    store();
+    __syncthreads();
+    for (int64_t t = t0; t < t1; ++t) {
+      const bool more = t + 1 < t1;
+      if (more) issue_rows(t + 1);
+      const uint16_t* lt = reinterpret_cast<const uint16_t*>(ls);
+#pragma unroll
+      for (int kk = 0; kk < T / 32; ++kk) {
+        if (kk == 1 && more) issue_values(t + 1);
+        const int rb = 32 * kk + 8 * q;  // this lane's 8 tile rows
+        uint32_t wd[8][3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) wd[j][p] = word(dw, rb + j, p);
+        u32x4 bf[2][3];
+        frags(wd, bf);
+#pragma unroll
+        for (int a = 0; a < NOW; ++a) {
+          const int o = wave + 8 * a;
+          if (o >= K) break;  // wave-uniform
+          int li[8];
+          bool any = false;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            li[j] = lt[o * T + rb + j];
+            any |= li[j] != kAbsent;
+          }
+          if (ballot64(any) == 0) continue;  // no row of the 32 has this offset
+          uint32_t wx[8][3];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int jr = li[j] < kUCap ? li[j] : kUCap;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) wx[j][p] = word(xw, jr, p);
+          }
+          bool farj = false;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) farj |= li[j] >= kUCap && li[j] != kAbsent;
+          if (ballot64(farj)) {
+            // rows past the staged capacity (rare): their pair straight from global memory, split here
+            const int64_t u0 = u_start[t];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              if (li[j] >= kUCap && li[j] != kAbsent) {
+                const float2 v = *reinterpret_cast<const float2*>(x + (int64_t)u_rows[u0 + li[j]] * c_in + ci0 + 2 * r);
+                float a0 = v.x, a1 = v.y;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                  const uint32_t h = pk_bf16(a0, a1);
+                  wx[j][p] = h;
+                  a0 -= __uint_as_float(h << 16);
+                  a1 -= __uint_as_float(h & 0xffff0000u);
+                }
+              }
+            }
+          }
+          u32x4 af[2][3];
+          frags(wx, af);
+#pragma unroll
+          for (int sa = 0; sa < 2; ++sa)
+#pragma unroll
+            for (int sb = 0; sb < 2; ++sb) {
+              floatx4 c = mfma_bf16(af[sa][2], bf[sb][0], floatx4{0.f, 0.f, 0.f, 0.f});
+              c = mfma_bf16(af[sa][1], bf[sb][1], c);
+              c = mfma_bf16(af[sa][0], bf[sb][2], c);
+              c = mfma_bf16(af[sa][1], bf[sb][0], c);
+              c = mfma_bf16(af[sa][0], bf[sb][1], c);
+              acc[a][sa][sb] += mfma_bf16(af[sa][0], bf[sb][0], c);
+            }
+        }
+      }
+      __syncthreads();  // reads of tile t done
+      if (more) store();
+      __syncthreads();
+    }
+  }
+  // partial dW of this range: slab[range][o][ci][co]
+  float* sb = slab + (int64_t)range * K * c_in * c_out;
+#pragma unroll
+  for (int a = 0; a < NOW; ++a) {
+    const int o = wave + 8 * a;
+    if (o >= K) break;
+#pragma unroll
+    for (int sa = 0; sa < 2; ++sa)
+#pragma unroll
+      for (int sbb = 0; sbb < 2; ++sbb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          sb[((int64_t)o * c_in + ci0 + 2 * (4 * q + jj) + sa) * c_out + co0 + 2 * r + sbb] = acc[a][sa][sbb][jj];
+  }
+}
+
+// dW[e] = sum over ranges in order of slab[range][e]
+__global__ __launch_bounds__(256) void wgrad_ranges_reduce_kernel(const floatx4* __restrict__ slab, int n_ranges,
+                                                                  int64_t n4, floatx4* __restrict__ dw) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  floatx4 s = slab[i];
+  for (int k = 1; k < n_ranges; ++k) s += slab[(int64_t)k * n4 + i];
+  dw[i] = s;
+}
+
 inline int local_nt(int c_out) { return (c_out / 16) % 2 == 0 ? 2 : 1; }
 
 static int g_local_wr = 2;     // row parts per block (waves = 4 x wr); msp_debug_conv_local (experiments)
@@ -775,6 +1012,37 @@ int msp_debug_conv_local_abl(int abl) {
 // profiles/r02/kbench_local_r02_levels.log): ahead from 64 channels on both sides and 4096 rows up (levels
 // 1-4 of m = 32: 0-34 % less time), behind on the 32-channel level 0 (the per-wave tile form x6r and the
 // dense row groups) and on the few-tile levels 5-6 (grids of 16 / 4 tiles).
+int msp_wgrad_local_ok(int64_t n_rows, int K, int c_in, int c_out) {
+  return (n_rows > 0 && K <= kKMax && c_in % 32 == 0 && c_out % 32 == 0) ? 1 : 0;
+}
+
+int64_t msp_wgrad_local_ranges(int64_t n_rows, int c_in, int c_out) {
+  const int64_t n_tiles = ceil_div(n_rows > 0 ? n_rows : 1, 128);
+  const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
+  int64_t r = cu_count() / (slices > 0 ? slices : 1);
+  if (r < 1) r = 1;
+  return r < n_tiles ? r : n_tiles;
+}
+
+int msp_conv_wgrad_local(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
+                         const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
+                         int64_t n_rows, int64_t n_ranges, float* slab, float* dw, msp_stream_t stream) {
+  MSP_REQUIRE(msp_wgrad_local_ok(n_rows, K, c_in, c_out), "msp_conv_wgrad_local: needs K <= %d and channels in "
+              "multiples of 32 (K=%d c_in=%d c_out=%d)", kKMax, K, c_in, c_out);
+  MSP_REQUIRE(tile_rows == 128, "msp_conv_wgrad_local: tile_rows must be 128 (got %d)", tile_rows);
+  MSP_REQUIRE(n_ranges >= 1, "msp_conv_wgrad_local: n_ranges must be >= 1");
+  hipStream_t s = as_stream(stream);
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
+  const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
+  wgrad_x6t_kernel<<<(unsigned)(n_ranges * slices), 512, 0, s>>>(x, c_in, dy, c_out, lidx, u_start, u_rows, perm, K,
+                                                                   n_tiles, n_tiles * tile_rows, (int)n_ranges, slab);
+  const int64_t n4 = (int64_t)K * c_in * c_out / 4;
+  wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
+                                                                         (int)n_ranges, n4,
+                                                                         reinterpret_cast<floatx4*>(dw));
+  return check_launch("msp_conv_wgrad_local");
+}
+
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {
   return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 64 && c_out >= 64 && n_rows >= 4096) ? 1 : 0;
 }

@@ -189,6 +189,32 @@ def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
     return dw
 
 
+# tile-local weight gradient (msp_conv_wgrad_local) instead of the pair-list form where it applies.  Off: on the
+# headline batch it ran 0.84-1.2x the pair-list form's speed (scripts/kbench_wgrad_local.py,
+# profiles/r02/kbench_wgrad_local_r02.log) -- its dense 32-row steps carry ~45 % zero rows, the pair lists none.
+WGRAD_LOCAL = False
+
+
+def conv_wgrad_local(x, dy, rules, K, kind="wgrad", flops=None):
+    """Submanifold weight gradient over the tile-local rulebook (SubmRules.local): per tile the distinct x rows
+    and the dy rows staged in LDS once; partial sums per tile range added in order (msp_conv_wgrad_local)."""
+    c_in, c_out = x.size(1), dy.size(1)
+    n = dy.size(0)
+    loc = rules.local()
+    ranges = int(_lib.query("msp_wgrad_local_ranges", _lib.I64(n), c_in, c_out))
+    dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
+    slab = torch.empty((ranges, K, c_in, c_out), dtype=torch.float32, device=x.device)
+    if flops is None:
+        flops = 2.0 * rules.n_rules * c_in * c_out
+    # compulsory bytes: x and dy rows, the tile-local rulebook, dW
+    nbytes = 4 * (x.size(0) * c_in + n * c_out + K * c_in * c_out) + \
+        4 * loc["total"] + 2 * K * loc["n_tiles"] * loc["tile_rows"] + 4 * loc["n_tiles"] * loc["tile_rows"]
+    _record(kind + "/x6t", flops, lambda: call(
+        "msp_conv_wgrad_local", ptr(x), c_in, ptr(dy), c_out, K, loc["tile_rows"], ptr(loc["lidx"]),
+        ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), n, ranges, ptr(slab), ptr(dw), _stream(x)), nbytes)
+    return dw
+
+
 def conv_nbr(x, wt, K, flip, c_out, nbr, n_rows, kind="conv_nbr", flops=0, perm=None):
     """Dense row-group form of the submanifold convolution straight from the
     neighbour map nbr[K][n_rows] (msp_conv_nbr: no tile rulebook); with perm,
@@ -235,7 +261,9 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             p = rules.pairs
             V = xp.size(0)
-            if int(_lib.query("msp_wgrad_band_ok", _lib.I64(V), K, cin_p, cout_p)):
+            if WGRAD_LOCAL and int(_lib.query("msp_wgrad_local_ok", _lib.I64(V), K, cin_p, cout_p)):
+                dwp = conv_wgrad_local(xp, g, rules, K, flops=2.0 * p.total * cin * cout)
+            elif int(_lib.query("msp_wgrad_band_ok", _lib.I64(V), K, cin_p, cout_p)):
                 dwp = conv_wgrad_band(xp, g, p, K, V)  # rows staged in LDS per band
             else:  # weight gradient beside the backward-data (opt-in)
                 dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)

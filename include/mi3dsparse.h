@@ -174,6 +174,17 @@ int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows);
  * [K][c_in][c_out], else [K][c_out][c_in]).  Workspace:
  * msp_conv_local_workspace_size (the split weight image). */
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out);
+
+/* Submanifold weight gradient over the same tile-local rulebook: dW[o][ci][co] = sum over rows i of
+ * x[nbr(i, o)][ci] dy[i][co] (the forward's [K][c_in][c_out] layout), each tile's distinct x rows and its dy
+ * rows staged in LDS once.  Channels in multiples of 32, K <= 27 (msp_wgrad_local_ok).  Blocks run
+ * n_ranges contiguous tile ranges (msp_wgrad_local_ranges) per 32 x 32 channel slice; slab holds
+ * n_ranges x K x c_in x c_out floats of partial sums, added in range order into dw. */
+int msp_wgrad_local_ok(int64_t n_rows, int K, int c_in, int c_out);
+int64_t msp_wgrad_local_ranges(int64_t n_rows, int c_in, int c_out);
+int msp_conv_wgrad_local(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
+                         const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
+                         int64_t n_rows, int64_t n_ranges, float* slab, float* dw, msp_stream_t stream);
 size_t msp_conv_local_workspace_size(int K, int c_in, int c_out);
 int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                    const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,

@@ -11,8 +11,8 @@ print(f"total kernel time {tot/1e6:.1f} ms")
 # split_weights [+ split_reduce]): average per call, to set beside bench.py's
 # roofline.avg_launch_us (HIP events around each call)
 fam = ("conv_x6g_kernel", "conv_x6r_kernel", "conv_x6d_kernel", "conv_x6p_kernel", "conv_tile7_kernel",
-       "conv_tilep_kernel", "conv_tile4_kernel", "conv_tile_kernel")
-ft = sum(float(r['TotalDurationNs']) for r in rows if any(c in r['Name'] for c in fam + ("split_weights_kernel", "split_reduce_kernel")))
+       "conv_tilep_kernel", "conv_tile4_kernel", "conv_tile_kernel", "conv_x6s_kernel", "conv_x6l_kernel")
+ft = sum(float(r['TotalDurationNs']) for r in rows if any(c in r['Name'] for c in fam + ("split_weights_kernel", "split_weights_lane_kernel", "split_reduce_kernel")))
 fn = sum(int(r['Calls']) for r in rows if any(c + '<' in r['Name'] or c + '(' in r['Name'] for c in fam))
 if fn:
     print(f"conv family: {fn} calls, {ft / fn / 1e3:.1f} us per call (kernel + split_weights + split_reduce)")

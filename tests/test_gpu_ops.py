@@ -715,3 +715,28 @@ def test_conv_local_overflow_rows():
     y = ops.conv_local(x, w, K, 2, 32, r, V)
     ref = _local_ref(x, w.transpose(1, 2), nbr, 0)
     assert (y.double() - ref).abs().max().item() / ref.abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 32), (64, 32), (96, 64), (64, 128)])
+def test_conv_wgrad_local_accuracy(cin, cout):
+    """msp_conv_wgrad_local (tile-local weight gradient, split-bf16 MFMA) against an fp64 evaluation of
+    dW[o] = sum_i x[nbr(i, o)]^T dy[i], and against the pair-list form."""
+    from sparseconvnet import ops
+    torch.manual_seed(cin + 3 * cout)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    rules = t.metadata.level(64).subm_rules(3)
+    V = t.metadata.level(64).n
+    x = torch.randn(V, cin, device=DEV)
+    dy = torch.randn(V, cout, device=DEV)
+    dw = ops.conv_wgrad_local(x, dy, rules, 27)
+    nb = rules.nbr.long()
+    ref = torch.empty(27, cin, cout, dtype=torch.float64, device=DEV)
+    for o in range(27):
+        m = nb[o] >= 0
+        ref[o] = x.double()[nb[o][m]].t() @ dy.double()[m]
+    scale = ref.abs().max().item()
+    assert (dw.double() - ref).abs().max().item() / scale < 1e-6
+    p = rules.pairs
+    dwp = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
+    assert (dw - dwp).abs().max().item() / scale < 3e-6
