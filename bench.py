@@ -145,10 +145,13 @@ class KernelRecorder:
 
 
 def pmc_traffic():
-    """HBM bytes per msp_conv_tile call measured with rocprofv3 PMC counters on
-    this workload (scripts/pmc_traffic.sh; committed under profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    if not os.path.isfile(path):
+    """HBM bytes per conv-family call measured with rocprofv3 PMC counters on this workload
+    (scripts/pmc_traffic.sh; committed under profiles/, newest round first), or None."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        if os.path.isfile(path):
+            break
+    else:
         return None, None
     with open(path) as f:
         d = json.load(f)
@@ -273,6 +276,9 @@ def main():
                     help="weight gradients on a side stream beside the backward-data (sparseconvnet.ops)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="build each batch's metadata inside its own forward (no side-stream input pipelining)")
+    ap.add_argument("--prefetch-at", choices=["end", "fwd"], default="end",
+                    help="when the next batch's metadata is built: after the step's optimizer call is queued (end) "
+                         "or right after its forward is queued (fwd: the build's host reads overlap the forward)")
     ap.add_argument("--workload", choices=["unet", "contrastive"], default=None,
                     help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
                          "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
@@ -344,19 +350,28 @@ def main():
     cls_loss, _ = LOSS_REGISTRY.get("Classification")
     con_loss, _ = LOSS_REGISTRY.get("TextContrastive")
 
+    prefetch_s = []
+
+    def prefetch(i):
+        # input pipelining: the next batch's voxelisation and rulebooks on a side stream while this step's
+        # kernels run (sparseconvnet.prefetch_metadata)
+        t = time.perf_counter()
+        scn.prefetch_metadata(model, batches[(i + 1) % len(batches)][0].coords, wait_for_producer=False)
+        prefetch_s.append(time.perf_counter() - t)
+
     def step(i):
         x, y, _, text = batches[i % len(batches)]
         opt.zero_grad(set_to_none=True)
         logits, meta = model((x, text), istrain=True)
+        if not args.no_prefetch and args.prefetch_at == "fwd":
+            prefetch(i)
         loss = cls_loss(logits, y)
         if contrastive:
             loss = loss + con_loss(*meta)
         loss.backward()
         opt.step()
-        if not args.no_prefetch:
-            # input pipelining: the next batch's voxelisation and rulebooks on a
-            # side stream while this step's backward drains (sparseconvnet.prefetch_metadata)
-            scn.prefetch_metadata(model, batches[(i + 1) % len(batches)][0].coords, wait_for_producer=False)
+        if not args.no_prefetch and args.prefetch_at == "end":
+            prefetch(i)
         return loss
 
     for i in range(args.warmup):
@@ -443,7 +458,9 @@ def main():
                 "parallelism": f"dp{world}",
                 "comm_backend": dist.get_backend() if world > 1 else None,
                 "input_pipeline": "none" if args.no_prefetch else
-                "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step",
+                "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step "
+                f"(after its {'optimizer' if args.prefetch_at == 'end' else 'forward'} call is queued; host "
+                f"time {1e3 * statistics.median(prefetch_s) if prefetch_s else 0:.1f} ms median)",
                 "active_voxels_per_step_rank0": batches[0][2],
                 "levels": stats,
                 "fwd_multiply_adds": macs,
@@ -452,7 +469,8 @@ def main():
         }
         if conv is not None:
             res["roofline"] = {
-                "kernel": "msp_conv_tile / msp_conv_nbr (submanifold fwd/bwd-data, strided conv fwd, deconv bwd-data)",
+                "kernel": "msp_conv_local / msp_conv_tile / msp_conv_nbr (submanifold fwd/bwd-data, strided conv fwd, "
+                          "deconv bwd-data)",
                 "bound": "mfma",
                 "achieved": conv["achieved"],
                 "peak": conv["peak"],
@@ -462,7 +480,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": conv["frac"],
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per msp_conv_tile / msp_conv_nbr call (PMC 2*FETCH_SIZE + WRITE_SIZE)",
+                "traffic_unit": "HBM bytes per conv-family call (PMC 2*FETCH_SIZE + WRITE_SIZE)",
                 "traffic_source": traffic_src,
                 "alg_bytes_per_call": conv["bytes"] / max(conv["launches"], 1),
                 "alg_bytes_gbs": conv["gbs"],

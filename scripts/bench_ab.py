@@ -27,7 +27,7 @@ for v in os.environ.get("AB", "tile,nbr").split(","):
     elif v.startswith("g"):
         lib.msp_debug_conv_nbr_variant(int(v[1:]))
     sys.argv = ["bench.py", "--steps", os.environ.get("STEPS", "10"), "--warmup", "2", "--no-cpu"] + \
-        (["--foreach-adam"] if v == "foreach" else []) + (["--concurrent-wgrad"] if v == "cw" else []) + (["--record", "none"] if v == "norec" else []) + (["--record", "conv"] if v == "recconv" else [])
+        (["--foreach-adam"] if v == "foreach" else []) + (["--concurrent-wgrad"] if v == "cw" else []) + (["--record", "none"] if v == "norec" else []) + (["--record", "conv"] if v == "recconv" else []) + (["--prefetch-at", "fwd"] if v == "pfwd" else []) + (["--no-prefetch"] if v == "nopf" else [])
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         bench.main()
@@ -35,4 +35,4 @@ for v in os.environ.get("AB", "tile,nbr").split(","):
     d = json.loads(line)
     res.append((v, d["ms_per_step"]))
     conv = d.get("roofline", {}).get("achieved", float("nan"))
-    print(f"{v:8s} {d['ms_per_step']:.2f} ms/step  conv TF/s {conv:.1f}", flush=True)
+    print(f"{v:8s} {d['ms_per_step']:.2f} ms/step  conv TF/s {conv:.1f}  {d['config']['input_pipeline'][-40:]}", flush=True)

@@ -3,15 +3,15 @@
 HBM/rocprofv3 section): FETCH_SIZE is doubled (gfx950 tallies 128-B
 requests at 64 B), WRITE_SIZE taken as is; both are in KB per dispatch.
 
-One msp_conv_tile call launches one conv kernel (conv_x6d / conv_x6r / conv_x6g / conv_x6p / conv_tilep /
-conv_tile7 / conv_tile4 / conv_tile) plus, for the x6 form, a
-split_weights and, for split grids, a split_reduce; traffic per call = sum
+One conv-family call (msp_conv_local / msp_conv_tile / msp_conv_nbr) launches one conv kernel (conv_x6s /
+conv_x6l / conv_x6d / conv_x6r / conv_x6g, older forms conv_x6p / conv_tilep / conv_tile7 / conv_tile4 /
+conv_tile) plus a split_weights(_lane) and, for split grids, a split_reduce; traffic per call = sum
 over the family's dispatches / number of conv kernel dispatches.
 Writes JSON: python scripts/pmc_traffic.py gpurun_out/pmc_<tag> out.json"""
 import csv, glob, json, os, sys
 
 root, out_path = sys.argv[1], sys.argv[2]
-conv_names = ("conv_x6d_kernel", "conv_x6p_kernel", "conv_x6r_kernel", "conv_x6g_kernel", "conv_tile7_kernel", "conv_tilep_kernel", "conv_tile4_kernel", "conv_tile_kernel")
+conv_names = ("conv_x6s_kernel", "conv_x6l_kernel", "conv_x6d_kernel", "conv_x6p_kernel", "conv_x6r_kernel", "conv_x6g_kernel", "conv_tile7_kernel", "conv_tilep_kernel", "conv_tile4_kernel", "conv_tile_kernel")
 tot = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
 ndisp = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}
 dur = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}
@@ -22,16 +22,16 @@ for f in sorted(glob.glob(os.path.join(root, "pass*", "**", "*counter_collection
         if ctr not in tot:
             continue
         is_conv = any(c + "<" in name or c + "(" in name for c in conv_names)
-        if is_conv or "split_reduce_kernel" in name or "split_weights_kernel" in name:
+        if is_conv or "split_reduce_kernel" in name or "split_weights_kernel" in name or "split_weights_lane_kernel" in name:
             tot[ctr] += float(r["Counter_Value"]) * 1024.0
             if is_conv:
                 ndisp[ctr] += 1
                 dur[ctr] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
 fetch = 2.0 * tot["FETCH_SIZE"] / max(ndisp["FETCH_SIZE"], 1)
 write = tot["WRITE_SIZE"] / max(ndisp["WRITE_SIZE"], 1)
-res = {"kernel": "msp_conv_tile / msp_conv_nbr", "calls": ndisp["FETCH_SIZE"],
+res = {"kernel": "msp_conv_local / msp_conv_tile / msp_conv_nbr", "calls": ndisp["FETCH_SIZE"],
        "fetch_bytes_per_call": fetch, "write_bytes_per_call": write, "traffic_bytes_per_call": fetch + write,
        "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE in separate runs of "
-               "`bench.py --steps 2 --warmup 1 --no-cpu`; conv kernel + split_weights + split_reduce dispatches per call"}
+               "`bench.py --steps 2 --warmup 1 --no-cpu`; conv kernel + split_weights(_lane) + split_reduce dispatches per call"}
 json.dump(res, open(out_path, "w"), indent=1)
 print(json.dumps(res, indent=1))
