@@ -1023,14 +1023,24 @@ size_t x6g_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c
 // super-steps round-robin, two register sets deep; positions past the piece
 // are clamped to its last pair and their x values zeroed (uniform branch:
 // only the last super-step of a wave in a piece can be partial).
-// ABL (timing only): 1 = no splits (raw bits as the pieces), 2 = no MFMAs.
-template <int WA, int WB, int ABL = 0>
-__global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
+// ABL (timing only, bits): 1 = no splits (raw bits as the pieces), 2 = no MFMAs, 4 = no row loads,
+// 8 = no pair-list loads.
+// d[j] = v of lane B + j of this lane's row of 16 (DPP row_newbcast), j = 0 .. 7
+template <int B, int... J>
+__device__ __forceinline__ void row_bcast8_(int32_t v, int32_t (&d)[8], std::integer_sequence<int, J...>) {
+  ((d[J] = __builtin_amdgcn_update_dpp(0, v, 0x150 + B + J, 0xF, 0xF, false)), ...);
+}
+template <int B>
+__device__ __forceinline__ void row_bcast8(int32_t v, int32_t (&d)[8]) {
+  row_bcast8_<B>(v, d, std::make_integer_sequence<int, 8>{});
+}
+
+template <int WA, int WB, int ABL = 0, int D = 2>
+__global__ __launch_bounds__(kThreads, D == 1 ? 4 : 1) void wgrad_x6_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
     const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
     int K, int64_t n_pieces, int n_ty, float* __restrict__ slab) {
   constexpr int TM = 16 * WA, TN = 16 * WB;
-  constexpr int D = 2;
   __shared__ float red[TM * TN];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
@@ -1051,36 +1061,41 @@ __global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
 #pragma unroll
     for (int t = 0; t < WB; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // pair indices: one word per lane per super-step (lanes r < 8 of row q hold pin of pairs 8q .. 8q+7, lanes
+  // r >= 8 their pout), handed to the 16 lanes of the row by DPP row broadcasts -- one coalesced load instead
+  // of 16 per lane
   struct Ix {
-    int32_t i[8], o[8];
+    int32_t w;
   };
   struct Vals {
     float a[8][WA], b[8][WB];
   };
+  const int32_t* pix = r < 8 ? pin : pout;
   auto ld_idx = [&](int64_t g, Ix& d) {
-    const int64_t pp = g + 8 * q;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t pc = min(pp + k, p1 - 1);
-      d.i[k] = pin[pc];
-      d.o[k] = pout[pc];
-    }
+    const int64_t pc = min(g + 8 * q + (r & 7), p1 - 1);
+    d.w = (ABL & 8) ? (int32_t)(pc >> 4) : pix[pc];  // ABL 8 (timing only): synthetic rows, pc / 16 < n_rows
   };
   const float* xm = x + m0 + WA * r;
   const float* dyn = dy + n0 + WB * r;
   auto ld_val = [&](const Ix& d, Vals& v) {
+    int32_t ii[8], oo[8];
+    row_bcast8<0>(d.w, ii);
+    row_bcast8<8>(d.w, oo);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      load_vec<WA>(xm + (int64_t)d.i[k] * c_in, v.a[k]);
-      load_vec<WB>(dyn + (int64_t)d.o[k] * c_out, v.b[k]);
+      if (ABL & 4) {  // timing only: values from the indices instead of the row loads
+#pragma unroll
+        for (int i = 0; i < WA; ++i) v.a[k][i] = (float)(ii[k] + i) * 1e-6f;
+#pragma unroll
+        for (int t = 0; t < WB; ++t) v.b[k][t] = (float)(oo[k] + t) * 1e-6f;
+      } else {
+        load_vec<WA>(xm + (int64_t)ii[k] * c_in, v.a[k]);
+        load_vec<WB>(dyn + (int64_t)oo[k] * c_out, v.b[k]);
+      }
     }
   };
-  auto compute = [&](int64_t g, const Vals& v) {
-    float a[8][WA];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int i = 0; i < WA; ++i) a[k][i] = v.a[k][i];
+  auto compute = [&](int64_t g, Vals& v) {
+    auto& a = v.a;
     if (g + 32 > p1) {  // uniform: partial super-step, zero the x values of pairs past the piece
       const int64_t pp = g + 8 * q;
 #pragma unroll
@@ -1126,7 +1141,9 @@ __global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
   constexpr int64_t kStride = 32 * kWaves;
   const int64_t g0 = p0 + 32 * wave;
   if (g0 < p1) {  // wave-uniform
-    Ix X[D];
+    // values run D super-steps ahead, indices U = 2D ahead of their values (one VGPR per set)
+    constexpr int U = 2 * D;
+    Ix X[U];
     Vals V[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -1134,20 +1151,21 @@ __global__ __launch_bounds__(kThreads) void wgrad_x6_kernel(
       ld_val(X[k], V[k]);
     }
 #pragma unroll
-    for (int k = 0; k < D; ++k) ld_idx(g0 + (D + k) * kStride, X[k]);
-    for (int64_t g = g0; g < p1; g += D * kStride) {
+    for (int k = 0; k < U; ++k) ld_idx(g0 + (D + k) * kStride, X[k]);
+    for (int64_t g = g0; g < p1; g += U * kStride) {
 #pragma unroll
-      for (int k = 0; k < D; ++k) {
-        if (g + k * kStride < p1) compute(g + k * kStride, V[k]);
+      for (int k = 0; k < U; ++k) {
+        Vals& v = V[k % D];
+        if (g + k * kStride < p1) compute(g + k * kStride, v);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {  // mark the set read on every path
 #pragma unroll
-          for (int i = 0; i < WA; ++i) asm volatile("" ::"v"(V[k].a[kk][i]));
+          for (int i = 0; i < WA; ++i) asm volatile("" ::"v"(v.a[kk][i]));
 #pragma unroll
-          for (int t = 0; t < WB; ++t) asm volatile("" ::"v"(V[k].b[kk][t]));
+          for (int t = 0; t < WB; ++t) asm volatile("" ::"v"(v.b[kk][t]));
         }
-        ld_val(X[k], V[k]);
-        ld_idx(g + (2 * D + k) * kStride, X[k]);
+        ld_val(X[k], v);                                 // step + D
+        ld_idx(g + (k + D + U) * kStride, X[k]);         // step + D + U
       }
     }
   }
@@ -1434,8 +1452,17 @@ int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const 
                                                         K, n_pieces, n_ty, slab);                         \
     launched = true;                                                                                      \
   }
+#define LWD(A, B)                                                                                             \
+  if (!launched && WA == A && WB == B && (g_wgrad_abl & 16)) {                                               \
+    wgrad_x6_kernel<A, B, 0, 1><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, \
+                                                          K, n_pieces, n_ty, slab);                         \
+    launched = true;                                                                                         \
+  }
+  LWD(2, 2) LWD(3, 2) LWD(4, 2)
+#undef LWD
   if (g_wgrad_abl) {
     LWA(2, 2, 1) LWA(4, 2, 1) LWA(2, 2, 2) LWA(4, 2, 2) LWA(2, 2, 3) LWA(4, 2, 3)
+    LWA(2, 2, 4) LWA(4, 2, 4) LWA(2, 2, 8) LWA(4, 2, 8) LWA(2, 2, 12) LWA(4, 2, 12) LWA(2, 2, 15) LWA(4, 2, 15)
   }
 #undef LWA
   LW(1, 1) LW(2, 1) LW(3, 1) LW(4, 1) LW(1, 2) LW(2, 2) LW(3, 2) LW(4, 2)
