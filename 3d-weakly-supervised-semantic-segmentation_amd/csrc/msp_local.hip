@@ -921,6 +921,304 @@ __global__ __launch_bounds__(256) void wgrad_ranges_reduce_kernel(const floatx4*
   dw[i] = s;
 }
 
+// ---------------------------------------------------------------- chunk-local convolution (narrow levels)
+// Level 0 of the m = 32 UNet has 32 channels and 7.7 rules per row: the dense 16-row groups of conv_x6s fill
+// 0.37 of their MFMA rows there, and the per-wave gather tiles (conv_x6r) fetch every rule's row from L2/MALL
+// (1.3 GB per call) and stall on that latency.  This form keeps the compacted chunks of the tile rulebook
+// (16 rules of one offset per chunk: 0.71 of the MFMA rows carry a rule with 64-row tiles) but reads their
+// input rows from LDS: a 128-row unit (two 64-row rulebook tiles) stages its distinct input rows once per 32
+// input channels (fp32, 1.57 x 128 rows on average), and the chunks scatter their 16 x 32 partial products into
+// fp32 accumulators in LDS.
+//
+// Metadata (msp_chunk_local, from the 64-row tile rulebook): per unit the sorted distinct input rows of its
+// chunks (first kQCap of them), and per chunk entry a packed word: position in that list (0xFFFF past kQCap:
+// read from global memory) | row inside the unit << 16 (128: padding slot).
+//
+// Kernel (conv_x6q): block = 4 waves on one unit and 32 output columns; wave (h, c) takes half h's chunks
+// (tile 2 unit + h), class c = the first or second half of that tile's chunk list.  The two classes own
+// separate accumulators (rows of one class never meet in two waves at once: chunks of one offset name
+// distinct rows, and a class is processed in order by one wave per half); they are added in class order at
+// the end, so results are deterministic.  Weights: the lane-ordered split image of split_weights_lane_kernel,
+// one register set per offset run, the next two runs' sets loaded ahead.
+constexpr int kQT = 64;        // rulebook tile rows (half a unit)
+constexpr int kQUnit = 128;    // rows of a unit
+constexpr int kQCap = 320;     // staged distinct rows per unit (slot kQCap: zero row)
+constexpr uint32_t kQFar = 0xFFFFu;
+
+// staged row j (32 fp32 channels = 8 16-byte units): unit u at j*8 + (u ^ ((j >> 1) & 7)) -- the 16 distinct
+// rows j mod 16 of one ds_read_b128 lane group land on 16 distinct bank quads at a fixed u
+__device__ __forceinline__ int xq_unit(int j, int u) { return j * 8 + (u ^ ((j >> 1) & 7)); }
+// accumulator row (AU 16-byte units): the same spreading for AU = 8 (32 columns) and AU = 4 (16 columns)
+template <int AU>
+__device__ __forceinline__ int aq_unit(int row, int u) {
+  return row * AU + (u ^ ((row >> (AU == 8 ? 1 : 2)) & (AU - 1)));
+}
+
+template <int N2>
+__global__ __launch_bounds__(kLT) void chunk_local_kernel(const int64_t* __restrict__ tile_start, int64_t n_tiles,
+                                                          const int32_t* __restrict__ chunk_src,
+                                                          const uint16_t* __restrict__ chunk_row,
+                                                          int32_t* __restrict__ u_rows, int32_t* __restrict__ u_cnt,
+                                                          uint32_t* __restrict__ chunk_lr) {
+  constexpr int PER = N2 / kLT;
+  __shared__ int32_t a[N2];
+  __shared__ int32_t uq[N2];
+  const int64_t u = blockIdx.x;
+  const int64_t t0 = 2 * u, t1 = t0 + 1 < n_tiles ? t0 + 2 : t0 + 1;
+  const int64_t e0 = tile_start[t0] * MSP_CHUNK, e1 = tile_start[t1] * MSP_CHUNK;
+  const int64_t emid = tile_start[t0 + 1] * MSP_CHUNK;  // first entry of the second tile
+  const int ne = (int)(e1 - e0);                        // <= N2 (host checks the largest tile)
+  for (int i = threadIdx.x; i < N2; i += kLT) a[i] = i < ne ? chunk_src[e0 + i] : INT32_MAX;
+  __syncthreads();
+  bitonic_i32<N2>(a);
+  const int base = threadIdx.x * PER;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = base + j;
+    c += a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1]);
+  }
+  int tot;
+  int off = block_excl_scan<kLT>(c, &tot);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = base + j;
+    if (a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1])) {
+      uq[off] = a[i];
+      if (off < kQCap) u_rows[u * kQCap + off] = a[i];
+      ++off;
+    }
+  }
+  for (int j = tot + threadIdx.x; j < kQCap; j += kLT) u_rows[u * kQCap + j] = -1;  // unused slots: -1
+  if (threadIdx.x == 0) u_cnt[u] = tot;
+  __syncthreads();
+  for (int i = threadIdx.x; i < ne; i += kLT) {
+    const int64_t e = e0 + i;
+    const int32_t v = chunk_src[e];
+    int lo = 0, hi = tot;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (uq[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    const int rt = chunk_row[e];
+    const uint32_t row = rt >= kQT ? (uint32_t)kQUnit : (uint32_t)(rt + (e >= emid ? kQT : 0));
+    chunk_lr[e] = (lo < kQCap ? (uint32_t)lo : kQFar) | (row << 16);
+  }
+}
+
+// DV: value lead (chunks; indices lead by 2 DV).  NT = 2: 32 output columns per block.
+// ABL (timing experiments only, wrong results): 1 no staging loads, 2 no index loads, 4 no accumulator reads,
+// 8 no MFMAs, 16 no weight loads.
+template <int NT, int DV, int ABL = 0>
+__global__ __launch_bounds__(256) void conv_x6q_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
+    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
+    const uint32_t* __restrict__ chunk_lr, const int32_t* __restrict__ chunk_src,
+    const int32_t* __restrict__ u_rows, const int32_t* __restrict__ u_cnt, int64_t n_rows, int64_t n_tiles, int n_y,
+    float* __restrict__ out) {
+  constexpr int NC = 16 * NT, AU = NC / 4, AR = kQUnit + 1;  // accumulator rows per class (+ padding row)
+  constexpr int SR = (kQCap * 8 + 255) / 256;                // staging items per thread
+  __shared__ floatx4 xs[(kQCap + 1) * 8];
+  __shared__ floatx4 as[2 * AR * AU];
+  __shared__ int runs_s[4][32];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = wave >> 1, cls = wave & 1;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int cy = (int)(lb % n_y);
+  const int64_t unit = lb / n_y;
+  const int nks = (c_in + 31) / 32;
+
+  // this wave's chunk range: the first or second half of its tile's list
+  const int64_t tix = 2 * unit + h;
+  int64_t wb = 0, we = 0;
+  if (tix < n_tiles) {
+    const int64_t cb = tile_start[tix], ce = tile_start[tix + 1];
+    const int64_t mid = cb + (ce - cb + 1) / 2;
+    wb = cls ? mid : cb;
+    we = cls ? ce : mid;
+  }
+  const int n = (int)(we - wb);
+
+  // staging rows of this thread, the same for every k-slice (-1: slot past the unit's list)
+  static_assert(SR * 256 == kQCap * 8, "staging items must cover the list exactly");
+  int32_t srow[SR];
+#pragma unroll
+  for (int b = 0; b < SR; ++b) srow[b] = u_rows[unit * kQCap + ((tid + 256 * b) >> 3)];
+  for (int i = tid; i < 2 * AR * AU; i += 256) as[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (tid < 8) xs[kQCap * 8 + tid] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // offset runs of the wave's range: (first chunk << 8) | offset, at most K <= 27 (chunks sorted by offset)
+  int n_runs = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const int ic = i < n ? i : n - 1;
+    const int o = chunk_off[wb + ic];
+    const int op = chunk_off[wb + (ic > 0 ? ic - 1 : 0)];
+    const bool st = i < n && (i == 0 || o != op);
+    const unsigned long long m = ballot64(st);
+    const int pos = n_runs + mbcnt64(m);
+    if (st && pos < 32) runs_s[wave][pos] = (i << 8) | o;
+    n_runs += __popcll(m);
+  }
+  __syncthreads();  // runs, zeroed accumulators and zero row visible
+  const int nr_c = n_runs > 0 ? n_runs : 1;
+  const int run_l = n_runs > 0 ? runs_s[wave][lane < n_runs ? lane : n_runs - 1] : 0;
+  auto run_at = [&](int j) -> int { return __builtin_amdgcn_readlane(run_l, j < nr_c ? j : nr_c - 1); };
+  auto start_of = [&](int j) -> int { return j < n_runs ? (run_at(j) >> 8) : (1 << 22); };
+
+  struct Wt {
+    u32x4 w[NT][3];
+  };
+  auto ld_w = [&](int j, int ks, Wt& w) {
+    const int o = run_at(j) & 255;
+    if (ABL & 16) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) w.w[t][p] = u32x4{(uint32_t)(o + t), (uint32_t)p, 3u, 1u};
+      return;
+    }
+    const int ow = flip ? (K - 1 - o) : o;
+    const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * 3 * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w.w[t][p] = src[(t * 3 + p) * 64];
+  };
+  struct Val {
+    floatx4 a[2];
+    int row;
+  };
+  // last chunk a (clamped) look-ahead may read: an existing entry even for an empty range
+  const int64_t clast = we > wb ? we - 1 : (wb > 0 ? wb - 1 : 0);
+  auto ld_idx = [&](int i) -> uint32_t {  // chunk wb + i (clamped)
+    const int64_t c = wb + i < clast ? wb + i : clast;
+    if (ABL & 2) return (uint32_t)((r * 13 + i * 7) & 127) | ((uint32_t)(4 * r + (i & 3)) << 16);
+    return chunk_lr[c * MSP_CHUNK + r];
+  };
+  auto ld_val = [&](uint32_t lr, int i, int ks, Val& v) {
+    const int li = (int)(lr & 0xFFFFu);
+    const int j = li < kQCap ? li : kQCap;
+    v.a[0] = xs[xq_unit(j, 2 * q)];
+    v.a[1] = xs[xq_unit(j, 2 * q + 1)];
+    v.row = (int)(lr >> 16);
+    if (ballot64(li == (int)kQFar) != 0) {  // rows past the staged capacity: from global memory (rare)
+      const int64_t c = wb + i < clast ? wb + i : clast;
+      const int k = 32 * ks + 8 * q;
+      if (li == (int)kQFar && k < c_in) {
+        const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)chunk_src[c * MSP_CHUNK + r] * c_in + k);
+        v.a[0] = src[0];
+        v.a[1] = src[1];
+      }
+    }
+  };
+  floatx4* acc = as + cls * AR * AU;
+  // the accumulator rows of the next chunk are read right after this chunk's write (LDS operations of a wave
+  // complete in order: the read sees the write) and before the next look-ahead row reads, so waiting for them
+  // never waits for the look-ahead
+  auto rd_old = [&](int row, floatx4 (&old)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      old[t] = (ABL & 4) ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[aq_unit<AU>(row, 4 * t + q)];
+  };
+  auto run = [&](const Val& v, const Wt& w, const floatx4 (&old)[NT]) {
+    u32x4 xp[3];
+    split8(v.a[0], v.a[1], xp);
+    floatx4 c[NT];
+    if (ABL & 8) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[aq_unit<AU>(v.row, 4 * t + q)] =
+            old[t] + __builtin_bit_cast(floatx4, xp[0] ^ xp[1] ^ xp[2] ^ w.w[t][0] ^ w.w[t][1] ^ w.w[t][2]);
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w.w[t][2], xp[0], floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w.w[t][1], xp[1], c[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w.w[t][0], xp[2], c[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w.w[t][1], xp[0], c[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w.w[t][0], xp[1], c[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w.w[t][0], xp[0], c[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[aq_unit<AU>(v.row, 4 * t + q)] = old[t] + c[t];
+  };
+
+  constexpr int DI = 2 * DV;  // indices lead their values by DV chunks
+  for (int ks = 0; ks < nks; ++ks) {
+    // this slice's first indices and weights go out before the staging loads
+    uint32_t I[DV];
+#pragma unroll
+    for (int k = 0; k < DV; ++k) I[k] = ld_idx(k);
+    Wt Wc, Wn, Wm;
+    ld_w(0, ks, Wc);
+    ld_w(1, ks, Wn);
+    ld_w(2, ks, Wm);
+    if (ks > 0) __syncthreads();  // previous slice's row reads done
+    {
+      const int k0 = 32 * ks;
+      floatx4 v[SR];
+#pragma unroll
+      for (int b = 0; b < SR; ++b) {
+        const int i = tid + 256 * b;
+        const int k = k0 + 4 * (i & 7);
+        v[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (!(ABL & 1) && srow[b] >= 0 && k < c_in) v[b] = *reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + k);
+      }
+#pragma unroll
+      for (int b = 0; b < SR; ++b) {
+        const int i = tid + 256 * b;
+        if (srow[b] >= 0) xs[xq_unit(i >> 3, i & 7)] = v[b];
+      }
+    }
+    __syncthreads();
+    if (n > 0) {  // wave-uniform
+      Val S[DV];
+      floatx4 old[NT];
+#pragma unroll
+      for (int k = 0; k < DV; ++k) {
+        ld_val(I[k], k, ks, S[k]);
+        I[k] = ld_idx(DV + k);
+      }
+      rd_old(S[0].row, old);
+      int rho = 0, next_start = start_of(1);
+      for (int c = 0; c < n; c += DV) {
+#pragma unroll
+        for (int k = 0; k < DV; ++k) {
+          const int i = c + k;
+          if (i == next_start) {  // first chunk of run rho + 1
+            ++rho;
+            next_start = start_of(rho + 1);
+            Wc = Wn;
+            Wn = Wm;
+            ld_w(rho + 2, ks, Wm);
+          }
+          if (i < n) run(S[k], Wc, old);
+          rd_old(S[(k + 1) % DV].row, old);  // chunk i + 1
+          ld_val(I[k], i + DV, ks, S[k]);
+          I[k] = ld_idx(i + DI);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t row0 = unit * kQUnit;
+  for (int i = tid; i < kQUnit * AU; i += 256) {
+    const int row = i / AU, u = i % AU;
+    if (row0 + row < n_rows) {
+      const floatx4 v = as[aq_unit<AU>(row, u)] + as[AR * AU + aq_unit<AU>(row, u)];
+      *reinterpret_cast<floatx4*>(out + (row0 + row) * c_out + cy * NC + 4 * u) = v;
+    }
+  }
+}
+
 inline int local_nt(int c_out) { return (c_out / 16) % 2 == 0 ? 2 : 1; }
 
 static int g_local_wr = 2;     // row parts per block (waves = 4 x wr); msp_debug_conv_local (experiments)
@@ -1041,6 +1339,80 @@ int msp_conv_wgrad_local(const float* x, int c_in, const float* dy, int c_out, i
                                                                          (int)n_ranges, n4,
                                                                          reinterpret_cast<floatx4*>(dw));
   return check_launch("msp_conv_wgrad_local");
+}
+
+int64_t msp_chunk_local_cap(void) { return kQCap; }
+
+int msp_chunk_local(const int64_t* tile_start, int64_t n_rows, int tile_rows, int max_chunks,
+                    const int32_t* chunk_src, const uint16_t* chunk_row, int32_t* u_rows, int32_t* u_cnt,
+                    uint32_t* chunk_lr, msp_stream_t stream) {
+  MSP_REQUIRE(tile_rows == kQT, "msp_chunk_local: tile_rows must be %d (got %d)", kQT, tile_rows);
+  MSP_REQUIRE(n_rows >= 0 && n_rows < (1ll << 31), "msp_chunk_local: bad row count");
+  MSP_REQUIRE(max_chunks >= 0 && 2 * max_chunks * MSP_CHUNK <= 4096,
+              "msp_chunk_local: a tile has %d chunks (at most 128: K <= 32)", max_chunks);
+  const int64_t n_tiles = ceil_div(n_rows, kQT), n_units = ceil_div(n_tiles, 2);
+  if (n_units == 0) return MSP_OK;
+  MSP_REQUIRE(tile_start && chunk_src && chunk_row && u_rows && u_cnt && chunk_lr, "msp_chunk_local: NULL pointer");
+  hipStream_t s = as_stream(stream);
+  if (2 * max_chunks * MSP_CHUNK <= 2048)
+    chunk_local_kernel<2048><<<(unsigned)n_units, kLT, 0, s>>>(tile_start, n_tiles, chunk_src, chunk_row, u_rows,
+                                                               u_cnt, chunk_lr);
+  else
+    chunk_local_kernel<4096><<<(unsigned)n_units, kLT, 0, s>>>(tile_start, n_tiles, chunk_src, chunk_row, u_rows,
+                                                               u_cnt, chunk_lr);
+  return check_launch("msp_chunk_local");
+}
+
+static int g_chunk_dv = 2;     // value lead of conv_x6q (msp_debug_conv_chunk: experiments)
+static int g_chunk_pref = -1;  // -1: msp_conv_chunk_local_preferred's rule, 0 / 1: forced off / on
+static int g_chunk_abl = 0;    // ablation variant (timing only)
+
+int msp_debug_conv_chunk(int dv, int pref, int abl) {
+  if (dv == 2 || dv == 3 || dv == 4) g_chunk_dv = dv;
+  if (pref >= -1 && pref <= 1) g_chunk_pref = pref;
+  if (abl >= 0) g_chunk_abl = abl;
+  return MSP_OK;
+}
+
+// Measured on the headline batch's level 0 (scripts/kbench_chunk.py, profiles/r02/kbench_chunk_r02.log):
+// 0.43 / 0.74 / 0.79 ms for 32 -> 32 / 64 -> 32 / 32 -> 64 against 0.34 / 0.56 / 0.78 for the per-wave gather
+// tiles and the dense row groups -- the per-unit start-up (row list -> staged rows -> barrier, two blocks per CU)
+// costs more than the gathers it saves, so the library does not take it on its own (opt-in: force = 1 through
+// msp_debug_conv_chunk).
+int msp_conv_chunk_local_preferred(int64_t n_rows, int c_in, int c_out) {
+  const int fits = c_in % 16 == 0 && c_out % 32 == 0 && c_in <= 64 && c_out <= 64 && n_rows >= 4096;
+  return fits && g_chunk_pref == 1 ? 1 : 0;
+}
+
+int msp_conv_chunk_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                         const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                         const uint32_t* chunk_lr, const int32_t* u_rows, const int32_t* u_cnt, int64_t n_rows,
+                         float* out, void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 32 == 0,
+              "msp_conv_chunk_local: c_in must be a multiple of 16 and c_out of 32 (c_in=%d c_out=%d)", c_in, c_out);
+  MSP_REQUIRE(K >= 1 && K <= kKMax, "msp_conv_chunk_local: K must be in [1, %d] (got %d)", kKMax, K);
+  MSP_REQUIRE(tile_rows == kQT, "msp_conv_chunk_local: tile_rows must be %d (got %d)", kQT, tile_rows);
+  MSP_REQUIRE(flip >= 0 && flip <= 3, "msp_conv_chunk_local: flip must be 0..3 (got %d)", flip);
+  const size_t need = msp_conv_local_workspace_size(K, c_in, c_out);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_chunk_local: workspace too small (%zu < %zu)", ws_bytes, need);
+  const int64_t n_tiles = ceil_div(n_rows, kQT), n_units = ceil_div(n_tiles, 2);
+  if (n_units == 0) return MSP_OK;
+  hipStream_t s = as_stream(stream);
+  constexpr int NT = 2;
+  const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
+  u32x4* img = static_cast<u32x4*>(ws);
+  const int64_t lanes = (int64_t)K * n_y * nks * NT * 64;
+  split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                           (flip >> 1) & 1);
+  const unsigned grid = (unsigned)(n_units * n_y);
+#define LQ(DV, A)                                                                                              \
+  if (g_chunk_dv == DV && g_chunk_abl == A)                                                                    \
+    conv_x6q_kernel<NT, DV, A><<<grid, 256, 0, s>>>(x, c_in, img, K, flip & 1, c_out, tile_start, chunk_off,  \
+                                                    chunk_lr, chunk_src, u_rows, u_cnt, n_rows, n_tiles, n_y, out);
+  LQ(2, 0) LQ(3, 0) LQ(4, 0)
+  LQ(4, 1) LQ(4, 2) LQ(4, 4) LQ(4, 8) LQ(4, 16) LQ(4, 31)
+#undef LQ
+  return check_launch("msp_conv_chunk_local");
 }
 
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {

@@ -79,6 +79,24 @@ def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS):
                 max_u=max_u)
 
 
+CHUNK_TILE_ROWS = 64   # rulebook tiles of msp_conv_chunk_local (two per 128-row unit)
+
+
+def chunk_local_index(tiles, n, device, s):
+    """msp_chunk_local over a 64-row tile rulebook: per 128-row unit the sorted distinct input rows its chunks
+    name (first msp_chunk_local_cap of them) and per chunk entry (position in that list | row in unit << 16)."""
+    n_tiles = (n + CHUNK_TILE_ROWS - 1) // CHUNK_TILE_ROWS
+    n_units = (n_tiles + 1) // 2
+    cap = int(query("msp_chunk_local_cap"))
+    u_rows = torch.empty(max(n_units * cap, 1), dtype=torch.int32, device=device)
+    u_cnt = torch.empty(max(n_units, 1), dtype=torch.int32, device=device)
+    chunk_lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=device)  # uint32 bits
+    if n_units:
+        call("msp_chunk_local", ptr(tiles["tile_start"]), I64(n), CHUNK_TILE_ROWS, int(tiles["max_chunks"]),
+             ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), ptr(u_rows), ptr(u_cnt), ptr(chunk_lr), s)
+    return dict(tiles=tiles, u_rows=u_rows, u_cnt=u_cnt, chunk_lr=chunk_lr, n_units=n_units, cap=cap)
+
+
 class PairLists:
     """Per-offset (in, out) pair lists of an offset-major map, plus the chunk
     and block partitions used by msp_conv_pairs / msp_conv_wgrad."""
@@ -123,6 +141,7 @@ class SubmRules:
                  ptr(self.nbr), s)
         self._tiles = {}
         self._locals = {}
+        self._chunk = None
         self._dense = None
         self._map, self._n = self.nbr, V
         self.pairs = PairLists(self.nbr, K, V, dev, s)
@@ -157,6 +176,15 @@ class SubmRules:
             t = self._locals[tile_rows] = local_rulebook(self.nbr, self.K, self._n, self.nbr.device,
                                                          _lib.stream(self.nbr.device), tile_rows)
         return t
+
+    def chunk_local(self):
+        """Unit-local index of the 64-row tile rulebook (msp_chunk_local) for msp_conv_chunk_local, built on first
+        use: per 128-row unit the distinct input rows of its chunks, per chunk entry its position there."""
+        if self._chunk is None:
+            tiles = self.tiles_for(CHUNK_TILE_ROWS)
+            self._plan.append(("chunk", self._key))
+            self._chunk = chunk_local_index(tiles, self._n, self.nbr.device, _lib.stream(self.nbr.device))
+        return self._chunk
 
     def tiles_for(self, tile_rows):
         """Tile rulebook with tile_rows-row tiles, built on first use."""
@@ -367,6 +395,8 @@ class Metadata:
                 self._rules(entry[1]).dense_order()
             elif entry[0] == "local":
                 self._rules(entry[1]).local(entry[2])
+            elif entry[0] == "chunk":
+                self._rules(entry[1]).chunk_local()
 
     def tensors(self):
         """Every device tensor this metadata holds (for stream bookkeeping)."""

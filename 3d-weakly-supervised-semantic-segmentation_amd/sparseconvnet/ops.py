@@ -63,6 +63,9 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     if nbr is not None and n_rows and K <= 27 and CONV_LOCAL and \
             int(_lib.query("msp_conv_local_preferred", _lib.I64(n_rows), c_in, c_out)):
         return conv_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
+    if nbr is not None and n_rows and K <= 27 and CONV_CHUNK and \
+            int(_lib.query("msp_conv_chunk_local_preferred", _lib.I64(n_rows), c_in, c_out)):
+        return conv_chunk_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
     if nbr is not None and n_rows and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(n_rows), c_in, c_out)):
         perm, nbr_p = rules.dense_order()
         return conv_nbr(x, wt, K, flip, c_out, nbr_p, n_rows, kind, flops, perm)
@@ -106,6 +109,30 @@ def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0)
         "msp_conv_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
         ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), n_rows, ptr(out), ptr(ws), wsb, _stream(x)),
         nbytes)
+    return out[:n_rows]
+
+
+# chunk-local submanifold convolution (msp_conv_chunk_local) where the library prefers it (level 0 of m = 32)
+CONV_CHUNK = True
+
+
+def conv_chunk_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_chunk", flops=0):
+    """Submanifold convolution over the 64-row tile rulebook with each 128-row unit's distinct input rows staged
+    in LDS (SubmRules.chunk_local, msp_conv_chunk_local)."""
+    c_in = x.size(1)
+    loc = rules.chunk_local()
+    tiles = loc["tiles"]
+    out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
+    wsb = int(_lib.query("msp_conv_local_workspace_size", K, c_in, c_out))
+    ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
+    # compulsory bytes: input rows, output rows, weights, the rulebook (chunk offsets, one packed word per
+    # chunk entry, tile starts) and the units' distinct-row lists
+    nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
+        tiles["n_chunks"] * (1 + 16 * 4) + 8 * tiles["tile_start"].numel() + 4 * loc["u_rows"].numel()
+    _record(kind + "/x6q", flops, lambda: call(
+        "msp_conv_chunk_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tiles["tile_rows"],
+        ptr(tiles["tile_start"]), ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(loc["chunk_lr"]),
+        ptr(loc["u_rows"]), ptr(loc["u_cnt"]), n_rows, ptr(out), ptr(ws), wsb, _stream(x)), nbytes)
     return out[:n_rows]
 
 

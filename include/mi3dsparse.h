@@ -189,6 +189,24 @@ size_t msp_conv_local_workspace_size(int K, int c_in, int c_out);
 int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                    const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
                    int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
+/* Chunk-local submanifold convolution (the narrow large levels: msp_conv_chunk_local_preferred, level 0 of the
+ * m = 32 UNet).  Same sum as msp_conv_tile over a tile rulebook with tile_rows = 64 (K <= 27), with rows grouped
+ * in 128-row units (two rulebook tiles): msp_chunk_local lists per unit u the distinct input rows its chunks
+ * name, ascending, the first msp_chunk_local_cap() of them at u_rows[u * cap ..] and their count at u_cnt[u],
+ * and writes per chunk entry e the word chunk_lr[e] = (position in that list, 0xFFFF past the cap) | (row
+ * inside the unit, 128 for a padding slot) << 16; max_chunks = the rulebook's largest tile (<= 128).  The
+ * convolution stages each unit's listed rows in LDS once per 32 input channels and accumulates the chunks'
+ * partial products in LDS (entries past the cap read chunk_src from global memory).  c_in % 16 == 0,
+ * c_out % 32 == 0; flip and weight layouts as msp_conv_tile; workspace msp_conv_local_workspace_size. */
+int64_t msp_chunk_local_cap(void);
+int msp_chunk_local(const int64_t* tile_start, int64_t n_rows, int tile_rows, int max_chunks,
+                    const int32_t* chunk_src, const uint16_t* chunk_row, int32_t* u_rows, int32_t* u_cnt,
+                    uint32_t* chunk_lr, msp_stream_t stream);
+int msp_conv_chunk_local_preferred(int64_t n_rows, int c_in, int c_out);
+int msp_conv_chunk_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                         const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                         const uint32_t* chunk_lr, const int32_t* u_rows, const int32_t* u_cnt, int64_t n_rows,
+                         float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows);
 int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
