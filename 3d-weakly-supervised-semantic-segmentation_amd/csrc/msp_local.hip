@@ -944,6 +944,7 @@ constexpr int kQT = 64;        // rulebook tile rows (half a unit)
 constexpr int kQUnit = 128;    // rows of a unit
 constexpr int kQCap = 320;     // staged distinct rows per unit (slot kQCap: zero row)
 constexpr uint32_t kQFar = 0xFFFFu;
+constexpr int kWCap = 448;     // distinct rows per 128-row tile the weight gradient stages (msp_conv_wgrad_chunk)
 
 // staged row j (32 fp32 channels = 8 16-byte units): unit u at j*8 + (u ^ ((j >> 1) & 7)) -- the 16 distinct
 // rows j mod 16 of one ds_read_b128 lane group land on 16 distinct bank quads at a fixed u
@@ -954,17 +955,20 @@ __device__ __forceinline__ int aq_unit(int row, int u) {
   return row * AU + (u ^ ((row >> (AU == 8 ? 1 : 2)) & (AU - 1)));
 }
 
-template <int N2>
+// unit = TPU rulebook tiles of TR rows (TPU * TR = 128); list capacity cap per unit; largest count -> *mx
+template <int N2, int TPU, int TR>
 __global__ __launch_bounds__(kLT) void chunk_local_kernel(const int64_t* __restrict__ tile_start, int64_t n_tiles,
                                                           const int32_t* __restrict__ chunk_src,
-                                                          const uint16_t* __restrict__ chunk_row,
+                                                          const uint16_t* __restrict__ chunk_row, int cap,
                                                           int32_t* __restrict__ u_rows, int32_t* __restrict__ u_cnt,
-                                                          uint32_t* __restrict__ chunk_lr) {
+                                                          uint32_t* __restrict__ chunk_lr,
+                                                          unsigned long long* __restrict__ mx) {
   constexpr int PER = N2 / kLT;
+  static_assert(TPU * TR == kQUnit, "a unit is 128 rows");
   __shared__ int32_t a[N2];
   __shared__ int32_t uq[N2];
   const int64_t u = blockIdx.x;
-  const int64_t t0 = 2 * u, t1 = t0 + 1 < n_tiles ? t0 + 2 : t0 + 1;
+  const int64_t t0 = TPU * u, t1 = t0 + 1 < n_tiles ? t0 + TPU : t0 + 1;
   const int64_t e0 = tile_start[t0] * MSP_CHUNK, e1 = tile_start[t1] * MSP_CHUNK;
   const int64_t emid = tile_start[t0 + 1] * MSP_CHUNK;  // first entry of the second tile
   const int ne = (int)(e1 - e0);                        // <= N2 (host checks the largest tile)
@@ -985,12 +989,15 @@ __global__ __launch_bounds__(kLT) void chunk_local_kernel(const int64_t* __restr
     const int i = base + j;
     if (a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1])) {
       uq[off] = a[i];
-      if (off < kQCap) u_rows[u * kQCap + off] = a[i];
+      if (off < cap) u_rows[u * cap + off] = a[i];
       ++off;
     }
   }
-  for (int j = tot + threadIdx.x; j < kQCap; j += kLT) u_rows[u * kQCap + j] = -1;  // unused slots: -1
-  if (threadIdx.x == 0) u_cnt[u] = tot;
+  for (int j = tot + threadIdx.x; j < cap; j += kLT) u_rows[u * cap + j] = -1;  // unused slots: -1
+  if (threadIdx.x == 0) {
+    u_cnt[u] = tot;
+    if (mx) atomicMax(mx, (unsigned long long)tot);
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < ne; i += kLT) {
     const int64_t e = e0 + i;
@@ -1002,8 +1009,8 @@ __global__ __launch_bounds__(kLT) void chunk_local_kernel(const int64_t* __restr
       else hi = mid;
     }
     const int rt = chunk_row[e];
-    const uint32_t row = rt >= kQT ? (uint32_t)kQUnit : (uint32_t)(rt + (e >= emid ? kQT : 0));
-    chunk_lr[e] = (lo < kQCap ? (uint32_t)lo : kQFar) | (row << 16);
+    const uint32_t row = rt >= TR ? (uint32_t)kQUnit : (uint32_t)(rt + (TPU == 2 && e >= emid ? TR : 0));
+    chunk_lr[e] = (lo < cap ? (uint32_t)lo : kQFar) | (row << 16);
   }
 }
 
@@ -1219,6 +1226,256 @@ __global__ __launch_bounds__(256) void conv_x6q_kernel(
   }
 }
 
+// ---------------------------------------------------------------- chunk-local weight gradient
+// dW[o][ci][co] = sum over the rules (i, j) of offset o of x[i][ci] dy[j][co], over the 128-row tile rulebook.
+// The pair-list form (wgrad_x6_kernel) gathers x and dy per rule from L2/MALL (7-8x the compulsory bytes at
+// levels 0-1) and splits every gathered value per use; the dense tile-local form (wgrad_x6t_kernel) staged
+// the rows once but ran 32-row k-steps with ~45 % zero rows.  Here a tile's distinct x rows and its 128 dy rows
+// are staged in LDS once per 32 x 32 channel slice as three bf16 piece images ([row][32 channels], 8-byte
+// units XOR-spread by row bit 2), and the k-steps are the compacted chunks of the rulebook: two 16-rule chunks
+// of one offset per 32-deep MFMA step (an odd last chunk is paired with the zero row).  The MFMA operands
+// (A = x^T, B = dy^T: 8 consecutive rules of one channel per lane) come straight out of the gathered rows with
+// the transposing LDS read ds_read_b64_tr_b16: lane 4 qq + p of a 16-lane group names rule qq's row and its
+// channels 4p .. 4p+3, and lane i receives channel i of the group's 4 rules -- no split or permute in the loop.
+// Block = 8 waves, persistent over a contiguous range of tiles for one 32 x 32 slice; wave w owns offsets
+// w, w + 8, w + 16, w + 24 and keeps their 32 x 32 tiles in registers over the range; the next tile's rows,
+// values and rule words are in flight in registers while the current tile computes.  Per range a slab of
+// partial dW is written and the ranges are added in order (deterministic).
+constexpr int kWTile = 128;
+constexpr int kWMaxCh = 216;                   // chunks of one 128-row tile (K <= 27 offsets x 8)
+constexpr int kWXImg = (kWCap + 1) * 32;       // bf16 elements of one x piece image (+ zero row kWCap)
+constexpr int kWDImg = (kWTile + 1) * 32;      // dy piece image (+ zero row 128)
+
+// bf16 element offset of 8-byte unit v (channels 4v .. 4v+3 of the slice) of row j in a piece image
+__device__ __forceinline__ int wimg_off(int j, int v) { return j * 32 + 4 * (v ^ (((j >> 2) & 1) << 2)); }
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint2 tr_read(const uint16_t* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+  return __builtin_bit_cast(uint2, v);
+}
+
+// 4 fp32 -> three bf16x4 pieces (8 bytes each), v = p[0] + p[1] + p[2] exactly (as split8)
+__device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
+  float v[4] = {a[0], a[1], a[2], a[3]};
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t h = pk_bf16(v[2 * i], v[2 * i + 1]);
+      if (i == 0) p[s].x = h;
+      else p[s].y = h;
+      if (s < 2) {
+        v[2 * i] -= __uint_as_float(h << 16);
+        v[2 * i + 1] -= __uint_as_float(h & 0xffff0000u);
+      }
+    }
+  }
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
+    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
+    const uint32_t* __restrict__ chunk_lr, const int32_t* __restrict__ u_rows, int64_t n_rows, int64_t n_tiles,
+    int n_ranges, float* __restrict__ slab) {
+  constexpr int NTH = 64 * NW, NOW = 32 / NW;          // offsets per wave: o = wave + NW a, a < NOW
+  constexpr int XI = (kWCap * 8 + NTH - 1) / NTH;     // x staging items (row, 4 channels) per thread
+  constexpr int DI = kWTile * 8 / NTH;                // dy staging items per thread
+  constexpr int EI = (kWMaxCh * 16 + NTH - 1) / NTH;  // rule words per thread
+  static_assert(DI * NTH == kWTile * 8, "dy staging items must divide evenly");
+  __shared__ __attribute__((aligned(16))) uint16_t xim[3 * kWXImg];
+  __shared__ __attribute__((aligned(16))) uint16_t dim[3 * kWDImg];
+  __shared__ uint32_t ent[(kWMaxCh + 1) * 16];  // + one chunk: the partner read of a last odd chunk stays inside
+  __shared__ uint8_t offs[kWMaxCh];
+  __shared__ int otab[2][32];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, p4 = i16 & 3;
+  const int n_sl_o = c_out / 32, n_slices = (c_in / 32) * n_sl_o;
+  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
+  const int slice = (int)(lb % n_slices);
+  const int range = (int)(lb / n_slices);
+  const int ci0 = 32 * (slice / n_sl_o), co0 = 32 * (slice % n_sl_o);
+  const int64_t t0 = (int64_t)range * n_tiles / n_ranges, t1 = (int64_t)(range + 1) * n_tiles / n_ranges;
+
+  floatx4 acc[NOW][2][2];
+#pragma unroll
+  for (int a = 0; a < NOW; ++a)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[a][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // zero rows (never overwritten) and the padding chunk of the rule words
+  for (int i = tid; i < 3 * 32; i += NTH) {
+    xim[(i / 32) * kWXImg + kWCap * 32 + (i % 32)] = 0;
+    dim[(i / 32) * kWDImg + kWTile * 32 + (i % 32)] = 0;
+  }
+  if (tid < 16) ent[kWMaxCh * 16 + tid] = (uint32_t)kWCap | ((uint32_t)kWTile << 16);
+
+  // ---- staging registers: rows of tile t + 1 (loaded at the start of t), then its values and rule words
+  int32_t srow[XI];
+  floatx4 xv[XI], dv[DI];
+  uint32_t ev[EI];
+  int co_v = 255, s_nch = 0;
+  auto issue_rows = [&](int64_t t) {
+#pragma unroll
+    for (int b = 0; b < XI; ++b) {
+      const int it = tid + NTH * b;
+      srow[b] = it < kWCap * 8 ? u_rows[t * kWCap + (it >> 3)] : -1;
+    }
+  };
+  auto issue_vals = [&](int64_t t) {  // values of tile t (rows in srow) and its rule words
+#pragma unroll
+    for (int b = 0; b < XI; ++b) {
+      const int u = (tid + NTH * b) & 7;
+      xv[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (srow[b] >= 0) xv[b] = *reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + ci0 + 4 * u);
+    }
+#pragma unroll
+    for (int b = 0; b < DI; ++b) {
+      const int it = tid + NTH * b, u = it & 7;
+      const int64_t row = t * kWTile + (it >> 3);
+      dv[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (row < n_rows) dv[b] = *reinterpret_cast<const floatx4*>(dy + row * c_out + co0 + 4 * u);
+    }
+    const int64_t c0 = tile_start[t];
+    s_nch = (int)(tile_start[t + 1] - c0);
+#pragma unroll
+    for (int b = 0; b < EI; ++b) {
+      const int e = tid + NTH * b;
+      ev[b] = e < s_nch * 16 ? chunk_lr[c0 * 16 + e] : 0u;
+    }
+    co_v = tid < s_nch ? chunk_off[c0 + tid] : 255;
+  };
+  auto store = [&]() {  // the staged tile into LDS (two barriers: offset table)
+#pragma unroll
+    for (int b = 0; b < XI; ++b) {
+      if (srow[b] >= 0) {
+        const int it = tid + NTH * b;
+        uint2 pc[3];
+        split4(xv[b], pc);
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+          *reinterpret_cast<uint2*>(xim + pp * kWXImg + wimg_off(it >> 3, it & 7)) = pc[pp];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < DI; ++b) {
+      const int it = tid + NTH * b;
+      uint2 pc[3];
+      split4(dv[b], pc);
+#pragma unroll
+      for (int pp = 0; pp < 3; ++pp)
+        *reinterpret_cast<uint2*>(dim + pp * kWDImg + wimg_off(it >> 3, it & 7)) = pc[pp];
+    }
+#pragma unroll
+    for (int b = 0; b < EI; ++b) {
+      const int e = tid + NTH * b;
+      if (e < s_nch * 16) ent[e] = ev[b];
+    }
+    if (tid < s_nch) offs[tid] = (uint8_t)co_v;
+    if (tid < 64) otab[tid >> 5][tid & 31] = 0;
+    __syncthreads();
+    if (tid < s_nch) {
+      const int o = offs[tid];
+      if (tid == 0 || offs[tid - 1] != o) otab[0][o] = tid;
+      if (tid == s_nch - 1 || offs[tid + 1] != o) otab[1][o] = tid + 1;
+    }
+    __syncthreads();
+  };
+
+  // ---- one 32-rule step over the two chunks cA, cA + 1 (the second only if hasB): the B fragments (dy) of
+  // both 16-column halves, then per 16-row half of x its A fragments and 12 MFMAs (36 fragment registers live)
+  auto rows_of = [&](int cA, bool hasB, int (&xr)[2], int (&dr)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kp = 8 * g + 4 * h + qq, cs = kp >> 4;
+      uint32_t w = ent[(cA + cs) * 16 + (kp & 15)];
+      if (cs == 1 && !hasB) w = (uint32_t)kWCap | ((uint32_t)kWTile << 16);
+      const int ls = (int)(w & 0xFFFFu);
+      xr[h] = ls < kWCap ? ls : kWCap;
+      dr[h] = (int)(w >> 16);
+    }
+  };
+  auto frag = [&](const uint16_t* img, const int (&rr)[2], int v) {
+    const uint2 lo = tr_read(img + wimg_off(rr[0], v));
+    const uint2 hi = tr_read(img + wimg_off(rr[1], v));
+    return u32x4{lo.x, lo.y, hi.x, hi.y};
+  };
+  auto kstep = [&](int cA, bool hasB, floatx4 (&ac)[2][2]) {
+    int xr[2], dr[2];
+    rows_of(cA, hasB, xr, dr);
+    u32x4 fb[2][3], fa[3];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int pp = 0; pp < 3; ++pp) fb[sb][pp] = frag(dim + pp * kWDImg, dr, 4 * sb + p4);
+#pragma unroll
+    for (int sa = 0; sa < 2; ++sa) {
+#pragma unroll
+      for (int pp = 0; pp < 3; ++pp) fa[pp] = frag(xim + pp * kWXImg, xr, 4 * sa + p4);
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        floatx4 c = mfma_bf16(fa[2], fb[sb][0], floatx4{0.f, 0.f, 0.f, 0.f});
+        c = mfma_bf16(fa[1], fb[sb][1], c);
+        c = mfma_bf16(fa[0], fb[sb][2], c);
+        c = mfma_bf16(fa[1], fb[sb][0], c);
+        c = mfma_bf16(fa[0], fb[sb][1], c);
+        ac[sa][sb] += mfma_bf16(fa[0], fb[sb][0], c);
+      }
+    }
+  };
+
+  if (t0 < t1) {
+    issue_rows(t0);
+    issue_vals(t0);
+    store();
+    for (int64_t t = t0; t < t1; ++t) {
+      const bool more = t + 1 < t1;
+      if (more) issue_rows(t + 1);
+      // this wave's offsets: chunk range and 32-rule steps, flattened over the (up to) four offsets
+      int first[NOW + 1], endc[NOW + 1], S[NOW + 1];
+      S[0] = 0;
+#pragma unroll
+      for (int a = 0; a < NOW; ++a) {
+        const int o = wave + NW * a;
+        first[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[0][o]) : 0;
+        endc[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[1][o]) : 0;
+        S[a + 1] = S[a] + (endc[a] - first[a] + 1) / 2;
+      }
+      const int n_st = S[NOW];
+      const int s_vals = n_st / 2;  // the next tile's values go out half-way through (their rows have landed)
+      int s = 0;
+#pragma unroll
+      for (int a = 0; a < NOW; ++a) {  // constant slot index: acc[a] stays in registers
+        for (int c = first[a]; c < endc[a]; c += 2, ++s) {
+          if (s == s_vals && more) issue_vals(t + 1);
+          kstep(c, c + 1 < endc[a], acc[a]);
+        }
+      }
+      if (n_st == 0 && more) issue_vals(t + 1);
+      __syncthreads();  // reads of tile t done
+      if (more) store();
+    }
+  }
+  // partial dW of this range: slab[range][o][ci][co]
+  float* sb = slab + (int64_t)range * K * c_in * c_out;
+#pragma unroll
+  for (int a = 0; a < NOW; ++a) {
+    const int o = wave + NW * a;
+    if (o >= K) break;
+#pragma unroll
+    for (int sa = 0; sa < 2; ++sa)
+#pragma unroll
+      for (int sbb = 0; sbb < 2; ++sbb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          sb[((int64_t)o * c_in + ci0 + 16 * sa + 4 * g + jj) * c_out + co0 + 16 * sbb + i16] = acc[a][sa][sbb][jj];
+  }
+}
+
 inline int local_nt(int c_out) { return (c_out / 16) % 2 == 0 ? 2 : 1; }
 
 static int g_local_wr = 2;     // row parts per block (waves = 4 x wr); msp_debug_conv_local (experiments)
@@ -1341,25 +1598,36 @@ int msp_conv_wgrad_local(const float* x, int c_in, const float* dy, int c_out, i
   return check_launch("msp_conv_wgrad_local");
 }
 
-int64_t msp_chunk_local_cap(void) { return kQCap; }
+int64_t msp_chunk_local_cap(int tile_rows) { return tile_rows == kQT ? kQCap : kWCap; }
 
 int msp_chunk_local(const int64_t* tile_start, int64_t n_rows, int tile_rows, int max_chunks,
                     const int32_t* chunk_src, const uint16_t* chunk_row, int32_t* u_rows, int32_t* u_cnt,
-                    uint32_t* chunk_lr, msp_stream_t stream) {
-  MSP_REQUIRE(tile_rows == kQT, "msp_chunk_local: tile_rows must be %d (got %d)", kQT, tile_rows);
+                    uint32_t* chunk_lr, int64_t* max_count, msp_stream_t stream) {
+  MSP_REQUIRE(tile_rows == 64 || tile_rows == 128, "msp_chunk_local: tile_rows must be 64 or 128 (got %d)",
+              tile_rows);
   MSP_REQUIRE(n_rows >= 0 && n_rows < (1ll << 31), "msp_chunk_local: bad row count");
-  MSP_REQUIRE(max_chunks >= 0 && 2 * max_chunks * MSP_CHUNK <= 4096,
-              "msp_chunk_local: a tile has %d chunks (at most 128: K <= 32)", max_chunks);
-  const int64_t n_tiles = ceil_div(n_rows, kQT), n_units = ceil_div(n_tiles, 2);
+  MSP_REQUIRE(max_chunks >= 0 && (kQUnit / tile_rows) * max_chunks * MSP_CHUNK <= 4096,
+              "msp_chunk_local: a tile has %d chunks (K <= 32 allows at most %d)", max_chunks,
+              4096 / MSP_CHUNK / (kQUnit / tile_rows));
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows), tpu = kQUnit / tile_rows, n_units = ceil_div(n_tiles, tpu);
+  hipStream_t s = as_stream(stream);
+  if (max_count) MSP_HIP(hipMemsetAsync(max_count, 0, sizeof(int64_t), s), "msp_chunk_local");
   if (n_units == 0) return MSP_OK;
   MSP_REQUIRE(tile_start && chunk_src && chunk_row && u_rows && u_cnt && chunk_lr, "msp_chunk_local: NULL pointer");
-  hipStream_t s = as_stream(stream);
-  if (2 * max_chunks * MSP_CHUNK <= 2048)
-    chunk_local_kernel<2048><<<(unsigned)n_units, kLT, 0, s>>>(tile_start, n_tiles, chunk_src, chunk_row, u_rows,
-                                                               u_cnt, chunk_lr);
-  else
-    chunk_local_kernel<4096><<<(unsigned)n_units, kLT, 0, s>>>(tile_start, n_tiles, chunk_src, chunk_row, u_rows,
-                                                               u_cnt, chunk_lr);
+  const int cap = (int)msp_chunk_local_cap(tile_rows);
+  auto* mx = reinterpret_cast<unsigned long long*>(max_count);
+  const bool small = tpu * max_chunks * MSP_CHUNK <= 2048;
+#define CL(N2, TPU, TR)                                                                                         \
+  chunk_local_kernel<N2, TPU, TR><<<(unsigned)n_units, kLT, 0, s>>>(tile_start, n_tiles, chunk_src, chunk_row, cap, \
+                                                                    u_rows, u_cnt, chunk_lr, mx)
+  if (tile_rows == 64) {
+    if (small) CL(2048, 2, 64);
+    else CL(4096, 2, 64);
+  } else {
+    if (small) CL(2048, 1, 128);
+    else CL(4096, 1, 128);
+  }
+#undef CL
   return check_launch("msp_chunk_local");
 }
 
@@ -1413,6 +1681,59 @@ int msp_conv_chunk_local(const float* x, int c_in, const float* wt, int K, int f
   LQ(4, 1) LQ(4, 2) LQ(4, 4) LQ(4, 8) LQ(4, 16) LQ(4, 31)
 #undef LQ
   return check_launch("msp_conv_chunk_local");
+}
+
+static int g_wchunk_nw = 8;  // waves per block of wgrad_x6c (8 or 16; msp_debug_wgrad_chunk: experiments)
+
+int msp_debug_wgrad_chunk(int nw) {
+  if (nw == 8 || nw == 16) g_wchunk_nw = nw;
+  return MSP_OK;
+}
+
+int msp_wgrad_chunk_ok(int64_t n_rows, int K, int c_in, int c_out) {
+  return (n_rows > 0 && K >= 1 && K <= 27 && c_in % 32 == 0 && c_out % 32 == 0) ? 1 : 0;
+}
+
+// Measured against the pair lists on the headline batch (scripts/kbench_wgrad_local.py,
+// profiles/r02/kbench_wgrad_chunk_r02.log): 0.59 vs 0.65 ms at level 1 64 -> 64, 0.40 vs 0.46 at level 2,
+// 0.59 vs 0.68 at level 0 32 -> 64; behind at level 0's 32 and 64 -> 32 (0.36 / 0.60 vs 0.35 / 0.55 ms); the
+// few-tile levels (< 2^14 rows) are unmeasured and stay on the pair lists.
+int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out) {
+  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && c_out >= 64 && n_rows >= (1 << 14) ? 1 : 0;
+}
+
+int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out) {
+  const int64_t n_tiles = ceil_div(n_rows > 0 ? n_rows : 1, kWTile);
+  const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
+  int64_t r = cu_count() / (slices > 0 ? slices : 1);
+  if (r < 1) r = 1;
+  return r < n_tiles ? r : n_tiles;
+}
+
+int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
+                         const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
+                         const int32_t* u_rows, int64_t n_rows, int64_t n_ranges, float* slab, float* dw,
+                         msp_stream_t stream) {
+  MSP_REQUIRE(msp_wgrad_chunk_ok(n_rows, K, c_in, c_out), "msp_conv_wgrad_chunk: needs K <= 27 and channels in "
+              "multiples of 32 (K=%d c_in=%d c_out=%d n=%lld)", K, c_in, c_out, (long long)n_rows);
+  MSP_REQUIRE(tile_rows == kWTile, "msp_conv_wgrad_chunk: tile_rows must be %d (got %d)", kWTile, tile_rows);
+  MSP_REQUIRE(n_ranges >= 1, "msp_conv_wgrad_chunk: n_ranges must be >= 1");
+  hipStream_t s = as_stream(stream);
+  const int64_t n_tiles = ceil_div(n_rows, kWTile);
+  const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
+  if (g_wchunk_nw == 16)
+    wgrad_x6c_kernel<16><<<(unsigned)(n_ranges * slices), 1024, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
+                                                                        chunk_lr, u_rows, n_rows, n_tiles,
+                                                                        (int)n_ranges, slab);
+  else
+    wgrad_x6c_kernel<8><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
+                                                                      chunk_lr, u_rows, n_rows, n_tiles,
+                                                                      (int)n_ranges, slab);
+  const int64_t n4 = (int64_t)K * c_in * c_out / 4;
+  wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
+                                                                         (int)n_ranges, n4,
+                                                                         reinterpret_cast<floatx4*>(dw));
+  return check_launch("msp_conv_wgrad_chunk");
 }
 
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {

@@ -37,9 +37,13 @@ PROTOTYPES = {
     "msp_tile_local_workspace_size": (SZ, [I64, I]),
     "msp_tile_local": (I, [P, I, I64, I, P, P, I64, P, P, P, SZ, P]),
     "msp_conv_local_preferred": (I, [I64, I, I]),
-    "msp_chunk_local_cap": (I64, []),
-    "msp_chunk_local": (I, [P, I64, I, I, P, P, P, P, P, P]),
+    "msp_chunk_local_cap": (I64, [I]),
+    "msp_chunk_local": (I, [P, I64, I, I, P, P, P, P, P, P, P]),
     "msp_conv_chunk_local_preferred": (I, [I64, I, I]),
+    "msp_wgrad_chunk_ok": (I, [I64, I, I, I]),
+    "msp_wgrad_chunk_preferred": (I, [I64, I, I, I]),
+    "msp_wgrad_chunk_ranges": (I64, [I64, I, I]),
+    "msp_conv_wgrad_chunk": (I, [P, I, P, I, I, I, P, P, P, P, I64, I64, P, P, P]),
     "msp_conv_chunk_local": (I, [P, I, P, I, I, I, I, P, P, P, P, P, P, I64, P, P, SZ, P]),
     "msp_wgrad_local_ok": (I, [I64, I, I, I]),
     "msp_wgrad_local_ranges": (I64, [I64, I, I]),

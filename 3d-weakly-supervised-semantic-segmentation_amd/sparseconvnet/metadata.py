@@ -82,19 +82,26 @@ def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS):
 CHUNK_TILE_ROWS = 64   # rulebook tiles of msp_conv_chunk_local (two per 128-row unit)
 
 
-def chunk_local_index(tiles, n, device, s):
-    """msp_chunk_local over a 64-row tile rulebook: per 128-row unit the sorted distinct input rows its chunks
-    name (first msp_chunk_local_cap of them) and per chunk entry (position in that list | row in unit << 16)."""
-    n_tiles = (n + CHUNK_TILE_ROWS - 1) // CHUNK_TILE_ROWS
-    n_units = (n_tiles + 1) // 2
-    cap = int(query("msp_chunk_local_cap"))
+def chunk_local_index(tiles, n, device, s, with_max=False):
+    """msp_chunk_local over a tile rulebook (64-row tiles: two per 128-row unit, the convolution's index; 128-row
+    tiles: one per unit, the weight gradient's): per unit the sorted distinct input rows its chunks name (first
+    msp_chunk_local_cap of them, -1 after) and per chunk entry (position in that list | row in unit << 16).
+    with_max: also the largest unit's count (one host read)."""
+    tr = int(tiles["tile_rows"])
+    n_tiles = (n + tr - 1) // tr
+    n_units = (n_tiles + 128 // tr - 1) // (128 // tr)
+    cap = int(query("msp_chunk_local_cap", tr))
     u_rows = torch.empty(max(n_units * cap, 1), dtype=torch.int32, device=device)
     u_cnt = torch.empty(max(n_units, 1), dtype=torch.int32, device=device)
     chunk_lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=device)  # uint32 bits
+    mx = torch.zeros(1, dtype=torch.int64, device=device) if with_max else None
     if n_units:
-        call("msp_chunk_local", ptr(tiles["tile_start"]), I64(n), CHUNK_TILE_ROWS, int(tiles["max_chunks"]),
-             ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), ptr(u_rows), ptr(u_cnt), ptr(chunk_lr), s)
-    return dict(tiles=tiles, u_rows=u_rows, u_cnt=u_cnt, chunk_lr=chunk_lr, n_units=n_units, cap=cap)
+        call("msp_chunk_local", ptr(tiles["tile_start"]), I64(n), tr, int(tiles["max_chunks"]),
+             ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), ptr(u_rows), ptr(u_cnt), ptr(chunk_lr), ptr(mx), s)
+    out = dict(tiles=tiles, u_rows=u_rows, u_cnt=u_cnt, chunk_lr=chunk_lr, n_units=n_units, cap=cap)
+    if with_max:
+        out["max_u"] = int(mx.item()) if n_units else 0
+    return out
 
 
 class PairLists:
@@ -142,6 +149,7 @@ class SubmRules:
         self._tiles = {}
         self._locals = {}
         self._chunk = None
+        self._wchunk = None
         self._dense = None
         self._map, self._n = self.nbr, V
         self.pairs = PairLists(self.nbr, K, V, dev, s)
@@ -185,6 +193,17 @@ class SubmRules:
             self._plan.append(("chunk", self._key))
             self._chunk = chunk_local_index(tiles, self._n, self.nbr.device, _lib.stream(self.nbr.device))
         return self._chunk
+
+    def wgrad_index(self):
+        """Per 128-row tile of the 128-row tile rulebook: the distinct input rows and each chunk entry's
+        position among them (msp_chunk_local), for msp_conv_wgrad_chunk; built on first use.  None when a tile
+        names more distinct rows than the kernel stages (msp_chunk_local_cap(128)): the pair lists serve then."""
+        if self._wchunk is None:
+            tiles = self.tiles_for(128)
+            self._plan.append(("wchunk", self._key))
+            idx = chunk_local_index(tiles, self._n, self.nbr.device, _lib.stream(self.nbr.device), with_max=True)
+            self._wchunk = idx if idx["max_u"] <= idx["cap"] else False
+        return self._wchunk or None
 
     def tiles_for(self, tile_rows):
         """Tile rulebook with tile_rows-row tiles, built on first use."""
@@ -397,6 +416,8 @@ class Metadata:
                 self._rules(entry[1]).local(entry[2])
             elif entry[0] == "chunk":
                 self._rules(entry[1]).chunk_local()
+            elif entry[0] == "wchunk":
+                self._rules(entry[1]).wgrad_index()
 
     def tensors(self):
         """Every device tensor this metadata holds (for stream bookkeeping)."""

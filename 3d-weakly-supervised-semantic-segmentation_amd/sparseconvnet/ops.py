@@ -242,6 +242,37 @@ def conv_wgrad_local(x, dy, rules, K, kind="wgrad", flops=None):
     return dw
 
 
+# chunk-local weight gradient (msp_conv_wgrad_chunk) for submanifold convolutions where the library prefers it
+WGRAD_CHUNK = True
+
+
+def conv_wgrad_chunk(x, dy, rules, K, kind="wgrad", flops=None):
+    """Submanifold weight gradient over the 128-row tile rulebook (SubmRules.wgrad_index): per tile the distinct
+    x rows and the 128 dy rows staged in LDS once per 32 x 32 channel slice, the compacted chunks as MFMA
+    k-steps (msp_conv_wgrad_chunk); partial sums per tile range added in order.  None when a tile names more
+    distinct rows than the kernel stages."""
+    idx = rules.wgrad_index()
+    if idx is None:
+        return None
+    c_in, c_out = x.size(1), dy.size(1)
+    n = dy.size(0)
+    tiles = idx["tiles"]
+    ranges = int(_lib.query("msp_wgrad_chunk_ranges", _lib.I64(n), c_in, c_out))
+    dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
+    slab = torch.empty((ranges, K, c_in, c_out), dtype=torch.float32, device=x.device)
+    if flops is None:
+        flops = 2.0 * rules.n_rules * c_in * c_out
+    # compulsory bytes: x and dy rows, the rulebook (one packed word per chunk entry, chunk offsets, tile
+    # starts), the tiles' distinct-row lists, dW
+    nbytes = 4 * (x.size(0) * c_in + n * c_out + K * c_in * c_out) + \
+        tiles["n_chunks"] * (1 + 16 * 4) + 8 * tiles["tile_start"].numel() + 4 * idx["u_rows"].numel()
+    _record(kind + "/x6c", flops, lambda: call(
+        "msp_conv_wgrad_chunk", ptr(x), c_in, ptr(dy), c_out, K, tiles["tile_rows"], ptr(tiles["tile_start"]),
+        ptr(tiles["chunk_off"]), ptr(idx["chunk_lr"]), ptr(idx["u_rows"]), n, ranges, ptr(slab), ptr(dw),
+        _stream(x)), nbytes)
+    return dw
+
+
 def conv_nbr(x, wt, K, flip, c_out, nbr, n_rows, kind="conv_nbr", flops=0, perm=None):
     """Dense row-group form of the submanifold convolution straight from the
     neighbour map nbr[K][n_rows] (msp_conv_nbr: no tile rulebook); with perm,
@@ -288,7 +319,12 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             p = rules.pairs
             V = xp.size(0)
-            if WGRAD_LOCAL and int(_lib.query("msp_wgrad_local_ok", _lib.I64(V), K, cin_p, cout_p)):
+            dwp = None
+            if WGRAD_CHUNK and int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)):
+                dwp = conv_wgrad_chunk(xp, g, rules, K, flops=2.0 * p.total * cin * cout)
+            if dwp is not None:
+                pass
+            elif WGRAD_LOCAL and int(_lib.query("msp_wgrad_local_ok", _lib.I64(V), K, cin_p, cout_p)):
                 dwp = conv_wgrad_local(xp, g, rules, K, flops=2.0 * p.total * cin * cout)
             elif int(_lib.query("msp_wgrad_band_ok", _lib.I64(V), K, cin_p, cout_p)):
                 dwp = conv_wgrad_band(xp, g, p, K, V)  # rows staged in LDS per band

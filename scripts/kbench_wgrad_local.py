@@ -1,6 +1,8 @@
-"""Micro-benchmark: the tile-local weight gradient (msp_conv_wgrad_local) against the pair-list form
-(msp_conv_wgrad) on the headline batch's real submanifold rulebooks, with the max error of each against an
-fp64 evaluation (relative to max |dW|).  Usage: python scripts/kbench_wgrad_local.py (env LEVELS, M)."""
+"""Micro-benchmark: the tile-local weight gradients (msp_conv_wgrad_local: dense 32-row steps;
+msp_conv_wgrad_chunk: compacted chunks + transposing LDS reads) against the pair-list form (msp_conv_wgrad) on
+the headline batch's real submanifold rulebooks, with the max error of each against an fp64 evaluation
+(relative to max |dW|), and the chunk index build time.  Usage: python scripts/kbench_wgrad_local.py (env LEVELS,
+M, FORMS = comma list of pairs,local,chunk)."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
 import __graft_entry__ as g_; g_.add_path()
@@ -8,7 +10,9 @@ import torch
 import sparseconvnet as scn
 from sparseconvnet import _lib, ops
 from wsss3d.synthetic import make_batch
-_lib.load()
+lib = _lib.load()
+import ctypes
+lib.msp_debug_wgrad_chunk.argtypes = [ctypes.c_int]
 b = make_batch(8, 50, seed=1)
 t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
 meta = t.metadata
@@ -35,10 +39,17 @@ for L, size in enumerate(sizes):
     lvl = meta.level(size)
     rules = lvl.subm_rules(3)
     V = lvl.n
-    rules.local()
-    print(f"L{L} V={V} R={rules.n_rules}", flush=True)
+    forms = os.environ.get("FORMS", "pairs,chunk").split(",")
+    if "local" in forms:
+        rules.local()
+    tiles = rules.tiles_for(128)
+    ms_idx = timeit(lambda: scn.metadata.chunk_local_index(tiles, V, rules.nbr.device, _lib.stream()), 3)
+    idx = rules.wgrad_index()
+    print(f"L{L} V={V} R={rules.n_rules} chunks(128)={tiles['n_chunks']} max distinct/tile "
+          f"{'over cap' if idx is None else int(idx['u_cnt'][:idx['n_units']].max())} index build {ms_idx:.3f} ms",
+          flush=True)
     c = int(os.environ.get("M", "32")) * (L + 1)
-    for cin, cout in ((c, c), (2 * c, c)):
+    for cin, cout in ((c, c), (2 * c, c), (c, 2 * c)):
         torch.manual_seed(L)
         x = torch.randn(V, cin, device="cuda")
         dy = torch.randn(V, cout, device="cuda")
@@ -52,8 +63,15 @@ for L, size in enumerate(sizes):
             ref[o] = x64[nb[o][m]].t() @ dy64[m]
         scale = ref.abs().max().item()
         res = []
-        for name, f in (("pairs", lambda: ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)),
-                        ("local", lambda: ops.conv_wgrad_local(x, dy, rules, 27))):
+        fns = {"pairs": lambda: ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27),
+               "local": lambda: ops.conv_wgrad_local(x, dy, rules, 27),
+               "chunk": lambda: ops.conv_wgrad_chunk(x, dy, rules, 27)}
+        for nw in (8, 16):
+            def fnw(nw=nw):
+                lib.msp_debug_wgrad_chunk(nw)
+                return ops.conv_wgrad_chunk(x, dy, rules, 27)
+            fns[f"chunk{nw}"] = fnw
+        for name, f in ((k, fns[k]) for k in forms):
             ms = timeit(f)
             err = (f().double() - ref).abs().max().item() / scale
             res.append(f"{name} {ms:6.3f} ms {flops / ms / 1e9:5.1f} TF err {err:.1e}")

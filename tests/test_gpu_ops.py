@@ -753,6 +753,32 @@ def test_conv_chunk_local_accuracy(cin, cout, flip):
         assert bool((rows[u, 1:k] > rows[u, :k - 1]).all()) and bool((rows[u, k:] == -1).all())
 
 
+@pytest.mark.parametrize("cin,cout", [(32, 32), (64, 32), (32, 64), (96, 64)])
+def test_conv_wgrad_chunk_accuracy(cin, cout):
+    """msp_conv_wgrad_chunk (chunk-compacted tile-local weight gradient, transposing LDS reads, split-bf16
+    MFMA) against an fp64 evaluation of dW[o] = sum_i x[nbr(i, o)]^T dy[i] and against the pair-list form."""
+    from sparseconvnet import ops
+    torch.manual_seed(cin + 5 * cout)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    rules = t.metadata.level(64).subm_rules(3)
+    V = t.metadata.level(64).n
+    x = torch.randn(V, cin, device=DEV)
+    dy = torch.randn(V, cout, device=DEV)
+    dw = ops.conv_wgrad_chunk(x, dy, rules, 27)
+    assert dw is not None
+    nb = rules.nbr.long()
+    ref = torch.empty(27, cin, cout, dtype=torch.float64, device=DEV)
+    for o in range(27):
+        m = nb[o] >= 0
+        ref[o] = x[nb[o][m]].double().t() @ dy[m].double()
+    scale = ref.abs().max().item()
+    assert (dw.double() - ref).abs().max().item() / scale < 1e-6
+    p = rules.pairs
+    dwp = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
+    assert (dw - dwp).abs().max().item() / scale < 2e-6
+
+
 def test_conv_chunk_local_overflow_rows():
     """Units naming more distinct input rows than the LDS stage holds (320): a random map over a large input
     sends most rows down the global-memory path; results still match fp64."""
