@@ -1014,6 +1014,36 @@ __global__ __launch_bounds__(kLT) void chunk_local_kernel(const int64_t* __restr
   }
 }
 
+// Weight-gradient index from the tile-local rulebook (msp_tile_local, 128-row tiles): the tile's sorted
+// distinct input rows are already listed there, so each chunk entry of the 128-row tile rulebook only needs its
+// position in that list (binary search; rows past the list's staged capacity are excluded on the host).
+__global__ __launch_bounds__(kLT) void chunk_lidx_kernel(const int64_t* __restrict__ tile_start,
+                                                         const int32_t* __restrict__ chunk_src,
+                                                         const uint16_t* __restrict__ chunk_row,
+                                                         const int64_t* __restrict__ u_start,
+                                                         const int32_t* __restrict__ u_rows,
+                                                         uint32_t* __restrict__ chunk_lr) {
+  __shared__ int32_t uq[kWCap];
+  const int64_t t = blockIdx.x;
+  const int64_t u0 = u_start[t];
+  const int U = (int)(u_start[t + 1] - u0);
+  const int Us = U < kWCap ? U : kWCap;
+  for (int i = threadIdx.x; i < Us; i += kLT) uq[i] = u_rows[u0 + i];
+  __syncthreads();
+  const int64_t e0 = tile_start[t] * MSP_CHUNK, e1 = tile_start[t + 1] * MSP_CHUNK;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kLT) {
+    const int32_t v = chunk_src[e];
+    int lo = 0, hi = Us;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (uq[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    const int rt = chunk_row[e];
+    chunk_lr[e] = (uint32_t)(lo < Us ? lo : kQFar) | ((uint32_t)(rt >= kQUnit ? kQUnit : rt) << 16);
+  }
+}
+
 // DV: value lead (chunks; indices lead by 2 DV).  NT = 2: 32 output columns per block.
 // ABL (timing experiments only, wrong results): 1 no staging loads, 2 no index loads, 4 no accumulator reads,
 // 8 no MFMAs, 16 no weight loads.
@@ -1273,12 +1303,14 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
   }
 }
 
-template <int NW>
+// ABL (timing experiments only, wrong results): 1 no MFMAs, 2 no transposing reads, 4 no value loads,
+// 8 no staging stores
+template <int NW, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
-    const uint32_t* __restrict__ chunk_lr, const int32_t* __restrict__ u_rows, int64_t n_rows, int64_t n_tiles,
-    int n_ranges, float* __restrict__ slab) {
+    const uint32_t* __restrict__ chunk_lr, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
+    int64_t n_rows, int64_t n_tiles, int n_ranges, float* __restrict__ slab) {
   constexpr int NTH = 64 * NW, NOW = 32 / NW;          // offsets per wave: o = wave + NW a, a < NOW
   constexpr int XI = (kWCap * 8 + NTH - 1) / NTH;     // x staging items (row, 4 channels) per thread
   constexpr int DI = kWTile * 8 / NTH;                // dy staging items per thread
@@ -1319,11 +1351,13 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   floatx4 xv[XI], dv[DI];
   uint32_t ev[EI];
   int co_v = 255, s_nch = 0;
-  auto issue_rows = [&](int64_t t) {
+  auto issue_rows = [&](int64_t t) {  // the tile's distinct rows (<= kWCap: checked on the host)
+    const int64_t u0 = u_start[t];
+    const int nu = (int)(u_start[t + 1] - u0);
 #pragma unroll
     for (int b = 0; b < XI; ++b) {
       const int it = tid + NTH * b;
-      srow[b] = it < kWCap * 8 ? u_rows[t * kWCap + (it >> 3)] : -1;
+      srow[b] = it < nu * 8 ? u_rows[u0 + (it >> 3)] : -1;
     }
   };
   auto issue_vals = [&](int64_t t) {  // values of tile t (rows in srow) and its rule words
@@ -1331,14 +1365,14 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     for (int b = 0; b < XI; ++b) {
       const int u = (tid + NTH * b) & 7;
       xv[b] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (srow[b] >= 0) xv[b] = *reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + ci0 + 4 * u);
+      if (!(ABL & 4) && srow[b] >= 0) xv[b] = *reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + ci0 + 4 * u);
     }
 #pragma unroll
     for (int b = 0; b < DI; ++b) {
       const int it = tid + NTH * b, u = it & 7;
       const int64_t row = t * kWTile + (it >> 3);
       dv[b] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (row < n_rows) dv[b] = *reinterpret_cast<const floatx4*>(dy + row * c_out + co0 + 4 * u);
+      if (!(ABL & 4) && row < n_rows) dv[b] = *reinterpret_cast<const floatx4*>(dy + row * c_out + co0 + 4 * u);
     }
     const int64_t c0 = tile_start[t];
     s_nch = (int)(tile_start[t + 1] - c0);
@@ -1352,7 +1386,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   auto store = [&]() {  // the staged tile into LDS (two barriers: offset table)
 #pragma unroll
     for (int b = 0; b < XI; ++b) {
-      if (srow[b] >= 0) {
+      if (!(ABL & 8) && srow[b] >= 0) {
         const int it = tid + NTH * b;
         uint2 pc[3];
         split4(xv[b], pc);
@@ -1363,6 +1397,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     }
 #pragma unroll
     for (int b = 0; b < DI; ++b) {
+      if (ABL & 8) break;
       const int it = tid + NTH * b;
       uint2 pc[3];
       split4(dv[b], pc);
@@ -1400,6 +1435,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     }
   };
   auto frag = [&](const uint16_t* img, const int (&rr)[2], int v) {
+    if (ABL & 2) return u32x4{(uint32_t)rr[0], (uint32_t)rr[1], (uint32_t)v, 7u};
     const uint2 lo = tr_read(img + wimg_off(rr[0], v));
     const uint2 hi = tr_read(img + wimg_off(rr[1], v));
     return u32x4{lo.x, lo.y, hi.x, hi.y};
@@ -1418,6 +1454,10 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       for (int pp = 0; pp < 3; ++pp) fa[pp] = frag(xim + pp * kWXImg, xr, 4 * sa + p4);
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
+        if (ABL & 1) {
+          ac[sa][sb] += __builtin_bit_cast(floatx4, fa[0] ^ fa[1] ^ fa[2] ^ fb[sb][0] ^ fb[sb][1] ^ fb[sb][2]);
+          continue;
+        }
         floatx4 c = mfma_bf16(fa[2], fb[sb][0], floatx4{0.f, 0.f, 0.f, 0.f});
         c = mfma_bf16(fa[1], fb[sb][1], c);
         c = mfma_bf16(fa[0], fb[sb][2], c);
@@ -1684,9 +1724,11 @@ int msp_conv_chunk_local(const float* x, int c_in, const float* wt, int K, int f
 }
 
 static int g_wchunk_nw = 8;  // waves per block of wgrad_x6c (8 or 16; msp_debug_wgrad_chunk: experiments)
+static int g_wchunk_abl = 0;
 
-int msp_debug_wgrad_chunk(int nw) {
+int msp_debug_wgrad_chunk(int nw, int abl) {
   if (nw == 8 || nw == 16) g_wchunk_nw = nw;
+  if (abl >= 0) g_wchunk_abl = abl;
   return MSP_OK;
 }
 
@@ -1710,10 +1752,25 @@ int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out) {
   return r < n_tiles ? r : n_tiles;
 }
 
+int64_t msp_wgrad_chunk_cap(void) { return kWCap; }
+
+int msp_wgrad_chunk_index(const int64_t* tile_start, const int32_t* chunk_src, const uint16_t* chunk_row,
+                          int64_t n_rows, const int64_t* u_start, const int32_t* u_rows, uint32_t* chunk_lr,
+                          msp_stream_t stream) {
+  MSP_REQUIRE(n_rows >= 0 && n_rows < (1ll << 31), "msp_wgrad_chunk_index: bad row count");
+  const int64_t n_tiles = ceil_div(n_rows, kWTile);
+  if (n_tiles == 0) return MSP_OK;
+  MSP_REQUIRE(tile_start && chunk_src && chunk_row && u_start && u_rows && chunk_lr,
+              "msp_wgrad_chunk_index: NULL pointer");
+  chunk_lidx_kernel<<<(unsigned)n_tiles, kLT, 0, as_stream(stream)>>>(tile_start, chunk_src, chunk_row, u_start,
+                                                                      u_rows, chunk_lr);
+  return check_launch("msp_wgrad_chunk_index");
+}
+
 int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
                          const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
-                         const int32_t* u_rows, int64_t n_rows, int64_t n_ranges, float* slab, float* dw,
-                         msp_stream_t stream) {
+                         const int64_t* u_start, const int32_t* u_rows, int64_t n_rows, int64_t n_ranges,
+                         float* slab, float* dw, msp_stream_t stream) {
   MSP_REQUIRE(msp_wgrad_chunk_ok(n_rows, K, c_in, c_out), "msp_conv_wgrad_chunk: needs K <= 27 and channels in "
               "multiples of 32 (K=%d c_in=%d c_out=%d n=%lld)", K, c_in, c_out, (long long)n_rows);
   MSP_REQUIRE(tile_rows == kWTile, "msp_conv_wgrad_chunk: tile_rows must be %d (got %d)", kWTile, tile_rows);
@@ -1721,14 +1778,19 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
   hipStream_t s = as_stream(stream);
   const int64_t n_tiles = ceil_div(n_rows, kWTile);
   const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
-  if (g_wchunk_nw == 16)
+#define WC(A)                                                                                                  \
+  else if (g_wchunk_abl == A) wgrad_x6c_kernel<8, A><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(               \
+      x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  if (g_wchunk_abl == 0 && g_wchunk_nw == 16)
     wgrad_x6c_kernel<16><<<(unsigned)(n_ranges * slices), 1024, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
-                                                                        chunk_lr, u_rows, n_rows, n_tiles,
+                                                                        chunk_lr, u_start, u_rows, n_rows, n_tiles,
                                                                         (int)n_ranges, slab);
+  WC(1) WC(2) WC(4) WC(8) WC(15)
   else
     wgrad_x6c_kernel<8><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
-                                                                      chunk_lr, u_rows, n_rows, n_tiles,
+                                                                      chunk_lr, u_start, u_rows, n_rows, n_tiles,
                                                                       (int)n_ranges, slab);
+#undef WC
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
   wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
                                                                          (int)n_ranges, n4,

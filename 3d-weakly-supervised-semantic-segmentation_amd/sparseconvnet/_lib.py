@@ -43,7 +43,9 @@ PROTOTYPES = {
     "msp_wgrad_chunk_ok": (I, [I64, I, I, I]),
     "msp_wgrad_chunk_preferred": (I, [I64, I, I, I]),
     "msp_wgrad_chunk_ranges": (I64, [I64, I, I]),
-    "msp_conv_wgrad_chunk": (I, [P, I, P, I, I, I, P, P, P, P, I64, I64, P, P, P]),
+    "msp_wgrad_chunk_cap": (I64, []),
+    "msp_wgrad_chunk_index": (I, [P, P, P, I64, P, P, P, P]),
+    "msp_conv_wgrad_chunk": (I, [P, I, P, I, I, I, P, P, P, P, P, I64, I64, P, P, P]),
     "msp_conv_chunk_local": (I, [P, I, P, I, I, I, I, P, P, P, P, P, P, I64, P, P, SZ, P]),
     "msp_wgrad_local_ok": (I, [I64, I, I, I]),
     "msp_wgrad_local_ranges": (I64, [I64, I, I]),

@@ -195,14 +195,22 @@ class SubmRules:
         return self._chunk
 
     def wgrad_index(self):
-        """Per 128-row tile of the 128-row tile rulebook: the distinct input rows and each chunk entry's
-        position among them (msp_chunk_local), for msp_conv_wgrad_chunk; built on first use.  None when a tile
-        names more distinct rows than the kernel stages (msp_chunk_local_cap(128)): the pair lists serve then."""
+        """msp_wgrad_chunk_index over the 128-row tile rulebook and the tile-local rulebook (which lists each
+        tile's distinct input rows) for msp_conv_wgrad_chunk, built on first use.  None when a tile names more
+        distinct rows than the kernel stages (msp_wgrad_chunk_cap): the pair lists serve then."""
         if self._wchunk is None:
-            tiles = self.tiles_for(128)
-            self._plan.append(("wchunk", self._key))
-            idx = chunk_local_index(tiles, self._n, self.nbr.device, _lib.stream(self.nbr.device), with_max=True)
-            self._wchunk = idx if idx["max_u"] <= idx["cap"] else False
+            loc = self.local()
+            if loc["max_u"] > int(query("msp_wgrad_chunk_cap")):
+                self._wchunk = False
+            else:
+                tiles = self.tiles_for(128)
+                self._plan.append(("wchunk", self._key))
+                lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=self.nbr.device)
+                if self._n:
+                    call("msp_wgrad_chunk_index", ptr(tiles["tile_start"]), ptr(tiles["chunk_src"]),
+                         ptr(tiles["chunk_row"]), I64(self._n), ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(lr),
+                         _lib.stream(self.nbr.device))
+                self._wchunk = dict(tiles=tiles, chunk_lr=lr, u_start=loc["u_start"], u_rows=loc["u_rows"])
         return self._wchunk or None
 
     def tiles_for(self, tile_rows):

@@ -268,8 +268,8 @@ def conv_wgrad_chunk(x, dy, rules, K, kind="wgrad", flops=None):
         tiles["n_chunks"] * (1 + 16 * 4) + 8 * tiles["tile_start"].numel() + 4 * idx["u_rows"].numel()
     _record(kind + "/x6c", flops, lambda: call(
         "msp_conv_wgrad_chunk", ptr(x), c_in, ptr(dy), c_out, K, tiles["tile_rows"], ptr(tiles["tile_start"]),
-        ptr(tiles["chunk_off"]), ptr(idx["chunk_lr"]), ptr(idx["u_rows"]), n, ranges, ptr(slab), ptr(dw),
-        _stream(x)), nbytes)
+        ptr(tiles["chunk_off"]), ptr(idx["chunk_lr"]), ptr(idx["u_start"]), ptr(idx["u_rows"]), n, ranges,
+        ptr(slab), ptr(dw), _stream(x)), nbytes)
     return dw
 
 

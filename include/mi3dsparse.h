@@ -195,8 +195,8 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
  * name, ascending, the first msp_chunk_local_cap() of them at u_rows[u * cap ..] and their count at u_cnt[u],
  * and writes per chunk entry e the word chunk_lr[e] = (position in that list, 0xFFFF past the cap) | (row
  * inside the unit, 128 for a padding slot) << 16; max_chunks = the rulebook's largest tile (<= 128).
- * tile_rows 128 (the weight gradient's index, msp_conv_wgrad_chunk): a unit is one rulebook tile and the cap
- * msp_chunk_local_cap(128).  max_count (device int64, nullable) gets the largest unit's count.  The
+ * tile_rows 128: a unit is one rulebook tile (cap msp_chunk_local_cap(128)).  max_count (device int64,
+ * nullable) gets the largest unit's count.  The
  * convolution stages each unit's listed rows in LDS once per 32 input channels and accumulates the chunks'
  * partial products in LDS (entries past the cap read chunk_src from global memory).  c_in % 16 == 0,
  * c_out % 32 == 0; flip and weight layouts as msp_conv_tile; workspace msp_conv_local_workspace_size. */
@@ -205,20 +205,27 @@ int msp_chunk_local(const int64_t* tile_start, int64_t n_rows, int tile_rows, in
                     const int32_t* chunk_src, const uint16_t* chunk_row, int32_t* u_rows, int32_t* u_cnt,
                     uint32_t* chunk_lr, int64_t* max_count, msp_stream_t stream);
 int msp_conv_chunk_local_preferred(int64_t n_rows, int c_in, int c_out);
-/* Submanifold weight gradient over a 128-row tile rulebook and its msp_chunk_local index (tile_rows = 128):
- * dW[o][ci][co] = sum over the rules (i, j) of offset o of x[i][ci] dy[j][co] (the forward's [K][c_in][c_out]
- * layout).  Per tile the distinct x rows and the 128 dy rows are staged in LDS once per 32 x 32 channel slice
- * (exact bf16 pieces), the rulebook's chunks are the MFMA k-steps.  Needs every tile's distinct-row count
- * (msp_chunk_local max_count) <= msp_chunk_local_cap(128), K <= 27, channels in multiples of 32
- * (msp_wgrad_chunk_ok).  Blocks run n_ranges contiguous tile ranges (msp_wgrad_chunk_ranges) per slice; slab
- * holds n_ranges x K x c_in x c_out floats of partial sums, added in range order into dw. */
+/* Submanifold weight gradient over a 128-row tile rulebook (msp_tile_rulebook, tile_rows = 128) and the
+ * tile-local rulebook of the same map (msp_tile_local, tile_rows = 128): dW[o][ci][co] = sum over the rules
+ * (i, j) of offset o of x[i][ci] dy[j][co] (the forward's [K][c_in][c_out] layout).  msp_wgrad_chunk_index
+ * writes per chunk entry e chunk_lr[e] = (position of its input row in its tile's u_rows list) | (row in the
+ * tile, 128 for a padding slot) << 16.  msp_conv_wgrad_chunk stages per tile the listed x rows and the 128 dy
+ * rows in LDS once per 32 x 32 channel slice (exact bf16 pieces); the rulebook's chunks are the MFMA k-steps.
+ * Needs every tile's list (msp_tile_local's largest count) <= msp_wgrad_chunk_cap(), K <= 27, channels in
+ * multiples of 32 (msp_wgrad_chunk_ok; msp_wgrad_chunk_preferred: the shapes the library takes it for).
+ * Blocks run n_ranges contiguous tile ranges (msp_wgrad_chunk_ranges) per slice; slab holds n_ranges x K x
+ * c_in x c_out floats of partial sums, added in range order into dw. */
+int64_t msp_wgrad_chunk_cap(void);
 int msp_wgrad_chunk_ok(int64_t n_rows, int K, int c_in, int c_out);
 int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out);
 int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out);
+int msp_wgrad_chunk_index(const int64_t* tile_start, const int32_t* chunk_src, const uint16_t* chunk_row,
+                          int64_t n_rows, const int64_t* u_start, const int32_t* u_rows, uint32_t* chunk_lr,
+                          msp_stream_t stream);
 int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
                          const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
-                         const int32_t* u_rows, int64_t n_rows, int64_t n_ranges, float* slab, float* dw,
-                         msp_stream_t stream);
+                         const int64_t* u_start, const int32_t* u_rows, int64_t n_rows, int64_t n_ranges,
+                         float* slab, float* dw, msp_stream_t stream);
 int msp_conv_chunk_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                          const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                          const uint32_t* chunk_lr, const int32_t* u_rows, const int32_t* u_cnt, int64_t n_rows,

@@ -12,7 +12,8 @@ from sparseconvnet import _lib, ops
 from wsss3d.synthetic import make_batch
 lib = _lib.load()
 import ctypes
-lib.msp_debug_wgrad_chunk.argtypes = [ctypes.c_int]
+lib.msp_debug_wgrad_chunk.argtypes = [ctypes.c_int, ctypes.c_int]
+ABLS = [int(a) for a in os.environ.get("ABL", "").split(",") if a]
 b = make_batch(8, 50, seed=1)
 t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
 meta = t.metadata
@@ -43,10 +44,15 @@ for L, size in enumerate(sizes):
     if "local" in forms:
         rules.local()
     tiles = rules.tiles_for(128)
-    ms_idx = timeit(lambda: scn.metadata.chunk_local_index(tiles, V, rules.nbr.device, _lib.stream()), 3)
+    rules.local()
+
+    def rebuild():
+        rules._wchunk = None
+        return rules.wgrad_index()
+    ms_idx = timeit(rebuild, 3)
     idx = rules.wgrad_index()
     print(f"L{L} V={V} R={rules.n_rules} chunks(128)={tiles['n_chunks']} max distinct/tile "
-          f"{'over cap' if idx is None else int(idx['u_cnt'][:idx['n_units']].max())} index build {ms_idx:.3f} ms",
+          f"{rules.local()['max_u']}{' (over cap)' if idx is None else ''} index build {ms_idx:.3f} ms",
           flush=True)
     c = int(os.environ.get("M", "32")) * (L + 1)
     for cin, cout in ((c, c), (2 * c, c), (c, 2 * c)):
@@ -68,9 +74,18 @@ for L, size in enumerate(sizes):
                "chunk": lambda: ops.conv_wgrad_chunk(x, dy, rules, 27)}
         for nw in (8, 16):
             def fnw(nw=nw):
-                lib.msp_debug_wgrad_chunk(nw)
+                lib.msp_debug_wgrad_chunk(nw, 0)
                 return ops.conv_wgrad_chunk(x, dy, rules, 27)
             fns[f"chunk{nw}"] = fnw
+        for abl in ABLS:
+            def fab(abl=abl):
+                lib.msp_debug_wgrad_chunk(8, abl)
+                try:
+                    return ops.conv_wgrad_chunk(x, dy, rules, 27)
+                finally:
+                    lib.msp_debug_wgrad_chunk(8, 0)
+            fns[f"abl{abl}"] = fab
+            forms = forms + [f"abl{abl}"] if f"abl{abl}" not in forms else forms
         for name, f in ((k, fns[k]) for k in forms):
             ms = timeit(f)
             err = (f().double() - ref).abs().max().item() / scale
