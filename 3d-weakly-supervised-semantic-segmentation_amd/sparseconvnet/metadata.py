@@ -470,6 +470,7 @@ class Metadata:
 # memory was handed to a new tensor can never pick up another batch's rulebooks.
 _PREFETCHED = {}
 _SIDE = {}
+_CAPTURED = []
 
 
 def _coords_key(coords, spatial_size):
@@ -513,7 +514,28 @@ def take_prefetched(coords, spatial_size):
     del _PREFETCHED[coords.device.index]
     _, _, m, ev = hit
     cur = torch.cuda.current_stream(coords.device)
+    if torch.cuda.is_current_stream_capturing():
+        # inside a graph capture (bench.py --graph): the replaying stream waits on the build before the graph
+        # runs (prefetch_event, taken before the capture), and the Metadata must outlive every replay: it is
+        # parked here until the capturer takes it with captured_metadata()
+        _CAPTURED.append(m)
+        return m
     cur.wait_event(ev)
     for t in m.tensors():
         t.record_stream(cur)
     return m
+
+
+def captured_metadata():
+    """The Metadata consumed inside graph captures since the last call (the capturer keeps them alive for
+    as long as it replays the graph)."""
+    out = list(_CAPTURED)
+    _CAPTURED.clear()
+    return out
+
+
+def prefetch_event(device):
+    """The build event of the entry pending on `device` (None if none): a stream that will replay a graph
+    capturing the consumption of that entry must wait on it first."""
+    hit = _PREFETCHED.get(torch.device(device).index)
+    return None if hit is None else hit[3]

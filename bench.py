@@ -279,6 +279,10 @@ def main():
     ap.add_argument("--prefetch-at", choices=["end", "fwd"], default="end",
                     help="when the next batch's metadata is built: after the step's optimizer call is queued (end) "
                          "or right after its forward is queued (fwd: the build's host reads overlap the forward)")
+    ap.add_argument("--graph", type=int, choices=[0, 1], default=None,
+                    help="1: capture every step afresh into a HIP graph (built after the step's metadata is "
+                         "prefetched, replayed on the compute stream while the next step is prefetched and "
+                         "captured; one rank only) -- removes the per-kernel launch gaps; default off")
     ap.add_argument("--workload", choices=["unet", "contrastive"], default=None,
                     help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
                          "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
@@ -346,7 +350,11 @@ def main():
     n_params = sum(p.numel() for p in model.parameters())
     # the reference's optimizer (train.py:39, Adam lr 1e-3); one fused multi-tensor kernel per step
     # (--foreach-adam: torch's default foreach form, ~21 launches per step)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else {"fused": True}))
+    # HIP-graph steps (--graph): one rank only (the DDP gradient all-reduce stays eager), metadata prefetched
+    use_graph = bool(args.graph if args.graph is not None else 0) and world == 1 and not args.no_prefetch \
+        and args.prefetch_at == "end"
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
+                                                           {"fused": True, "capturable": use_graph}))
     cls_loss, _ = LOSS_REGISTRY.get("Classification")
     con_loss, _ = LOSS_REGISTRY.get("TextContrastive")
 
@@ -359,42 +367,114 @@ def main():
         scn.prefetch_metadata(model, batches[(i + 1) % len(batches)][0].coords, wait_for_producer=False)
         prefetch_s.append(time.perf_counter() - t)
 
+    host_t = [] if os.environ.get("BENCH_HOST_TIMING") else None  # host enqueue time per phase (diagnostic)
+
     def step(i):
         x, y, _, text = batches[i % len(batches)]
+        h0 = time.perf_counter()
         opt.zero_grad(set_to_none=True)
         logits, meta = model((x, text), istrain=True)
+        h1 = time.perf_counter()
         if not args.no_prefetch and args.prefetch_at == "fwd":
             prefetch(i)
         loss = cls_loss(logits, y)
         if contrastive:
             loss = loss + con_loss(*meta)
         loss.backward()
+        h2 = time.perf_counter()
         opt.step()
+        h3 = time.perf_counter()
         if not args.no_prefetch and args.prefetch_at == "end":
             prefetch(i)
+        if host_t is not None:
+            host_t.append((h1 - h0, h2 - h1, h3 - h2, time.perf_counter() - h3))
         return loss
+
+    from sparseconvnet import metadata as scn_meta
+    cur = torch.cuda.current_stream(dev)
+    cap_stream = torch.cuda.Stream(dev) if use_graph else None
+    capture_s = []
+
+    def body(i):  # one training step without its prefetch (what a graph captures)
+        x, y, _, text = batches[i % len(batches)]
+        opt.zero_grad(set_to_none=True)
+        logits, meta = model((x, text), istrain=True)
+        loss = cls_loss(logits, y)
+        if contrastive:
+            loss = loss + con_loss(*meta)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def capture(i):
+        """Graph of step i, whose metadata is the pending prefetch; returns (graph, metadata it reads, the
+        metadata's build event).  Nothing executes here: the kernels run at replay."""
+        t = time.perf_counter()
+        ev = scn_meta.prefetch_event(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cap_stream):
+            g.capture_begin()
+            body(i)
+            g.capture_end()
+        keep = scn_meta.captured_metadata()
+        if not keep:
+            raise RuntimeError("bench.py --graph: the captured step did not consume its prefetched metadata")
+        capture_s.append(time.perf_counter() - t)
+        return g, keep, ev
+
+    def replay(entry):
+        g, keep, ev = entry
+        cur.wait_event(ev)  # the metadata build (side stream) before the graph reads it
+        for m in keep:
+            for t in m.tensors():
+                t.record_stream(cur)
+        g.replay()
+        done = torch.cuda.Event()
+        done.record(cur)
+        return done
 
     for i in range(args.warmup):
         step(i)
-    rec = KernelRecorder(args.record, pool=2 * 700 * args.steps)
-    _lib.set_recorder(rec if args.record != "none" else None)
+    rec = KernelRecorder(args.record if not use_graph else "none", pool=2 * 700 * args.steps)
+    _lib.set_recorder(rec if args.record != "none" and not use_graph else None)
+    entry = None
+    if use_graph:  # the first step's metadata and graph, before the timed region (as eager's last warm-up does)
+        prefetch(-1)
+        entry = capture(0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     rec.active = True
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
+    if use_graph:
+        inflight = []
+        for i in range(args.steps):
+            inflight.append((entry, replay(entry)))
+            prefetch(i)  # batch i + 1 on the side stream while step i runs
+            while len(inflight) > 1:  # at most one step ahead of the device
+                inflight[0][1].synchronize()
+                inflight.pop(0)
+            entry = capture(i + 1) if i + 1 < args.steps else None
+    else:
+        for i in range(args.steps):
+            step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     rec.active = False
+    if use_graph:
+        inflight = entry = None
+        _lib.set_recorder(None)
+    if host_t:
+        med = [1e3 * statistics.median(c) for c in zip(*host_t[-args.steps:])]
+        print(f"bench.py host enqueue ms per step (median): forward {med[0]:.2f}  loss+backward {med[1]:.2f}  "
+              f"optimizer {med[2]:.2f}  prefetch {med[3]:.2f}  sum {sum(med):.2f}", file=sys.stderr)
     vox = sum(batches[i % len(batches)][2] for i in range(args.steps))
     dt_max, vox_all = dp.max_over_ranks(dt), dp.sum_over_ranks(float(vox))
     _lib.set_recorder(None)
     fams = rec.summary()
-    fam_steps = args.family_steps if args.record != "all" else 0
+    fam_steps = args.family_steps if (args.record != "all" or use_graph) else 0
     if fam_steps:
         # every family bracketed, outside the timed region (see --record)
         rec_all = KernelRecorder("all", pool=2 * 700 * fam_steps)
@@ -405,6 +485,8 @@ def main():
         rec_all.active = False
         _lib.set_recorder(None)
         fams_all = rec_all.summary()
+        if use_graph:  # HIP events cannot time kernels inside a graph: the conv family from the recorded steps
+            fams = fams_all
     else:
         fams_all = fams
         fam_steps = args.steps
@@ -461,6 +543,10 @@ def main():
                 "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step "
                 f"(after its {'optimizer' if args.prefetch_at == 'end' else 'forward'} call is queued; host "
                 f"time {1e3 * statistics.median(prefetch_s) if prefetch_s else 0:.1f} ms median)",
+                "launch": (f"every step captured afresh into a HIP graph after its metadata is prefetched and replayed "
+                           f"on the compute stream (capture host time {1e3 * statistics.median(capture_s):.1f} ms "
+                           "median, overlapped with the previous step's replay)") if use_graph and capture_s else
+                "eager kernel launches",
                 "active_voxels_per_step_rank0": batches[0][2],
                 "levels": stats,
                 "fwd_multiply_adds": macs,
@@ -487,6 +573,10 @@ def main():
                 "launches": conv["launches"],
                 "avg_launch_us": conv["ms"] / max(conv["launches"], 1) * 1e3,
                 "per_kind": conv["per_kind"],
+                "source": (f"{fam_steps} eagerly launched steps right after the timed region, each conv call "
+                           "bracketed with HIP events on its launch stream (the timed steps run as HIP graphs, "
+                           "whose kernels events cannot time; same kernels and shapes)") if use_graph else
+                          "the timed steps, each conv call bracketed with HIP events on its launch stream",
             }
             res["roofline_families"] = {
                 f: {k: v for k, v in d.items() if k != "per_kind" and k != "bytes"} | {"per_kind": d["per_kind"]}

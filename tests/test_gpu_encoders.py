@@ -249,3 +249,47 @@ def test_prefetch_entry_needs_the_same_tensor():
         assert md.take_prefetched(xs[1].coords, 4096) is None
         assert md.take_prefetched(xs[0].coords, 4096) is m2 and m2 is not m
         assert not md._PREFETCHED
+
+
+def test_graph_captured_step_matches_eager():
+    """bench.py --graph: a training step captured into a HIP graph after its metadata was prefetched, then
+    replayed, leaves parameters, gradients and Adam state bit-identical to the same step launched eagerly
+    (same kernels in the same order), and the capture consumes the prefetched metadata."""
+    import copy
+    import torch.nn.functional as F
+    from sparseconvnet import metadata as md
+    model, xs, ys = _prefetch_model()
+    twin = copy.deepcopy(model)
+    opts = [torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=True) for m in (model, twin)]
+
+    def body(m, opt, k):
+        opt.zero_grad(set_to_none=True)
+        logits, _ = m((xs[k], None), istrain=True)
+        F.multilabel_soft_margin_loss(logits, ys[k]).backward()
+        opt.step()
+
+    for m, opt in zip((model, twin), opts):   # plan + optimizer state, eagerly
+        body(m, opt, 0)
+    torch.cuda.synchronize()
+    scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False)
+    body(model, opts[0], 1)                   # eager, prefetched
+    scn.prefetch_metadata(twin, xs[1].coords, wait_for_producer=False)
+    ev = md.prefetch_event(DEV)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        g.capture_begin()
+        body(twin, opts[1], 1)
+        g.capture_end()
+    keep = md.captured_metadata()
+    assert len(keep) == 1 and not md._PREFETCHED
+    cur = torch.cuda.current_stream()
+    cur.wait_event(ev)
+    g.replay()
+    torch.cuda.synchronize()
+    for (na, a), (nb, b) in zip(model.named_parameters(), twin.named_parameters()):
+        assert torch.equal(a, b), na
+        assert torch.equal(a.grad, b.grad), na
+    for sa, sb in zip(opts[0].state.values(), opts[1].state.values()):
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(sa[k], sb[k])
