@@ -490,7 +490,9 @@ def prefetch(coords, spatial_size, plan, wait_for_producer=True):
     if side is None:
         side = _SIDE[dev.index] = torch.cuda.Stream(dev)
     cur = torch.cuda.current_stream(dev)
-    if wait_for_producer:
+    if isinstance(wait_for_producer, torch.cuda.Event):
+        side.wait_event(wait_for_producer)
+    elif wait_for_producer:
         side.wait_stream(cur)
     with torch.cuda.stream(side):
         m = Metadata(dev)

@@ -373,8 +373,9 @@ def prefetch_metadata(model, coords, wait_for_producer=True):
     queued backward/optimizer too, so there is no overlap.  Pass False for
     coords that are already complete on the device (a resident batch, or one
     whose producer was synchronised): the build then runs beside the queued
-    work.  The entry is keyed on the coords tensor object itself and only the
-    latest prefetch per device is kept."""
+    work.  A torch.cuda.Event orders the build after that event only (bench.py
+    --graph paces its capture loop this way).  The entry is keyed on the coords
+    tensor object itself and only the latest prefetch per device is kept."""
     for m in model.modules():
         if isinstance(m, InputLayer):
             plan = getattr(m, "last_plan", None)

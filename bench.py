@@ -282,7 +282,7 @@ def main():
     ap.add_argument("--graph", type=int, choices=[0, 1], default=None,
                     help="1: capture every step afresh into a HIP graph (built after the step's metadata is "
                          "prefetched, replayed on the compute stream while the next step is prefetched and "
-                         "captured; one rank only) -- removes the per-kernel launch gaps; default off")
+                         "captured; one rank only: the DDP all-reduce stays eager) -- removes the per-kernel launch gaps; default 1")
     ap.add_argument("--workload", choices=["unet", "contrastive"], default=None,
                     help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
                          "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
@@ -351,7 +351,7 @@ def main():
     # the reference's optimizer (train.py:39, Adam lr 1e-3); one fused multi-tensor kernel per step
     # (--foreach-adam: torch's default foreach form, ~21 launches per step)
     # HIP-graph steps (--graph): one rank only (the DDP gradient all-reduce stays eager), metadata prefetched
-    use_graph = bool(args.graph if args.graph is not None else 0) and world == 1 and not args.no_prefetch \
+    use_graph = bool(args.graph if args.graph is not None else 1) and world == 1 and not args.no_prefetch \
         and args.prefetch_at == "end"
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
                                                            {"fused": True, "capturable": use_graph}))
@@ -360,11 +360,12 @@ def main():
 
     prefetch_s = []
 
-    def prefetch(i):
+    def prefetch(i, after=None):
         # input pipelining: the next batch's voxelisation and rulebooks on a side stream while this step's
-        # kernels run (sparseconvnet.prefetch_metadata)
+        # kernels run (sparseconvnet.prefetch_metadata); `after`: an event the build waits for
         t = time.perf_counter()
-        scn.prefetch_metadata(model, batches[(i + 1) % len(batches)][0].coords, wait_for_producer=False)
+        scn.prefetch_metadata(model, batches[(i + 1) % len(batches)][0].coords,
+                              wait_for_producer=after if after is not None else False)
         prefetch_s.append(time.perf_counter() - t)
 
     host_t = [] if os.environ.get("BENCH_HOST_TIMING") else None  # host enqueue time per phase (diagnostic)
@@ -393,6 +394,11 @@ def main():
     from sparseconvnet import metadata as scn_meta
     cur = torch.cuda.current_stream(dev)
     cap_stream = torch.cuda.Stream(dev) if use_graph else None
+    # one memory pool for every step's graph: blocks a finished step's graph freed are reused by later captures
+    # (replays are ordered on the compute stream); a private pool per graph would hand its memory back with a
+    # device-synchronising free each step
+    graph_pool = torch.cuda.graph_pool_handle() if use_graph else None
+
     capture_s = []
 
     def body(i):  # one training step without its prefetch (what a graph captures)
@@ -413,7 +419,7 @@ def main():
         ev = scn_meta.prefetch_event(dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(cap_stream):
-            g.capture_begin()
+            g.capture_begin(pool=graph_pool, capture_error_mode="relaxed")
             body(i)
             g.capture_end()
         keep = scn_meta.captured_metadata()
@@ -422,15 +428,22 @@ def main():
         capture_s.append(time.perf_counter() - t)
         return g, keep, ev
 
+    replay_ev = []
+
     def replay(entry):
         g, keep, ev = entry
         cur.wait_event(ev)  # the metadata build (side stream) before the graph reads it
         for m in keep:
             for t in m.tensors():
                 t.record_stream(cur)
+        if host_t is not None:
+            replay_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+            replay_ev[-1][0].record(cur)
         g.replay()
-        done = torch.cuda.Event()
+        done = torch.cuda.Event(enable_timing=host_t is not None)
         done.record(cur)
+        if host_t is not None:
+            replay_ev[-1] = (replay_ev[-1][0], done)
         return done
 
     for i in range(args.warmup):
@@ -447,14 +460,37 @@ def main():
     rec.active = True
     t0 = time.perf_counter()
     if use_graph:
-        inflight = []
+        inflight, done_prev = [], None
         for i in range(args.steps):
-            inflight.append((entry, replay(entry)))
-            prefetch(i)  # batch i + 1 on the side stream while step i runs
-            while len(inflight) > 1:  # at most one step ahead of the device
-                inflight[0][1].synchronize()
-                inflight.pop(0)
+            h0 = time.perf_counter()
+            done = replay(entry)
+            inflight.append((entry, done, i))
+            h1 = time.perf_counter()
+            # batch i + 1 on the side stream, after step i - 1's graph on the device: the build's count reads
+            # pace the host (at most one step ahead: step i is queued while step i + 1 is captured)
+            prefetch(i, done_prev)
+            done_prev = done
+            h2 = time.perf_counter()
+            # the step's metadata is released now (its tensors were marked as used by the compute stream); the
+            # graphs themselves are kept until the loop has drained: destroying an executable graph here
+            # synchronised with the device (measured: 49 ms per step of host wait, the device idle through the
+            # next capture)
+            inflight[-1] = (inflight[-1][0][0], None, i)
+            h3 = time.perf_counter()
             entry = capture(i + 1) if i + 1 < args.steps else None
+            if host_t is not None:
+                host_t.append((h1 - h0, h2 - h1, h3 - h2, time.perf_counter() - h3))
+        if host_t:
+            med = [1e3 * statistics.median(c) for c in zip(*host_t[-args.steps:])]
+            print(f"bench.py graph loop host ms per step (median): replay call {med[0]:.2f}  prefetch {med[1]:.2f}  "
+                  f"release {med[2]:.2f}  capture {med[3]:.2f}", file=sys.stderr)
+            host_t.clear()
+            torch.cuda.synchronize()
+            print("bench.py graph replays, device ms:", [round(a.elapsed_time(b), 1) for a, b in replay_ev],
+                  file=sys.stderr)
+            print("bench.py graph replays, device idle before each, ms:",
+                  [round(replay_ev[k][1].elapsed_time(replay_ev[k + 1][0]), 1) for k in range(len(replay_ev) - 1)],
+                  file=sys.stderr)
     else:
         for i in range(args.steps):
             step(i)
