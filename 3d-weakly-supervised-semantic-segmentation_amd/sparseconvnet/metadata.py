@@ -213,6 +213,15 @@ class SubmRules:
                 self._wchunk = dict(tiles=tiles, chunk_lr=lr, u_start=loc["u_start"], u_rows=loc["u_rows"])
         return self._wchunk or None
 
+    def note_use(self, purpose, c_in, c_out):
+        """Record in the plan that a convolution / weight gradient with these channel counts runs over these
+        rules: a replay then builds what that call selects for ITS batch's sizes (ops.prepare)."""
+        e = ("use", self._key, purpose, int(c_in), int(c_out))
+        seen = self.__dict__.setdefault("_uses", set())
+        if e not in seen:
+            seen.add(e)
+            self._plan.append(e)
+
     def tiles_for(self, tile_rows):
         """Tile rulebook with tile_rows-row tiles, built on first use."""
         t = self._tiles.get(tile_rows)
@@ -242,6 +251,7 @@ class DownRules:
         self.pairs = PairLists(self.down, K, coarse.n, dev, s)
 
     tiles_for = SubmRules.tiles_for
+    note_use = SubmRules.note_use
 
 
 class Level:
@@ -410,9 +420,20 @@ class Metadata:
 
     def replay(self, plan):
         """Build, in order, the rulebooks another forward of the same network
-        requested (its `plan`); later requests then find them built."""
+        requested (its `plan`); later requests then find them built.  Rules
+        with recorded uses ("use": a convolution or weight gradient and its
+        channel counts) get what those uses select for this batch's sizes
+        (ops.prepare) instead of the concrete rulebooks the other batch built."""
+        from . import ops
+        used = {e[1] for e in plan if e[0] == "use"}
         for entry in plan:
-            if entry[0] == "down":
+            if entry[0] in ("tiles", "dense", "local", "chunk", "wchunk") and entry[1] in used:
+                continue
+            if entry[0] == "use":
+                rules = self._rules(entry[1])
+                rules.note_use(entry[2], entry[3], entry[4])
+                ops.prepare(rules, entry[2], entry[3], entry[4])
+            elif entry[0] == "down":
                 self.downsample(entry[1], entry[2])
             elif entry[0] == "subm":
                 self.level(entry[1]).subm_rules(entry[2])

@@ -54,22 +54,60 @@ def _record(kind, flops, fn, nbytes=0):
 
 
 # ------------------------------------------------------------------ convolution helpers
+def conv_form(rules, n_rows, c_in, c_out, K):
+    """Which form (and so which rulebook) the convolution over `rules` takes for these sizes: "local", "chunk",
+    "nbr", or the tile height of msp_conv_tile -- the library's preference queries."""
+    nbr = getattr(rules, "nbr", None)  # submanifold rules carry the neighbour map
+    if nbr is not None and n_rows and K <= 27 and CONV_LOCAL and \
+            int(_lib.query("msp_conv_local_preferred", _lib.I64(n_rows), c_in, c_out)):
+        return "local"
+    if nbr is not None and n_rows and K <= 27 and CONV_CHUNK and \
+            int(_lib.query("msp_conv_chunk_local_preferred", _lib.I64(n_rows), c_in, c_out)):
+        return "chunk"
+    if nbr is not None and n_rows and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(n_rows), c_in, c_out)):
+        return "nbr"
+    return int(_lib.query("msp_conv_tile_rows", _lib.I64(n_rows), c_in, c_out))
+
+
+def prepare(rules, purpose, c_in, c_out):
+    """Build the rulebooks a convolution ("conv": forward / backward-data) or a submanifold weight gradient
+    ("wgrad") over `rules` will use for these channel counts, for the rules' own row count (Metadata.replay:
+    a prefetched batch gets exactly what its sizes select, even when they cross a threshold the previous
+    batch's did not)."""
+    n, K = rules._n, rules.K
+    if purpose == "conv":
+        f = conv_form(rules, n, c_in, c_out, K)
+        if f == "local":
+            rules.local()
+        elif f == "chunk":
+            rules.chunk_local()
+        elif f == "nbr":
+            rules.dense_order()
+        else:
+            rules.tiles_for(f)
+    elif purpose == "wgrad":
+        if WGRAD_CHUNK and int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(n), K, c_in, c_out)):
+            if rules.wgrad_index() is not None:
+                return
+        if WGRAD_LOCAL and int(_lib.query("msp_wgrad_local_ok", _lib.I64(n), K, c_in, c_out)):
+            rules.local()
+
+
 def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     """Output-stationary convolution over the rulebook's tile form; the tile
     height (and so which rulebook) is the library's choice for these channel
     counts (msp_conv_tile_rows)."""
     c_in = x.size(1)
-    nbr = getattr(rules, "nbr", None)  # submanifold rules carry the neighbour map
-    if nbr is not None and n_rows and K <= 27 and CONV_LOCAL and \
-            int(_lib.query("msp_conv_local_preferred", _lib.I64(n_rows), c_in, c_out)):
+    rules.note_use("conv", c_in, c_out)
+    f = conv_form(rules, n_rows, c_in, c_out, K)
+    if f == "local":
         return conv_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
-    if nbr is not None and n_rows and K <= 27 and CONV_CHUNK and \
-            int(_lib.query("msp_conv_chunk_local_preferred", _lib.I64(n_rows), c_in, c_out)):
+    if f == "chunk":
         return conv_chunk_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
-    if nbr is not None and n_rows and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(n_rows), c_in, c_out)):
+    if f == "nbr":
         perm, nbr_p = rules.dense_order()
         return conv_nbr(x, wt, K, flip, c_out, nbr_p, n_rows, kind, flops, perm)
-    tr = int(_lib.query("msp_conv_tile_rows", _lib.I64(n_rows), c_in, c_out))
+    tr = f
     tiles = rules.tiles_for(tr)
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
     if n_rows:
@@ -320,6 +358,7 @@ class SubmanifoldConvFunction(torch.autograd.Function):
             p = rules.pairs
             V = xp.size(0)
             dwp = None
+            rules.note_use("wgrad", cin_p, cout_p)
             if WGRAD_CHUNK and int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)):
                 dwp = conv_wgrad_chunk(xp, g, rules, K, flops=2.0 * p.total * cin * cout)
             if dwp is not None:

@@ -351,7 +351,8 @@ def main():
     # the reference's optimizer (train.py:39, Adam lr 1e-3); one fused multi-tensor kernel per step
     # (--foreach-adam: torch's default foreach form, ~21 launches per step)
     # HIP-graph steps (--graph): one rank only (the DDP gradient all-reduce stays eager), metadata prefetched
-    use_graph = bool(args.graph if args.graph is not None else 1) and world == 1 and not args.no_prefetch \
+    use_graph = bool(args.graph if args.graph is not None else not contrastive) and world == 1 \
+        and not args.no_prefetch \
         and args.prefetch_at == "end"
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
                                                            {"fused": True, "capturable": use_graph}))

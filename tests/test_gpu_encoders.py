@@ -293,3 +293,51 @@ def test_graph_captured_step_matches_eager():
     for sa, sb in zip(opts[0].state.values(), opts[1].state.values()):
         for k in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(sa[k], sb[k])
+
+
+def test_graph_capture_after_a_smaller_batch():
+    """The prefetched plan comes from the previous batch, whose level sizes may select other rulebooks (the
+    tile-local form from 4096 rows at 64 channels, the chunk-local weight gradient from 2^14 rows): replay
+    prepares what THIS batch's sizes select (recorded uses, ops.prepare), so a capture after a much smaller
+    batch builds nothing on demand (a host read there would abort the capture), and it matches eager."""
+    import copy
+    import torch.nn.functional as F
+    from sparseconvnet import metadata as md
+    from wsss3d import EasyDict
+    torch.manual_seed(0)
+    cls, _ = MODEL_REGISTRY.get("MultiLabel")
+    pc = EasyDict(name="SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=1, residual_blocks=True)
+    model = cls(pc).to(DEV)
+    twin = copy.deepcopy(model)
+    bs = [make_batch(1, 12, seed=31), make_batch(4, 50, seed=32)]
+    xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(DEV), feature=torch.from_numpy(b["feats"]).to(DEV),
+                   batch_offsets=b["batch_offsets"]) for b in bs]
+    ys = [torch.from_numpy(b["scene_labels"]).to(DEV) for b in bs]
+    opts = [torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=True) for m in (model, twin)]
+
+    def body(m, opt, k):
+        opt.zero_grad(set_to_none=True)
+        logits, _ = m((xs[k], None), istrain=True)
+        F.multilabel_soft_margin_loss(logits, ys[k]).backward()
+        opt.step()
+
+    for m, opt in zip((model, twin), opts):   # the small batch, eagerly: its plan
+        body(m, opt, 0)
+    torch.cuda.synchronize()
+    scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False)
+    body(model, opts[0], 1)
+    scn.prefetch_metadata(twin, xs[1].coords, wait_for_producer=False)
+    ev = md.prefetch_event(DEV)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        g.capture_begin(capture_error_mode="relaxed")
+        body(twin, opts[1], 1)
+        g.capture_end()
+    md.captured_metadata()
+    torch.cuda.current_stream().wait_event(ev)
+    g.replay()
+    torch.cuda.synchronize()
+    for (na, a), (nb, b) in zip(model.named_parameters(), twin.named_parameters()):
+        assert torch.equal(a, b), na
+        assert torch.equal(a.grad, b.grad), na
