@@ -193,7 +193,7 @@ _WGRAD_SIDE = {}
 WGRAD_CONCURRENT = False
 
 
-def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None):
+def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None, kind="wgrad"):
     """conv_wgrad on a side stream, ordered after the work already queued on
     the current stream, so it runs concurrently with the backward-data
     launched next on the current stream (both are latency-bound gathers at
@@ -202,7 +202,7 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None):
     backward returns, so everything after this autograd node is ordered
     after the weight gradient as well."""
     if not WGRAD_CONCURRENT:
-        return conv_wgrad(x, dy, pairs, pin, pout, K, flops=flops), lambda: None
+        return conv_wgrad(x, dy, pairs, pin, pout, K, kind, flops=flops), lambda: None
     dev = x.device
     cur = torch.cuda.current_stream(dev)
     side = _WGRAD_SIDE.get(dev.index)
@@ -210,7 +210,7 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None):
         side = _WGRAD_SIDE[dev.index] = torch.cuda.Stream(dev)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
-        dw = conv_wgrad(x, dy, pairs, pin, pout, K, flops=flops)
+        dw = conv_wgrad(x, dy, pairs, pin, pout, K, kind, flops=flops)
         ev = torch.cuda.Event()
         ev.record(side)
 
@@ -405,7 +405,7 @@ class ConvolutionFunction(torch.autograd.Function):
         dx = dw = None
         join = None
         if ctx.needs_input_grad[1]:
-            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)
+            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout, "wgrad_strided")
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             # dx[fine] = W[o] g[parent]: src = coarse (pair_out), dst = fine (pair_in)
@@ -445,7 +445,7 @@ class DeconvolutionFunction(torch.autograd.Function):
         dx = dw = None
         join = None
         if ctx.needs_input_grad[1]:
-            dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K, 2.0 * p.total * cin * cout)
+            dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K, 2.0 * p.total * cin * cout, "wgrad_deconv")
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             dxp = conv_tile(g, wp, K, 0, cin_p, rules, xp.size(0), "deconv_bwd_data",

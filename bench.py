@@ -55,7 +55,8 @@ HBM_PEAK_GBS = 8000.0
 
 # recorded kinds (sparseconvnet/ops.py _record) -> family
 CONV_KINDS = ("subm_fwd", "conv_fwd", "subm_bwd_data", "deconv_bwd_data")
-FAMILIES = {"wgrad": "wgrad", "nin_wgrad": "wgrad", "conv_bwd_data": "pairs", "deconv_fwd": "pairs",
+FAMILIES = {"wgrad": "wgrad", "nin_wgrad": "wgrad", "wgrad_strided": "wgrad", "wgrad_deconv": "wgrad",
+            "conv_bwd_data": "pairs", "deconv_fwd": "pairs",
             "nin_fwd": "nin", "nin_bwd_data": "nin", "bn_fwd": "bn", "bn_bwd": "bn", "bn_join": "bn"}
 
 
