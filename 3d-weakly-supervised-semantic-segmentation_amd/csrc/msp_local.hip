@@ -81,43 +81,77 @@ __device__ void bitonic_u64(uint64_t* a) {
   }
 }
 
-// the tile's K x T neighbour entries (absent -> INT32_MAX, sorted last), padded to N2
+// The tile's distinct input rows, unordered: its K x T neighbour entries (all loads in flight first) go
+// into an open-addressing hash set in LDS (2 N2 int32 slots, load <= 0.42, linear probing by LDS CAS); each
+// first insertion appends the row to uq.  Returns the count.  (Round 2 replaced a bitonic sort of all
+// N2 entries: a tile names 1.6-2 x T distinct rows of 27 T entries, so sorting only those is ~10x less work.)
 template <int T, int N2>
-__device__ void load_tile_entries(const int32_t* __restrict__ nbr, int K, int64_t n, int64_t t, int32_t* a) {
-  for (int i = threadIdx.x; i < N2; i += kLT) {
-    int32_t v = INT32_MAX;
+__device__ int tile_distinct(const int32_t* __restrict__ nbr, int K, int64_t n, int64_t t, int32_t* h, int32_t* uq,
+                             int* cnt) {
+  constexpr int HS = 2 * N2, HB = __builtin_ctz(HS);
+  constexpr int PER = N2 / kLT;  // K T <= N2 entries
+  for (int i = threadIdx.x; i < HS; i += kLT) h[i] = -1;
+  if (threadIdx.x == 0) *cnt = 0;
+  int32_t m[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = threadIdx.x + kLT * j;
+    m[j] = -1;
     if (i < K * T) {
       const int o = i / T, p = i - o * T;
       const int64_t row = t * T + p;
-      if (row < n) {
-        const int32_t m = nbr[(int64_t)o * n + row];
-        if (m >= 0) v = m;
-      }
+      if (row < n) m[j] = nbr[(int64_t)o * n + row];
     }
-    a[i] = v;
   }
   __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int32_t v = m[j];
+    if (v < 0) continue;
+    uint32_t sl = ((uint32_t)v * 2654435761u) >> (32 - HB);
+    while (true) {
+      const int32_t prev = atomicCAS(&h[sl], -1, v);
+      if (prev == -1) {
+        uq[atomicAdd(cnt, 1)] = v;
+        break;
+      }
+      if (prev == v) break;
+      sl = (sl + 1) & (HS - 1);
+    }
+  }
+  __syncthreads();
+  return *cnt;
+}
+
+// ascending bitonic sort of a[0 .. n2) (n2 a power of two, <= N2)
+__device__ void bitonic_i32_n(int32_t* a, int n2) {
+  for (int k = 2; k <= n2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n2; i += kLT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const int32_t u = a[i], v = a[ixj];
+          if ((u > v) == ((i & k) == 0)) {
+            a[i] = v;
+            a[ixj] = u;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 template <int T, int N2>
 __global__ __launch_bounds__(kLT) void local_count_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
                                                           int64_t* __restrict__ cnt,
                                                           unsigned long long* __restrict__ mx) {
-  __shared__ int32_t a[N2];
-  __shared__ int wsum[kLT / 64];
+  __shared__ int32_t h[2 * N2];
+  __shared__ int32_t uq[N2];
+  __shared__ int c;
   const int64_t t = blockIdx.x;
-  load_tile_entries<T, N2>(nbr, K, n, t, a);
-  bitonic_i32<N2>(a);
-  int c = 0;
-  for (int i = threadIdx.x; i < N2; i += kLT) c += a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1]);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
-  __syncthreads();
+  const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c);
   if (threadIdx.x == 0) {
-    int tot = 0;
-#pragma unroll
-    for (int w = 0; w < kLT / 64; ++w) tot += wsum[w];
     cnt[t] = tot;
     atomicMax(mx, (unsigned long long)tot);
   }
@@ -128,33 +162,20 @@ __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restri
                                                          int64_t n_pad, const int64_t* __restrict__ u_start,
                                                          int32_t* __restrict__ u_rows, uint16_t* __restrict__ lidx,
                                                          int32_t* __restrict__ perm, int order) {
-  constexpr int PER = N2 / kLT;
-  __shared__ int32_t a[N2];
+  __shared__ int32_t h[2 * N2];
   __shared__ int32_t uq[N2];
   __shared__ uint64_t mk[T];
+  __shared__ int c;
   const int64_t t = blockIdx.x;
-  load_tile_entries<T, N2>(nbr, K, n, t, a);
-  bitonic_i32<N2>(a);
-  // distinct rows, in order: per-thread runs of PER entries + a block scan
-  const int base = threadIdx.x * PER;
-  int c = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int i = base + j;
-    c += a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1]);
-  }
-  int tot;
-  int off = block_excl_scan<kLT>(c, &tot);
+  const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c);
+  // the distinct rows in ascending order
+  int n2 = 2;
+  while (n2 < tot) n2 <<= 1;
+  for (int i = tot + threadIdx.x; i < n2; i += kLT) uq[i] = INT32_MAX;
+  __syncthreads();
+  bitonic_i32_n(uq, n2);
   const int64_t u0 = u_start[t];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int i = base + j;
-    if (a[i] != INT32_MAX && (i == 0 || a[i] != a[i - 1])) {
-      uq[off] = a[i];
-      u_rows[u0 + off] = a[i];
-      ++off;
-    }
-  }
+  for (int i = threadIdx.x; i < tot; i += kLT) u_rows[u0 + i] = uq[i];
   // rows of the tile ordered by neighbour mask (padding rows last)
   for (int p = threadIdx.x; p < T; p += kLT) {
     const int64_t row = t * T + p;
@@ -192,10 +213,12 @@ __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restri
 }
 
 // ---------------------------------------------------------------- weights
-// wt -> lane-ordered split image: unit ((((o * n_y + cy) * nks + ks) * NT + t) * 3 + p) * 64 + lane holds
-// piece p of W^T[out 16 (cy NT + t) + r][k 32 ks + 8 q .. + 7] for lane = 16 q + r (zero past c_in), so a
-// wave loads its fragments of one step as 3 NT coalesced 1 KiB rows.  wlay 1: wt is [K][c_in][c_out]
-// (the module's layout), else [K][c_out][c_in].
+// wt -> lane-ordered weight image: unit ((((o * n_y + cy) * nks + ks) * NT + t) * WP + p) * 64 + lane holds,
+// for lane = 16 q + r, W^T[out 16 (cy NT + t) + r][k 32 ks + 8 q .. + 7] (zero past c_in) as its three bf16
+// pieces p (WP = 3, split once here) or as two fp32 float4 halves p (WP = 2, split by the reader in
+// registers: 2/3 of the bytes a step's fragments cost), so a wave loads its fragments of one step as WP NT
+// coalesced 1 KiB rows.  wlay 1: wt is [K][c_in][c_out] (the module's layout), else [K][c_out][c_in].
+template <int WP>
 __global__ __launch_bounds__(256) void split_weights_lane_kernel(const float* __restrict__ wt, int K, int c_out,
                                                                  int c_in, int NT, u32x4* __restrict__ img,
                                                                  int wlay) {
@@ -211,20 +234,42 @@ __global__ __launch_bounds__(256) void split_weights_lane_kernel(const float* __
   const int cy = (int)(rest % n_y);
   const int64_t o = rest / n_y;
   const int oc = 16 * (cy * NT + t) + r, k = 32 * ks + 8 * q;
-  u32x4 pc[3] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+  floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
   if (k < c_in) {  // c_in % 16 == 0: an octet is all data or all padding
     if (wlay) {
       const float* src = wt + (o * c_in + k) * c_out + oc;
-      split8(floatx4{src[0], src[c_out], src[2 * c_out], src[3 * c_out]},
-             floatx4{src[4 * c_out], src[5 * c_out], src[6 * c_out], src[7 * c_out]}, pc);
+      a = floatx4{src[0], src[c_out], src[2 * c_out], src[3 * c_out]};
+      b = floatx4{src[4 * c_out], src[5 * c_out], src[6 * c_out], src[7 * c_out]};
     } else {
       const floatx4* src = reinterpret_cast<const floatx4*>(wt + (o * c_out + oc) * c_in + k);
-      split8(src[0], src[1], pc);
+      a = src[0];
+      b = src[1];
     }
   }
-  u32x4* dst = img + ((g >> 6) * 3) * 64 + lane;
+  u32x4* dst = img + ((g >> 6) * WP) * 64 + lane;
+  if constexpr (WP == 3) {
+    u32x4 pc[3];
+    split8(a, b, pc);
 #pragma unroll
-  for (int p = 0; p < 3; ++p) dst[p * 64] = pc[p];
+    for (int p = 0; p < 3; ++p) dst[p * 64] = pc[p];
+  } else {
+    dst[0] = __builtin_bit_cast(u32x4, a);
+    dst[64] = __builtin_bit_cast(u32x4, b);
+  }
+}
+
+// a step's weight fragments as the three bf16 pieces the MFMAs take (WP = 2: split here, in registers)
+template <int NT, int WP>
+__device__ __forceinline__ void weight_pieces(const u32x4 (&w)[NT][WP], u32x4 (&wp)[NT][3]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if constexpr (WP == 3) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wp[t][p] = w[t][p];
+    } else {
+      split8(__builtin_bit_cast(floatx4, w[t][0]), __builtin_bit_cast(floatx4, w[t][1]), wp[t]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- convolution
@@ -235,7 +280,7 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 
 // ABL (timing experiments only, wrong results): bit 1 no weight loads, 2 no LDS input reads, 4 no staging,
 // 8 no MFMAs, 16 no index reads (every group active)
-template <int NT, int T, int D, int WR, int ABL = 0>
+template <int NT, int T, int D, int WR, int ABL = 0, int WP = 3>
 __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
@@ -272,23 +317,23 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  auto ld_w = [&](int s, u32x4 (&w)[NT][3]) {
+  auto ld_w = [&](int s, u32x4 (&w)[NT][WP]) {
     const int sc = s < n_steps ? s : n_steps - 1;
     const int ks = sc / kNJ, j = sc - ks * kNJ;
     const int o = oc + 4 * j < K ? oc + 4 * j : oc;
     const int ow = flip ? K - 1 - o : o;
-    const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * 3 * 64 + lane;
+    const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * WP * 64 + lane;
     if (ABL & 1) {
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) w[t][p] = u32x4{(uint32_t)(s + t), (uint32_t)p, 0u, 1u};
+        for (int p = 0; p < WP; ++p) w[t][p] = u32x4{(uint32_t)(s + t), (uint32_t)p, 0u, 1u};
       return;
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) w[t][p] = src[(t * 3 + p) * 64];
+      for (int p = 0; p < WP; ++p) w[t][p] = src[(t * WP + p) * 64];
   };
   constexpr int SB = WR == 1 ? 3 : 2;  // staging loads in flight per thread
   auto stage = [&](int ks) {
@@ -340,10 +385,12 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
 #pragma unroll
     for (int p = 0; p < 3; ++p) xp[p] = xs[xs_unit(jr, p, q)];
   };
-  auto run = [&](int s, const u32x4 (&w)[NT][3]) {
+  auto run = [&](int s, const u32x4 (&wl)[NT][WP]) {
     const int ks = s / kNJ, j = s - ks * kNJ;
     const int o = oc + 4 * j;
     if (o >= K) return;  // empty slot (wave-uniform)
+    u32x4 w[NT][3];
+    weight_pieces<NT, WP>(wl, w);
     const uint16_t* lo = ls + o * T + 16 * G * rp + r;
     int li[G];
 #pragma unroll
@@ -403,7 +450,7 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
   };
 
   static_assert(kNJ % D == 0, "steps per slice must be a multiple of the weight register sets");
-  u32x4 wf[D][NT][3];
+  u32x4 wf[D][NT][WP];
 #pragma unroll
   for (int d = 0; d < D; ++d) ld_w(d, wf[d]);
   for (int ks = 0; ks < nks; ++ks) {
@@ -452,7 +499,7 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
 // and loads only its own weight fragments (two steps ahead, across units).  At the end of a work item the
 // four offset classes' partial sums meet in LDS in class order (deterministic) and the rows are written
 // through the tile's row order.
-template <int NT>
+template <int NT, int WP = 3>
 __global__ __launch_bounds__(512, 2) void conv_x6l_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
@@ -544,7 +591,7 @@ __global__ __launch_bounds__(512, 2) void conv_x6l_kernel(
   };
 
   // ---- weights: step (u, j) -> fragments of offset oc + 4 j, slice ks, columns of this wave
-  auto ld_w = [&](int64_t u, int j, u32x4 (&w)[NT][3]) {
+  auto ld_w = [&](int64_t u, int j, u32x4 (&w)[NT][WP]) {
     if (u >= n_units) u = n_units - 1;
     int64_t tile;
     int cy, ks;
@@ -552,11 +599,11 @@ __global__ __launch_bounds__(512, 2) void conv_x6l_kernel(
     const int o = oc + 4 * j < K ? oc + 4 * j : oc;
     const int ow = flip ? K - 1 - o : o;
     const int cw = 2 * cy + ch;  // this wave's 16 NT-column slice
-    const u32x4* src = wimg + ((((int64_t)ow * (2 * n_y) + cw) * nks + ks) * NT) * 3 * 64 + lane;
+    const u32x4* src = wimg + ((((int64_t)ow * (2 * n_y) + cw) * nks + ks) * NT) * WP * 64 + lane;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) w[t][p] = src[(t * 3 + p) * 64];
+      for (int p = 0; p < WP; ++p) w[t][p] = src[(t * WP + p) * 64];
   };
 
   floatx4 acc[G][NT];
@@ -566,9 +613,11 @@ __global__ __launch_bounds__(512, 2) void conv_x6l_kernel(
 #pragma unroll
     for (int p = 0; p < 3; ++p) xp[p] = xs[buf][xs_unit(jr, p, q)];
   };
-  auto run = [&](int buf, int ks, int j, const u32x4 (&w)[NT][3]) {
+  auto run = [&](int buf, int ks, int j, const u32x4 (&wl)[NT][WP]) {
     const int o = oc + 4 * j;
     if (o >= K) return;  // empty slot (wave-uniform)
+    u32x4 w[NT][3];
+    weight_pieces<NT, WP>(wl, w);
     const uint16_t* lo = reinterpret_cast<const uint16_t*>(ls[buf]) + o * T + r;
     int li[G];
 #pragma unroll
@@ -626,7 +675,7 @@ __global__ __launch_bounds__(512, 2) void conv_x6l_kernel(
   stage_issue_values(0);
   stage_store(0);
   if (tid < 2 * kXU) xs[tid / kXU][kUCap * kXU + tid % kXU] = u32x4{0u, 0u, 0u, 0u};
-  u32x4 wf[2][NT][3];
+  u32x4 wf[2][NT][WP];
   ld_w(0, 0, wf[0]);
   ld_w(0, 1, wf[1]);
   __syncthreads();
@@ -1523,6 +1572,7 @@ static int g_local_order = 1;  // msp_tile_local: order rows inside a tile by ne
 static int g_local_nt = 0;     // forced column tiles per wave (0: local_nt)
 static int g_local_abl = 0;    // ablation variant (timing only; msp_debug_conv_local_abl)
 static int g_local_form = 2;   // 2: conv_x6l for 64 output channels, 1: wherever it applies, 0: conv_x6s
+static int g_local_wp = 3;     // weight image: 3 = bf16 pieces, 2 = fp32 split in registers (msp_debug_conv_local_wp)
 
 inline int cu_count() {
   static int n = 0;
@@ -1591,6 +1641,12 @@ int msp_debug_conv_local(int wr, int order, int nt) {
   if (wr == 1 || wr == 2) g_local_wr = wr;
   if (nt >= 0) g_local_nt = nt;
   if (order >= 0) g_local_order = order ? 1 : 0;
+  return MSP_OK;
+}
+
+// weight image of msp_conv_local: 3 = split once into bf16 pieces, 2 = fp32, split by the kernels in registers
+int msp_debug_conv_local_wp(int wp) {
+  if (wp == 2 || wp == 3) g_local_wp = wp;
   return MSP_OK;
 }
 
@@ -1710,8 +1766,8 @@ int msp_conv_chunk_local(const float* x, int c_in, const float* wt, int K, int f
   const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
   u32x4* img = static_cast<u32x4*>(ws);
   const int64_t lanes = (int64_t)K * n_y * nks * NT * 64;
-  split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
-                                                                           (flip >> 1) & 1);
+  split_weights_lane_kernel<3><<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                              (flip >> 1) & 1);
   const unsigned grid = (unsigned)(n_units * n_y);
 #define LQ(DV, A)                                                                                              \
   if (g_chunk_dv == DV && g_chunk_abl == A)                                                                    \
@@ -1825,15 +1881,20 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
     const int n_y = c_out / (32 * NT), nks = (c_in + 31) / 32;
     u32x4* img = static_cast<u32x4*>(ws);
     const int64_t lanes = (int64_t)K * (2 * n_y) * nks * NT * 64;
-    split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
-                                                                               (flip >> 1) & 1);
+    const int wp = g_local_wp;
+    if (wp == 2)
+      split_weights_lane_kernel<2><<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                                  (flip >> 1) & 1);
+    else
+      split_weights_lane_kernel<3><<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                                  (flip >> 1) & 1);
     const int64_t n_pad = n_tiles * tile_rows, n_items = n_tiles * n_y;
     const unsigned grid = (unsigned)(n_items < cu_count() ? n_items : cu_count());
-#define LP(N)                                                                                                   \
-  if (NT == N)                                                                                                \
-    conv_x6l_kernel<N><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad, \
-                                            n_y, n_items, out);
-    LP(1) LP(2) LP(3)
+#define LP(N, P)                                                                                                \
+  if (NT == N && wp == P)                                                                                     \
+    conv_x6l_kernel<N, P><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm,    \
+                                               n_pad, n_y, n_items, out);
+    LP(1, 3) LP(2, 3) LP(3, 3) LP(1, 2) LP(2, 2) LP(3, 2)
 #undef LP
     return check_launch("msp_conv_local");
   }
@@ -1841,17 +1902,23 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
   u32x4* img = static_cast<u32x4*>(ws);
   const int64_t lanes = (int64_t)K * n_y * nks * NT * 64;
-  split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
-                                                                             (flip >> 1) & 1);
+  const int wp = g_local_abl == 0 ? g_local_wp : 3;
+  if (wp == 2)
+    split_weights_lane_kernel<2><<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                                (flip >> 1) & 1);
+  else
+    split_weights_lane_kernel<3><<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                                (flip >> 1) & 1);
   const int64_t n_pad = n_tiles * tile_rows;
   const unsigned grid = (unsigned)(n_tiles * n_y);
   const int wr = g_local_wr;
-#define LX(N, W, A)                                                                                           \
-  if (NT == N && wr == W && g_local_abl == A)                                                                 \
-    conv_x6s_kernel<N, 128, 2, W, A><<<grid, 256 * W, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, \
-                                                              u_rows, perm, n_pad, n_y, out);
-  LX(2, 1, 0) LX(1, 1, 0) LX(2, 2, 0) LX(1, 2, 0)
-  LX(2, 2, 1) LX(2, 2, 2) LX(2, 2, 4) LX(2, 2, 8) LX(2, 2, 16) LX(2, 2, 15) LX(2, 2, 31)
+#define LX(N, W, A, P)                                                                                        \
+  if (NT == N && wr == W && g_local_abl == A && wp == P)                                                      \
+    conv_x6s_kernel<N, 128, 2, W, A, P><<<grid, 256 * W, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx,       \
+                                                                 u_start, u_rows, perm, n_pad, n_y, out);
+  LX(2, 1, 0, 3) LX(1, 1, 0, 3) LX(2, 2, 0, 3) LX(1, 2, 0, 3) LX(2, 1, 0, 2) LX(1, 1, 0, 2) LX(2, 2, 0, 2)
+  LX(1, 2, 0, 2)
+  LX(2, 2, 1, 3) LX(2, 2, 2, 3) LX(2, 2, 4, 3) LX(2, 2, 8, 3) LX(2, 2, 16, 3) LX(2, 2, 15, 3) LX(2, 2, 31, 3)
 #undef LX
   return check_launch("msp_conv_local");
 }

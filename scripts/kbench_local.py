@@ -14,8 +14,9 @@ lib = _lib.load()
 import ctypes
 lib.msp_debug_conv_local.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
 lib.msp_debug_conv_local_abl.argtypes = [ctypes.c_int]
+lib.msp_debug_conv_local_wp.argtypes = [ctypes.c_int]
 ABLS = [int(a) for a in os.environ.get("ABL", "").split(",") if a]  # ablation variants of local 2:1:0
-# local variants "wr:order:nt" (env VARIANTS)
+# local variants "wr:order:nt[:persistent[:wp]]" (env VARIANTS; wp = weight image, 3 pieces / 2 fp32)
 VARS = [tuple(int(v) for v in e.split(":")) for e in os.environ.get("VARIANTS", "1:1:0,2:1:0,2:1:1,2:0:0").split(",")]
 b = make_batch(8, 50, seed=1)
 t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
@@ -82,6 +83,7 @@ for L, size in enumerate(sizes):
             if var is not None:
                 lib.msp_debug_conv_local(var[0], -1, var[2])
                 lib.msp_debug_conv_local_abl(-2 if len(var) > 3 and var[3] else -1)
+                lib.msp_debug_conv_local_wp(var[4] if len(var) > 4 else 3)
                 rules._locals[128] = loc_sorted if var[1] else loc_key
             f = lambda: ops.conv_tile(x, wt, 27, flip, cout, rules, V)
             ms = timeit(f)
@@ -99,6 +101,7 @@ for L, size in enumerate(sizes):
             lib.msp_debug_conv_local_abl(0)
         print(f"   {cin:3d}->{cout:3d}  " + "  ".join(res), flush=True)
         lib.msp_debug_conv_local(2, 1, 0)
-        lib.msp_debug_conv_local_abl(-2)
+        lib.msp_debug_conv_local_abl(-3)
+        lib.msp_debug_conv_local_wp(3)
         rules._locals[128] = loc_sorted
 ops.CONV_LOCAL = True
