@@ -15,7 +15,11 @@ only exchange is the gradient all-reduce, so this is plain DDP:
   bound by the slowest rank;
 * `wrap()` builds DDP with local BatchNorm statistics (broadcast_buffers=False,
   as in a single-GPU reference run at the per-rank batch size; no SyncBN) and
-  gradient buckets sized for ring all-reduce over xGMI.
+  gradient buckets sized for ring all-reduce over xGMI;
+* `GradSync` is the same exchange for steps captured into HIP graphs (no DDP
+  hooks inside a capture): the gradients are views of one flat buffer that the
+  captured backward accumulates into in place, and one all-reduce over it runs
+  eagerly between the graph's replay and the optimizer step.
 """
 from __future__ import annotations
 
@@ -42,10 +46,11 @@ def init_from_env(device_type: str = "cuda", backend: str | None = None, device_
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = backend or ("nccl" if device_type == "cuda" else "gloo")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
+        # RCCL's communicator is created lazily, at the first collective (no device_id): bound eagerly, it
+        # made every later device-to-host read wait for ALL queued work on the device, not just its own
+        # stream -- the metadata prefetch's count reads then stalled behind the running step (82.8 vs
+        # 60.1 ms/step with a one-rank group, profiles/r02/bench_dp_selftest_r02.log)
+        dist.init_process_group(backend)
     return rank, world, local, device
 
 
@@ -75,6 +80,53 @@ def wrap(model, device, bucket_cap_mb: int = 64):
     ids = [device.index] if device.type == "cuda" else None
     return torch.nn.parallel.DistributedDataParallel(model, device_ids=ids, broadcast_buffers=False,
                                                      bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+
+
+class GradSync:
+    """Data-parallel gradient averaging for graph-captured steps.
+
+    DDP all-reduces from autograd hooks while backward runs; a HIP graph that
+    captures the backward would capture those collectives as well.  Here the
+    step's forward + backward is the graph and the exchange stays outside it:
+    the parameters start equal on every rank (broadcast from rank 0, as DDP's
+    constructor does), every gradient is a view of one flat fp32 buffer (so
+    the captured backward writes it in place and the step zeroes it with
+    ``zero_grad(set_to_none=False)``), and `average()` issues ONE all-reduce
+    over the whole buffer (120 MB for the headline UNet: one large RCCL ring
+    all-reduce over xGMI, ~1 ms) followed by the 1/world scaling -- the same
+    mean DDP computes.  BN buffers stay local (as `wrap`, broadcast_buffers=False)."""
+
+    def __init__(self, model, device):
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        if self.world > 1:
+            with torch.no_grad():
+                for p in self.params:
+                    dist.broadcast(p.data, 0)
+        total = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(total, device=device, dtype=torch.float32)
+        off = 0
+        for p in self.params:
+            if p.dtype != torch.float32:
+                raise TypeError("GradSync: fp32 parameters only")
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def check_views(self):
+        """The gradients must still be the flat buffer's views (a zero_grad(set_to_none=True) or a
+        non-accumulating backward would have replaced them)."""
+        off = 0
+        for p in self.params:
+            g = p.grad
+            if g is None or g.data_ptr() != self.flat[off:off + p.numel()].data_ptr():
+                raise RuntimeError("GradSync: a gradient is no longer a view of the flat buffer")
+            off += p.numel()
+
+    def average(self):
+        if dist.is_initialized():
+            dist.all_reduce(self.flat)
+        if self.world > 1:
+            self.flat.mul_(1.0 / self.world)
 
 
 def max_over_ranks(x: float) -> float:

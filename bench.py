@@ -283,7 +283,8 @@ def main():
     ap.add_argument("--graph", type=int, choices=[0, 1], default=None,
                     help="1: capture every step afresh into a HIP graph (built after the step's metadata is "
                          "prefetched, replayed on the compute stream while the next step is prefetched and "
-                         "captured; one rank only: the DDP all-reduce stays eager) -- removes the per-kernel launch gaps; default 1")
+                         "captured; N ranks: forward + backward captured, the gradient all-reduce and Adam eager after each "
+                         "replay) -- removes the per-kernel launch gaps; default 1")
     ap.add_argument("--workload", choices=["unet", "contrastive"], default=None,
                     help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
                          "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
@@ -304,6 +305,15 @@ def main():
     # one device); the measured configuration is RCCL with one GPU per rank
     rank, world, local, dev = dp.init_from_env("cuda", backend=os.environ.get("BENCH_BACKEND") or None,
                                                device_index=0 if os.environ.get("BENCH_SHARE_DEVICE") else None)
+    if os.environ.get("BENCH_DP_SELFTEST") and world == 1:
+        # a one-rank RCCL group: runs the N-rank graph path (eager all-reduce between per-step captures) on a
+        # one-GPU box, as a rehearsal of what the driver's multi-GPU runs execute
+        sock = socket.socket()
+        sock.bind(("127.0.0.1", 0))
+        port = sock.getsockname()[1]
+        sock.close()
+        be = "gloo" if os.environ["BENCH_DP_SELFTEST"] == "gloo" else "nccl"
+        dist.init_process_group(be, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     if rank == 0 and world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
               file=sys.stderr)
@@ -336,25 +346,30 @@ def main():
             text = (tok.to(dev), torch.arange(args.batch, device=dev))
         batches.append((x, y, v0, text))
 
+    # HIP-graph steps (--graph), metadata prefetched.  One rank: the whole step (Adam included) is the graph.
+    # N ranks: forward + backward are the graph, and the gradient all-reduce (one RCCL call over a flat buffer,
+    # dp.GradSync) and Adam run eagerly after its replay -- DDP's hooks would otherwise be captured
+    use_graph = bool(args.graph if args.graph is not None else not contrastive) \
+        and not args.no_prefetch \
+        and args.prefetch_at == "end"
+    graph_dp = use_graph and (world > 1 or dist.is_initialized())
+    wrap = (lambda m: m) if graph_dp else (lambda m: dp.wrap(m, dev))
     torch.manual_seed(0)
     if contrastive:
         pc = EasyDict(name="SparseConvFCNet", m=args.m, dimension=3, full_scale=4096, block_reps=args.reps,
                       residual_blocks=bool(args.residual))
         tc = EasyDict(name="TextTransformer", context_length=seq_len, width=512, layers=12, vocab_size=vocab)
         cls, _ = MODEL_REGISTRY.get("MultiLabelContrastive")
-        model = dp.wrap(cls(pc, tc).to(dev), dev)
+        model = wrap(cls(pc, tc).to(dev))
     else:
         pc = EasyDict(name="SparseConvUNet", m=args.m, dimension=3, full_scale=4096, block_reps=args.reps,
                       residual_blocks=bool(args.residual))
         cls, _ = MODEL_REGISTRY.get("MultiLabel")
-        model = dp.wrap(cls(pc).to(dev), dev)
+        model = wrap(cls(pc).to(dev))
     n_params = sum(p.numel() for p in model.parameters())
     # the reference's optimizer (train.py:39, Adam lr 1e-3); one fused multi-tensor kernel per step
     # (--foreach-adam: torch's default foreach form, ~21 launches per step)
-    # HIP-graph steps (--graph): one rank only (the DDP gradient all-reduce stays eager), metadata prefetched
-    use_graph = bool(args.graph if args.graph is not None else not contrastive) and world == 1 \
-        and not args.no_prefetch \
-        and args.prefetch_at == "end"
+    gsync = dp.GradSync(model, dev) if graph_dp else None
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
                                                            {"fused": True, "capturable": use_graph}))
     cls_loss, _ = LOSS_REGISTRY.get("Classification")
@@ -375,7 +390,7 @@ def main():
     def step(i):
         x, y, _, text = batches[i % len(batches)]
         h0 = time.perf_counter()
-        opt.zero_grad(set_to_none=True)
+        opt.zero_grad(set_to_none=gsync is None)
         logits, meta = model((x, text), istrain=True)
         h1 = time.perf_counter()
         if not args.no_prefetch and args.prefetch_at == "fwd":
@@ -385,6 +400,8 @@ def main():
             loss = loss + con_loss(*meta)
         loss.backward()
         h2 = time.perf_counter()
+        if gsync is not None:
+            gsync.average()
         opt.step()
         h3 = time.perf_counter()
         if not args.no_prefetch and args.prefetch_at == "end":
@@ -403,15 +420,16 @@ def main():
 
     capture_s = []
 
-    def body(i):  # one training step without its prefetch (what a graph captures)
+    def body(i):  # one training step without its prefetch (what a graph captures; N ranks: up to backward)
         x, y, _, text = batches[i % len(batches)]
-        opt.zero_grad(set_to_none=True)
+        opt.zero_grad(set_to_none=gsync is None)
         logits, meta = model((x, text), istrain=True)
         loss = cls_loss(logits, y)
         if contrastive:
             loss = loss + con_loss(*meta)
         loss.backward()
-        opt.step()
+        if gsync is None:
+            opt.step()
         return loss
 
     def capture(i):
@@ -425,6 +443,8 @@ def main():
             body(i)
             g.capture_end()
         keep = scn_meta.captured_metadata()
+        if gsync is not None:
+            gsync.check_views()
         if not keep:
             raise RuntimeError("bench.py --graph: the captured step did not consume its prefetched metadata")
         capture_s.append(time.perf_counter() - t)
@@ -442,6 +462,9 @@ def main():
             replay_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
             replay_ev[-1][0].record(cur)
         g.replay()
+        if gsync is not None:  # N ranks: the gradient exchange and Adam after the replayed backward
+            gsync.average()
+            opt.step()
         done = torch.cuda.Event(enable_timing=host_t is not None)
         done.record(cur)
         if host_t is not None:
@@ -531,7 +554,7 @@ def main():
 
     # one untimed forward for the per-level statistics and the MAC counter
     scn.forward_pass_multiplyAdd_count = 0
-    inner = model.module if world > 1 else model
+    inner = getattr(model, "module", model)
     x0 = batches[0][0]
     enc = inner.pc_encoder.encoder
     with torch.no_grad():
@@ -576,7 +599,10 @@ def main():
                 "scenes_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world}",
-                "comm_backend": dist.get_backend() if world > 1 else None,
+                "grad_exchange": None if not dist.is_initialized() else (
+                    "one all-reduce over a flat gradient buffer after each graph replay, then Adam (dp.GradSync)"
+                    if graph_dp else "DDP, 64 MB buckets overlapped with backward"),
+                "comm_backend": dist.get_backend() if dist.is_initialized() else None,
                 "input_pipeline": "none" if args.no_prefetch else
                 "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step "
                 f"(after its {'optimizer' if args.prefetch_at == 'end' else 'forward'} call is queued; host "
@@ -643,7 +669,7 @@ def main():
         if world == 1 and not args.no_cpu and not contrastive:
             res["cpu_baseline"] = cpu_baseline(args, host_batches[0], args.cpu_iters)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

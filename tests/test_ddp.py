@@ -76,3 +76,57 @@ def test_ddp_world2_gloo():
         p.join(timeout=600)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert dict(out) == {0: True, 1: True}
+
+
+def _gsync_worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "3d-weakly-supervised-semantic-segmentation_amd"), root):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from wsss3d import dp
+
+    try:
+        r, w, _, dev = dp.init_from_env("cpu")
+        torch.manual_seed(1 + r)  # different initial parameters: GradSync broadcasts rank 0's
+        net = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.ReLU(), torch.nn.Linear(7, 3))
+        gs = dp.GradSync(net, dev)
+        p0 = torch.cat([p.detach().flatten() for p in net.parameters()])
+        ref = p0.clone()
+        dist.broadcast(ref, 0)
+        ok = torch.equal(p0, ref) and gs.flat.numel() == p0.numel()
+        x = torch.randn(4, 5, generator=torch.Generator().manual_seed(r))
+        for _ in range(2):  # accumulation into the views, then zeroing in place
+            net.zero_grad(set_to_none=False)
+            net(x).square().sum().backward()
+        gs.check_views()
+        local = gs.flat.clone()
+        gs.average()
+        both = [torch.empty_like(local) for _ in range(w)]
+        dist.all_gather(both, local)
+        ok &= torch.allclose(gs.flat, sum(both) / w, rtol=1e-6, atol=1e-7)
+        out[rank] = bool(ok)
+        dist.destroy_process_group()
+    except Exception as e:
+        out[rank] = f"{type(e).__name__}: {e}"
+        raise
+
+
+def test_grad_sync_world2():
+    """dp.GradSync (the gradient exchange of bench.py's graph-captured N-rank steps): parameters start equal,
+    gradients are views of one flat buffer, average() gives the mean of the ranks' gradients."""
+    ctx = mp.get_context("spawn")
+    manager = ctx.Manager()
+    out = manager.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_gsync_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert dict(out) == {0: True, 1: True}, dict(out)

@@ -105,3 +105,97 @@ def test_ddp_world2_hip_model():
             p.kill()
     assert dict(out) == {0: True, 1: True}, dict(out)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _graph_worker(rank, world, port, out):
+    """bench.py's N-rank graph path: forward + backward captured into a HIP graph on the prefetched metadata,
+    gradients as views of one flat buffer (dp.GradSync), one all-reduce + Adam eagerly after the replay."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "3d-weakly-supervised-semantic-segmentation_amd"), root):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    import sparseconvnet as scn
+    from sparseconvnet import metadata as scn_meta
+    from wsss3d import EasyDict, MODEL_REGISTRY, dp
+    from wsss3d.synthetic import make_batch
+
+    try:
+        r, w, _, dev = dp.init_from_env("cuda", backend="gloo", device_index=0)
+        pc = EasyDict(name="SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=2,
+                      residual_blocks=True)
+        cls, _ = MODEL_REGISTRY.get("MultiLabel")
+        torch.manual_seed(0)
+        local = cls(pc).to(dev)
+        torch.manual_seed(0 if r == 0 else 7)  # rank 1 differs: GradSync must broadcast rank 0's parameters
+        model = cls(pc).to(dev)
+        gsync = dp.GradSync(model, dev)
+        ok = all(torch.equal(p, q) for p, q in zip(model.parameters(), local.parameters()))
+        bs = [make_batch(2, 20, seed=10 * r + k) for k in range(2)]
+        xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(dev), feature=torch.from_numpy(b["feats"]).to(dev),
+                       batch_offsets=b["batch_offsets"]) for b in bs]
+        ys = [torch.from_numpy(b["scene_labels"]).to(dev) for b in bs]
+
+        def loss_of(net, k):
+            logits, _ = net((xs[k], None), istrain=True)
+            return F.multilabel_soft_margin_loss(logits, ys[k])
+
+        model.zero_grad(set_to_none=False)
+        loss_of(model, 0).backward()         # records the rulebook plan
+        torch.cuda.synchronize()
+        assert scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False) is not None
+        ev = scn_meta.prefetch_event(dev)
+        g = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(dev)
+        with torch.cuda.stream(cap):
+            g.capture_begin(capture_error_mode="relaxed")
+            model.zero_grad(set_to_none=False)
+            loss_of(model, 1).backward()
+            g.capture_end()
+        assert scn_meta.captured_metadata()
+        gsync.check_views()
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_event(ev)
+        g.replay()
+        gsync.average()
+        loss_of(local, 1).backward()
+        for (k, p), q in zip(model.named_parameters(), local.parameters()):
+            gl = q.grad.clone()
+            dist.all_reduce(gl)
+            gl /= w
+            if not torch.allclose(p.grad, gl, rtol=1e-6, atol=1e-9):
+                ok = False
+                print(f"rank {r}: grad {k} differs by {(p.grad - gl).abs().max().item():.3e}", flush=True)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=True)
+        opt.step()
+        flat = torch.cat([p.detach().flatten() for p in model.parameters()])
+        ref = flat.clone()
+        dist.broadcast(ref, 0)
+        ok &= torch.equal(flat, ref)
+        torch.cuda.synchronize()
+        del g
+        out[rank] = bool(ok)
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        out[rank] = f"{type(e).__name__}: {e}"
+        raise
+
+
+def test_graph_dp_world2_hip_model():
+    ctx = mp.get_context("spawn")
+    manager = ctx.Manager()
+    out = manager.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert dict(out) == {0: True, 1: True}, dict(out)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
