@@ -654,6 +654,29 @@ def test_tile_local_rulebook(order):
     _check_local_rulebook(rules.nbr, loc, lvl.n)
 
 
+@pytest.mark.parametrize("mode", ["random", "dup", "distinct"])
+@pytest.mark.parametrize("T,K", [(64, 27), (128, 32), (256, 27)])
+def test_tile_local_rulebook_maps(T, K, mode):
+    """msp_tile_local's LDS hash-set build on arbitrary maps, every tile size the ABI takes: random rows,
+    heavy duplication (5 distinct rows, long probe chains of equal keys) and all K x T entries distinct (the
+    largest sort); V not a multiple of T."""
+    from sparseconvnet import _lib, metadata
+    torch.manual_seed(T + K)
+    V = 1000
+    if mode == "random":
+        nbr = torch.randint(0, 40000, (K, V), dtype=torch.int32, device=DEV)
+    elif mode == "dup":
+        nbr = torch.randint(0, 5, (K, V), dtype=torch.int32, device=DEV)
+    else:
+        nbr = (torch.arange(K * V, dtype=torch.int32, device=DEV).view(K, V) * 7919) % (K * V * 2 + 1)
+    if mode != "distinct":
+        nbr[torch.rand(K, V, device=DEV) < 0.3] = -1
+    loc = metadata.local_rulebook(nbr, K, V, nbr.device, _lib.stream(), T)
+    _check_local_rulebook(nbr, loc, V)
+    if mode == "distinct":
+        assert loc["max_u"] == K * T
+
+
 @pytest.mark.parametrize("form", [-1, -2], ids=["x6s", "x6l"])
 @pytest.mark.parametrize("cin,cout,flip", [(64, 64, 2), (64, 64, 1), (96, 96, 2), (192, 96, 1), (48, 64, 2),
                                            (64, 48, 1), (128, 16, 2), (32, 160, 1)])
