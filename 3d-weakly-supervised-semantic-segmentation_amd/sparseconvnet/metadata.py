@@ -106,9 +106,16 @@ def chunk_local_index(tiles, n, device, s, with_max=False):
 
 class PairLists:
     """Per-offset (in, out) pair lists of an offset-major map, plus the chunk
-    and block partitions used by msp_conv_pairs / msp_conv_wgrad."""
+    and block partitions used by msp_conv_pairs / msp_conv_wgrad.
 
-    def __init__(self, m, K, n, device, s):
+    The per-offset counts (the SCN rulebook size, the MAC counter) are taken
+    when the rules are built; the lists themselves are filled on first use of
+    `pair_in` / `pair_out` (recorded in the plan, so a prefetch of the next
+    batch builds them ahead): at levels whose convolutions and weight gradients
+    all run on the tile-local / chunk forms nothing reads them.  The fill needs
+    no host read, so a first use inside a graph capture is captured."""
+
+    def __init__(self, m, K, n, device, s, plan=None, key=None):
         nrb = max(1, (n + 2047) // 2048)
         mm = K * nrb
         ws = _ws((2 * mm + 1) * 8 + query("msp_scan_workspace_size", I64(mm)), device)
@@ -117,11 +124,9 @@ class PairLists:
         starts = self.off_start.tolist()
         self.total = int(starts[-1])
         self.counts = [starts[o + 1] - starts[o] for o in range(K)]
-        self.pair_in = torch.empty(max(self.total, 1), dtype=torch.int32, device=device)
-        self.pair_out = torch.empty(max(self.total, 1), dtype=torch.int32, device=device)
-        if self.total:
-            call("msp_pair_lists", ptr(m), K, n, ptr(self.pair_in), ptr(self.pair_out), self.total,
-                 ptr(self.off_start), ptr(ws), ws.numel(), s)
+        self._m, self._n, self._ws, self._dev = m, n, ws, device  # the filling call reuses the count's workspace
+        self._plan, self._key = plan, key
+        self._pin = self._pout = None
         self.K = K
         # 16-pair chunks per offset (msp_conv_pairs)
         cs = [0]
@@ -129,6 +134,26 @@ class PairLists:
             cs.append(cs[-1] + (c + CHUNK - 1) // CHUNK)
         self.n_chunks = cs[-1]
         self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(device, non_blocking=True)
+
+    def fill(self):
+        if self._pin is None:
+            if self._plan is not None:
+                self._plan.append(("pairs", self._key))
+            pin = torch.empty(max(self.total, 1), dtype=torch.int32, device=self._dev)
+            pout = torch.empty(max(self.total, 1), dtype=torch.int32, device=self._dev)
+            if self.total:
+                call("msp_pair_lists", ptr(self._m), self.K, self._n, ptr(pin), ptr(pout), self.total,
+                     ptr(self.off_start), ptr(self._ws), self._ws.numel(), _lib.stream(self._dev))
+            self._pin, self._pout, self._ws = pin, pout, None
+        return self
+
+    @property
+    def pair_in(self):
+        return self.fill()._pin
+
+    @property
+    def pair_out(self):
+        return self.fill()._pout
 
 
 DENSE_LOG2_WINDOW = 12  # rows of one mask-sorting window of msp_dense_order
@@ -152,7 +177,7 @@ class SubmRules:
         self._wchunk = None
         self._dense = None
         self._map, self._n = self.nbr, V
-        self.pairs = PairLists(self.nbr, K, V, dev, s)
+        self.pairs = PairLists(self.nbr, K, V, dev, s, self._plan, self._key)
         self.n_rules = self.pairs.total  # = SCN rulebook size (centre included)
 
     def dense_order(self):
@@ -248,7 +273,7 @@ class DownRules:
         self._tiles = {}
         self._map, self._n = self.down, coarse.n
         # pair_in = fine row, pair_out = coarse row, grouped by child offset
-        self.pairs = PairLists(self.down, K, coarse.n, dev, s)
+        self.pairs = PairLists(self.down, K, coarse.n, dev, s, self._plan, self._key)
 
     tiles_for = SubmRules.tiles_for
     note_use = SubmRules.note_use
@@ -447,6 +472,8 @@ class Metadata:
                 self._rules(entry[1]).chunk_local()
             elif entry[0] == "wchunk":
                 self._rules(entry[1]).wgrad_index()
+            elif entry[0] == "pairs":
+                self._rules(entry[1]).pairs.fill()
 
     def tensors(self):
         """Every device tensor this metadata holds (for stream bookkeeping)."""
@@ -464,7 +491,7 @@ class Metadata:
             elif isinstance(v, (Level, SubmRules, DownRules, PairLists, InputRules)) and id(v) not in seen:
                 seen.add(id(v))
                 for k, x in vars(v).items():
-                    if k != "_plan" and k != "plan":
+                    if k not in ("_plan", "plan", "_m"):
                         walk(x)
         walk(self.levels)
         walk(self.input)

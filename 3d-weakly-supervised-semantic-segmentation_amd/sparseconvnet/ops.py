@@ -91,6 +91,8 @@ def prepare(rules, purpose, c_in, c_out):
                 return
         if WGRAD_LOCAL and int(_lib.query("msp_wgrad_local_ok", _lib.I64(n), K, c_in, c_out)):
             rules.local()
+        else:
+            rules.pairs.fill()
 
 
 def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
