@@ -1572,7 +1572,9 @@ static int g_local_order = 1;  // msp_tile_local: order rows inside a tile by ne
 static int g_local_nt = 0;     // forced column tiles per wave (0: local_nt)
 static int g_local_abl = 0;    // ablation variant (timing only; msp_debug_conv_local_abl)
 static int g_local_form = 2;   // 2: conv_x6l for 64 output channels, 1: wherever it applies, 0: conv_x6s
+static int g_local_d = 2;      // weight register sets of conv_x6s (prefetch depth; msp_debug_conv_local_d)
 static int g_local_wp = 3;     // weight image: 3 = bf16 pieces, 2 = fp32 split in registers (msp_debug_conv_local_wp)
+static int g_local_min_ch = 64;  // msp_conv_local_preferred: channels on both sides from (msp_debug_conv_local_min_ch)
 
 inline int cu_count() {
   static int n = 0;
@@ -1647,6 +1649,11 @@ int msp_debug_conv_local(int wr, int order, int nt) {
 // weight image of msp_conv_local: 3 = split once into bf16 pieces, 2 = fp32, split by the kernels in registers
 int msp_debug_conv_local_wp(int wp) {
   if (wp == 2 || wp == 3) g_local_wp = wp;
+  return MSP_OK;
+}
+
+int msp_debug_conv_local_d(int d) {
+  if (d == 1 || d == 2) g_local_d = d;
   return MSP_OK;
 }
 
@@ -1855,7 +1862,15 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
 }
 
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {
-  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 64 && c_out >= 64 && n_rows >= 4096) ? 1 : 0;
+  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= g_local_min_ch && c_out >= g_local_min_ch &&
+          n_rows >= 4096) ? 1 : 0;
+}
+
+// Experiment hook: the smallest channel count msp_conv_local_preferred takes (64; 32 adds level 0 of m = 32,
+// on the persistent form at 32 output channels)
+int msp_debug_conv_local_min_ch(int c) {
+  if (c == 32 || c == 64) g_local_min_ch = c;
+  return MSP_OK;
 }
 
 size_t msp_conv_local_workspace_size(int K, int c_in, int c_out) {
@@ -1875,7 +1890,8 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
-  if (((g_local_form == 1 && c_out % 32 == 0) || (g_local_form == 2 && c_out == 64)) && g_local_abl == 0) {
+  if (((g_local_form == 1 && c_out % 32 == 0) ||
+       (g_local_form == 2 && (c_out == 64 || (c_out == 32 && g_local_min_ch <= 32)))) && g_local_abl == 0) {
     // persistent pipelined form: 16 NT columns per wave, two column halves per block
     const int NT = c_out % 96 == 0 ? 3 : (c_out % 64 == 0 ? 2 : 1);
     const int n_y = c_out / (32 * NT), nks = (c_in + 31) / 32;
@@ -1912,13 +1928,15 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int64_t n_pad = n_tiles * tile_rows;
   const unsigned grid = (unsigned)(n_tiles * n_y);
   const int wr = g_local_wr;
-#define LX(N, W, A, P)                                                                                        \
-  if (NT == N && wr == W && g_local_abl == A && wp == P)                                                      \
-    conv_x6s_kernel<N, 128, 2, W, A, P><<<grid, 256 * W, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx,       \
-                                                                 u_start, u_rows, perm, n_pad, n_y, out);
-  LX(2, 1, 0, 3) LX(1, 1, 0, 3) LX(2, 2, 0, 3) LX(1, 2, 0, 3) LX(2, 1, 0, 2) LX(1, 1, 0, 2) LX(2, 2, 0, 2)
-  LX(1, 2, 0, 2)
-  LX(2, 2, 1, 3) LX(2, 2, 2, 3) LX(2, 2, 4, 3) LX(2, 2, 8, 3) LX(2, 2, 16, 3) LX(2, 2, 15, 3) LX(2, 2, 31, 3)
+  const int dd = g_local_abl == 0 ? g_local_d : 2;
+#define LX(N, W, A, P, DD)                                                                                    \
+  if (NT == N && wr == W && g_local_abl == A && wp == P && dd == DD)                                          \
+    conv_x6s_kernel<N, 128, DD, W, A, P><<<grid, 256 * W, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx,      \
+                                                                  u_start, u_rows, perm, n_pad, n_y, out);
+  LX(2, 1, 0, 3, 2) LX(1, 1, 0, 3, 2) LX(2, 2, 0, 3, 2) LX(1, 2, 0, 3, 2) LX(2, 1, 0, 2, 2) LX(1, 1, 0, 2, 2)
+  LX(2, 2, 0, 2, 2) LX(1, 2, 0, 2, 2) LX(2, 2, 0, 3, 1) LX(1, 2, 0, 3, 1) LX(2, 2, 0, 2, 1)
+  LX(2, 2, 1, 3, 2) LX(2, 2, 2, 3, 2) LX(2, 2, 4, 3, 2) LX(2, 2, 8, 3, 2) LX(2, 2, 16, 3, 2) LX(2, 2, 15, 3, 2)
+  LX(2, 2, 31, 3, 2)
 #undef LX
   return check_launch("msp_conv_local");
 }

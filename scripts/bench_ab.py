@@ -4,7 +4,7 @@ Variants (comma list in AB): tile (no dense row groups), nbr0 (dense groups in
 key order), nbr (production: mask-sorted order), g<N> (dense kernel variant N,
 msp_debug_conv_nbr_variant), fuse / nofuse (residual fork/join fusions on / off),
 fused / foreach (Adam implementation), cw (weight gradients on a side stream), nolocal (gather forms instead of
-the tile-local convolution), x6s / x6l / x6l64 (tile-local kernel forms), norec (no HIP-event recording).  Usage: AB=tile,nbr python scripts/bench_ab.py"""
+the tile-local convolution), x6s / x6l / x6l64 (tile-local kernel forms), norec (no HIP-event recording), l0 (tile-local convolution at 32 channels too: level 0 of m = 32).  Usage: AB=tile,nbr python scripts/bench_ab.py"""
 import io, json, os, sys, contextlib
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
 import __graft_entry__ as g_; g_.add_path()
@@ -20,6 +20,7 @@ for v in os.environ.get("AB", "tile,nbr").split(","):
     modules.FUSE_RESIDUAL = v != "nofuse"
     ops.CONV_LOCAL = v != "nolocal"
     lib.msp_debug_conv_local_abl({"x6s": -1, "x6l": -2}.get(v, -3))
+    lib.msp_debug_conv_local_min_ch(32 if v == "l0" else 64)
     if v == "tile":
         _lib.query = lambda name, *a: 0 if name == "msp_conv_nbr_preferred" else orig_query(name, *a)
     elif v == "nbr0":
