@@ -633,6 +633,7 @@ class ResidualJoinFunction(torch.autograd.Function):
         _record("bn_join/hbm", 0, lambda: call("msp_add_bn_stats", ptr(a), ptr(b), V, C, ptr(out), ptr(partial),
                                                 _stream(a)), 12 * V * C)
         ctx.mark_non_differentiable(partial)
+        ctx.set_materialize_grads(False)  # no zero-filled fp64 "gradient" of the partials per join
         return out, partial
 
     @staticmethod
@@ -720,11 +721,14 @@ class SceneMeanFunction(torch.autograd.Function):
         ctx.level, ctx.rules, ctx.V, ctx.shift = level, rules, V, shift
         ctx.save_for_backward(npts)
         ctx.mark_non_differentiable(npts)
+        ctx.set_materialize_grads(False)
         return out, npts
 
     @staticmethod
     def backward(ctx, g, _gn):
         (npts,) = ctx.saved_tensors
+        if g is None:
+            return None, None, None, None
         g = g.contiguous()
         C = g.size(1)
         dx = torch.empty((max(ctx.V, 1), C), dtype=torch.float32, device=g.device)
