@@ -199,3 +199,24 @@ def test_graph_dp_world2_hip_model():
             p.kill()
     assert dict(out) == {0: True, 1: True}, dict(out)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_bench_graph_path_over_rccl():
+    """The exact code path the driver's multi-GPU bench runs (HIP-graph steps, dp.GradSync's all-reduce over
+    RCCL between replays, eager Adam), on a one-rank RCCL group (BENCH_DP_SELFTEST): a small workload must
+    complete and report the RCCL exchange."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, BENCH_DP_SELFTEST="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1", "--no-cpu",
+                        "--batch", "2", "--scale", "20", "--family-steps", "1"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["config"]["comm_backend"] == "nccl"
+    assert d["config"]["grad_exchange"] and "GradSync" in d["config"]["grad_exchange"]
+    assert "HIP graph" in d["config"]["launch"]
+    assert d["value"] > 0
