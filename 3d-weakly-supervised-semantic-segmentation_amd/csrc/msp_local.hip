@@ -280,7 +280,7 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 
 // ABL (timing experiments only, wrong results): bit 1 no weight loads, 2 no LDS input reads, 4 no staging,
 // 8 no MFMAs, 16 no index reads (every group active)
-template <int NT, int T, int D, int WR, int ABL = 0, int WP = 3>
+template <int NT, int T, int D, int WR, int ABL = 0, int WP = 3, int RI = 0>
 __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
@@ -336,8 +336,48 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
       for (int p = 0; p < WP; ++p) w[t][p] = src[(t * WP + p) * 64];
   };
   constexpr int SB = WR == 1 ? 3 : 2;  // staging loads in flight per thread
+  // RI: the thread's staged row indices loaded once per tile and kept in registers; every 32-channel slice
+  // then issues all of its value loads at once (one global latency per slice instead of index -> value)
+  constexpr int MI = (kUCap * 4 + NTH - 1) / NTH;
+  int32_t srow[RI ? MI : 1];
+  if constexpr (RI != 0) {
+#pragma unroll
+    for (int b = 0; b < MI; ++b) {
+      const int i = tid + NTH * b;
+      srow[b] = i < Us * 4 ? u_rows[u0 + (i >> 2)] : 0;
+    }
+  }
+  auto stage_ri = [&](int ks) {
+    const int k0 = 32 * ks;
+    floatx4 v[MI][2];
+#pragma unroll
+    for (int b = 0; b < MI; ++b) {
+      const int i = tid + NTH * b;
+      const int k = k0 + 8 * (i & 3);
+      v[b][0] = v[b][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (i < Us * 4 && k < c_in) {
+        const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)srow[RI ? b : 0] * c_in + k);
+        v[b][0] = src[0];
+        v[b][1] = src[1];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < MI; ++b) {
+      const int i = tid + NTH * b;
+      if (i < Us * 4) {
+        u32x4 pc[3];
+        split8(v[b][0], v[b][1], pc);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) xs[xs_unit(i >> 2, p, i & 3)] = pc[p];
+      }
+    }
+  };
   auto stage = [&](int ks) {
     if (ABL & 4) return;
+    if constexpr (RI != 0) {
+      stage_ri(ks);
+      return;
+    }
     const int k0 = 32 * ks;
     const int items = Us * 4;
     for (int i0 = tid; i0 < items; i0 += NTH * SB) {
@@ -1574,6 +1614,7 @@ static int g_local_abl = 0;    // ablation variant (timing only; msp_debug_conv_
 static int g_local_form = 2;   // 2: conv_x6l for 64 output channels, 1: wherever it applies, 0: conv_x6s
 static int g_local_d = 2;      // weight register sets of conv_x6s (prefetch depth; msp_debug_conv_local_d)
 static int g_local_wp = 3;     // weight image: 3 = bf16 pieces, 2 = fp32 split in registers (msp_debug_conv_local_wp)
+static int g_local_ri = 1;       // conv_x6s: row indices held in registers across slices (msp_debug_conv_local_ri)
 static int g_local_min_ch = 64;  // msp_conv_local_preferred: channels on both sides from (msp_debug_conv_local_min_ch)
 
 inline int cu_count() {
@@ -1649,6 +1690,11 @@ int msp_debug_conv_local(int wr, int order, int nt) {
 // weight image of msp_conv_local: 3 = split once into bf16 pieces, 2 = fp32, split by the kernels in registers
 int msp_debug_conv_local_wp(int wp) {
   if (wp == 2 || wp == 3) g_local_wp = wp;
+  return MSP_OK;
+}
+
+int msp_debug_conv_local_ri(int ri) {
+  g_local_ri = ri ? 1 : 0;
   return MSP_OK;
 }
 
@@ -1929,15 +1975,24 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const unsigned grid = (unsigned)(n_tiles * n_y);
   const int wr = g_local_wr;
   const int dd = g_local_abl == 0 ? g_local_d : 2;
+  const int ri = g_local_abl == 0 && wp == 3 && dd == 2 ? g_local_ri : 0;
+  if (ri && wr == 2 && NT == 2)
+    conv_x6s_kernel<2, 128, 2, 2, 0, 3, 1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start,
+                                                                u_rows, perm, n_pad, n_y, out);
+  else if (ri && wr == 2 && NT == 1)
+    conv_x6s_kernel<1, 128, 2, 2, 0, 3, 1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start,
+                                                                u_rows, perm, n_pad, n_y, out);
+  else {
 #define LX(N, W, A, P, DD)                                                                                    \
   if (NT == N && wr == W && g_local_abl == A && wp == P && dd == DD)                                          \
     conv_x6s_kernel<N, 128, DD, W, A, P><<<grid, 256 * W, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx,      \
                                                                   u_start, u_rows, perm, n_pad, n_y, out);
-  LX(2, 1, 0, 3, 2) LX(1, 1, 0, 3, 2) LX(2, 2, 0, 3, 2) LX(1, 2, 0, 3, 2) LX(2, 1, 0, 2, 2) LX(1, 1, 0, 2, 2)
-  LX(2, 2, 0, 2, 2) LX(1, 2, 0, 2, 2) LX(2, 2, 0, 3, 1) LX(1, 2, 0, 3, 1) LX(2, 2, 0, 2, 1)
-  LX(2, 2, 1, 3, 2) LX(2, 2, 2, 3, 2) LX(2, 2, 4, 3, 2) LX(2, 2, 8, 3, 2) LX(2, 2, 16, 3, 2) LX(2, 2, 15, 3, 2)
-  LX(2, 2, 31, 3, 2)
+    LX(2, 1, 0, 3, 2) LX(1, 1, 0, 3, 2) LX(2, 2, 0, 3, 2) LX(1, 2, 0, 3, 2) LX(2, 1, 0, 2, 2) LX(1, 1, 0, 2, 2)
+    LX(2, 2, 0, 2, 2) LX(1, 2, 0, 2, 2) LX(2, 2, 0, 3, 1) LX(1, 2, 0, 3, 1) LX(2, 2, 0, 2, 1)
+    LX(2, 2, 1, 3, 2) LX(2, 2, 2, 3, 2) LX(2, 2, 4, 3, 2) LX(2, 2, 8, 3, 2) LX(2, 2, 16, 3, 2) LX(2, 2, 15, 3, 2)
+    LX(2, 2, 31, 3, 2)
 #undef LX
+  }
   return check_launch("msp_conv_local");
 }
 

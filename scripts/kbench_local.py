@@ -15,8 +15,10 @@ import ctypes
 lib.msp_debug_conv_local.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
 lib.msp_debug_conv_local_abl.argtypes = [ctypes.c_int]
 lib.msp_debug_conv_local_wp.argtypes = [ctypes.c_int]
+lib.msp_debug_conv_local_ri.argtypes = [ctypes.c_int]
 ABLS = [int(a) for a in os.environ.get("ABL", "").split(",") if a]  # ablation variants of local 2:1:0
-# local variants "wr:order:nt[:persistent[:wp]]" (env VARIANTS; wp = weight image, 3 pieces / 2 fp32)
+# local variants "wr:order:nt[:persistent[:wp[:ri]]]" (env VARIANTS; wp = weight image, 3 pieces / 2 fp32; ri = 1:
+# conv_x6s keeps the staged rows' indices in registers across input-channel slices)
 VARS = [tuple(int(v) for v in e.split(":")) for e in os.environ.get("VARIANTS", "1:1:0,2:1:0,2:1:1,2:0:0").split(",")]
 b = make_batch(8, 50, seed=1)
 t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).cuda(), torch.from_numpy(b["feats"]).cuda()])
@@ -84,6 +86,7 @@ for L, size in enumerate(sizes):
                 lib.msp_debug_conv_local(var[0], -1, var[2])
                 lib.msp_debug_conv_local_abl(-2 if len(var) > 3 and var[3] else -1)
                 lib.msp_debug_conv_local_wp(var[4] if len(var) > 4 else 3)
+                lib.msp_debug_conv_local_ri(var[5] if len(var) > 5 else 1)
                 rules._locals[128] = loc_sorted if var[1] else loc_key
             f = lambda: ops.conv_tile(x, wt, 27, flip, cout, rules, V)
             ms = timeit(f)
@@ -103,5 +106,6 @@ for L, size in enumerate(sizes):
         lib.msp_debug_conv_local(2, 1, 0)
         lib.msp_debug_conv_local_abl(-3)
         lib.msp_debug_conv_local_wp(3)
+        lib.msp_debug_conv_local_ri(1)
         rules._locals[128] = loc_sorted
 ops.CONV_LOCAL = True
