@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
   constexpr int NC = 16 * NT;
   static_assert(4 * T * NC * 4 <= kXR * kXU * 16, "partial sums must fit the staging area");
   __shared__ u32x4 xs[kXR * kXU];
-  __shared__ uint16_t ls[kKMax * T];
+  __shared__ __attribute__((aligned(16))) uint16_t ls[kKMax * T];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int oc = wave & 3, rp = wave >> 2;  // offset class, row part (rows 16 G rp ..)
@@ -302,9 +302,29 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
   const int U = (int)(u_start[tile + 1] - u0);
   const int Us = U < kUCap ? U : kUCap;
   const int nks = (c_in + 31) / 32;
-  for (int i = tid; i < K * T; i += NTH) {
-    const int o = i / T, p = i - o * T;
-    ls[i] = lidx[(int64_t)o * n_pad + tile * T + p];
+  if constexpr (RI >= 2) {  // the index tile as 32-bit words, every load in flight before the LDS stores
+    constexpr int LW = (kKMax * T / 2 + NTH - 1) / NTH;
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lidx);
+    uint32_t wv[LW];
+#pragma unroll
+    for (int b = 0; b < LW; ++b) {
+      const int i = tid + NTH * b;  // word i = entries 2i, 2i + 1 of the [K][T] tile (T even: one offset)
+      wv[b] = 0u;
+      if (i < K * T / 2) {
+        const int e = 2 * i, o = e / T, pp = e - o * T;
+        wv[b] = lw[((int64_t)o * n_pad + tile * T + pp) >> 1];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < LW; ++b) {
+      const int i = tid + NTH * b;
+      if (i < K * T / 2) reinterpret_cast<uint32_t*>(ls)[i] = wv[b];
+    }
+  } else {
+    for (int i = tid; i < K * T; i += NTH) {
+      const int o = i / T, p = i - o * T;
+      ls[i] = lidx[(int64_t)o * n_pad + tile * T + p];
+    }
   }
   if (tid < kXU) xs[kUCap * kXU + tid] = u32x4{0u, 0u, 0u, 0u};
 
@@ -1611,10 +1631,14 @@ static int g_local_wr = 2;     // row parts per block (waves = 4 x wr); msp_debu
 static int g_local_order = 1;  // msp_tile_local: order rows inside a tile by neighbour mask
 static int g_local_nt = 0;     // forced column tiles per wave (0: local_nt)
 static int g_local_abl = 0;    // ablation variant (timing only; msp_debug_conv_local_abl)
-static int g_local_form = 2;   // 2: conv_x6l for 64 output channels, 1: wherever it applies, 0: conv_x6s
+// 0: conv_x6s everywhere (default since its staged rows' indices stay in registers and the index tile loads as
+// words: 2.5-4 % ahead of conv_x6l at level 1, profiles/r02/kbench_local_l1form_r02.log), 1: conv_x6l wherever it
+// applies, 2: conv_x6l for 64 output channels (the round-2 choice before that)
+constexpr int kLocalFormDefault = 0;
+static int g_local_form = kLocalFormDefault;
 static int g_local_d = 2;      // weight register sets of conv_x6s (prefetch depth; msp_debug_conv_local_d)
 static int g_local_wp = 3;     // weight image: 3 = bf16 pieces, 2 = fp32 split in registers (msp_debug_conv_local_wp)
-static int g_local_ri = 1;       // conv_x6s: row indices held in registers across slices (msp_debug_conv_local_ri)
+static int g_local_ri = 2;       // conv_x6s: row indices held in registers across slices (msp_debug_conv_local_ri)
 static int g_local_min_ch = 64;  // msp_conv_local_preferred: channels on both sides from (msp_debug_conv_local_min_ch)
 
 inline int cu_count() {
@@ -1694,7 +1718,7 @@ int msp_debug_conv_local_wp(int wp) {
 }
 
 int msp_debug_conv_local_ri(int ri) {
-  g_local_ri = ri ? 1 : 0;
+  g_local_ri = ri < 0 ? 0 : (ri > 2 ? 2 : ri);
   return MSP_OK;
 }
 
@@ -1704,8 +1728,8 @@ int msp_debug_conv_local_d(int d) {
 }
 
 int msp_debug_conv_local_abl(int abl) {
-  if (abl < 0) {  // -1 / -2 / -3: persistent form off / wherever it applies / 64 output channels only
-    g_local_form = abl == -2 ? 1 : (abl == -3 ? 2 : 0);
+  if (abl < 0) {  // -1 / -2 / -3 / -4: persistent form off / wherever it applies / the default / 64 channels only
+    g_local_form = abl == -2 ? 1 : (abl == -3 ? kLocalFormDefault : (abl == -4 ? 2 : 0));
     return MSP_OK;
   }
   g_local_abl = abl;
@@ -1976,7 +2000,10 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int wr = g_local_wr;
   const int dd = g_local_abl == 0 ? g_local_d : 2;
   const int ri = g_local_abl == 0 && wp == 3 && dd == 2 ? g_local_ri : 0;
-  if (ri && wr == 2 && NT == 2)
+  if (ri == 2 && wr == 2 && NT == 2)
+    conv_x6s_kernel<2, 128, 2, 2, 0, 3, 2><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start,
+                                                                u_rows, perm, n_pad, n_y, out);
+  else if (ri && wr == 2 && NT == 2)
     conv_x6s_kernel<2, 128, 2, 2, 0, 3, 1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start,
                                                                 u_rows, perm, n_pad, n_y, out);
   else if (ri && wr == 2 && NT == 1)

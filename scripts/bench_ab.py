@@ -19,7 +19,7 @@ for v in os.environ.get("AB", "tile,nbr").split(","):
     lib.msp_debug_conv_nbr_variant(0)
     modules.FUSE_RESIDUAL = v != "nofuse"
     ops.CONV_LOCAL = v != "nolocal"
-    lib.msp_debug_conv_local_abl({"x6s": -1, "x6l": -2}.get(v, -3))
+    lib.msp_debug_conv_local_abl({"x6s": -1, "x6l": -2, "x6l64": -4}.get(v, -3))
     lib.msp_debug_conv_local_min_ch(32 if v == "l0" else 64)
     if v == "tile":
         _lib.query = lambda name, *a: 0 if name == "msp_conv_nbr_preferred" else orig_query(name, *a)
