@@ -280,7 +280,7 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 
 // ABL (timing experiments only, wrong results): bit 1 no weight loads, 2 no LDS input reads, 4 no staging,
 // 8 no MFMAs, 16 no index reads (every group active)
-template <int NT, int T, int D, int WR, int ABL = 0, int WP = 3, int RI = 0>
+template <int NT, int T, int D, int WR, int ABL = 0, int WP = 3, int RI = 0, int XP = 1>
 __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
@@ -462,13 +462,17 @@ __global__ __launch_bounds__(256 * WR, 2 * WR) void conv_x6s_kernel(
       act |= (ballot64(pres) != 0 ? 1u : 0u) << g;
       far |= (ballot64(pres && li[g] >= kUCap) != 0 ? 1u : 0u) << g;
     }
-    u32x4 xa[3], xb[3];
-    xload(li[0], xa);
+    u32x4 xa[3], xb[3];  // XP = 0: xb unused
+    if (XP) xload(li[0], xa);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      u32x4(&cur)[3] = (g & 1) ? xb : xa;
-      u32x4(&nxt)[3] = (g & 1) ? xa : xb;
-      if (g + 1 < G) xload(li[g + 1], nxt);
+      u32x4(&cur)[3] = (XP && (g & 1)) ? xb : xa;
+      u32x4(&nxt)[3] = (XP && (g & 1)) ? xa : xb;
+      if (XP) {
+        if (g + 1 < G) xload(li[g + 1], nxt);
+      } else if ((act >> g) & 1) {  // XP = 0: the group's pieces read right before its MFMAs (12 fewer VGPRs)
+        xload(li[g], cur);
+      }
       if ((act >> g) & 1) {  // wave-uniform
         if ((far >> g) & 1) {  // rows past the staged capacity: straight from global memory (rare)
           const bool f = li[g] != kAbsent && li[g] >= kUCap;
@@ -1638,7 +1642,7 @@ constexpr int kLocalFormDefault = 0;
 static int g_local_form = kLocalFormDefault;
 static int g_local_d = 2;      // weight register sets of conv_x6s (prefetch depth; msp_debug_conv_local_d)
 static int g_local_wp = 3;     // weight image: 3 = bf16 pieces, 2 = fp32 split in registers (msp_debug_conv_local_wp)
-static int g_local_ri = 2;       // conv_x6s: row indices held in registers across slices (msp_debug_conv_local_ri)
+static int g_local_ri = 3;       // conv_x6s: row indices held in registers across slices (msp_debug_conv_local_ri)
 static int g_local_min_ch = 64;  // msp_conv_local_preferred: channels on both sides from (msp_debug_conv_local_min_ch)
 
 inline int cu_count() {
@@ -1718,7 +1722,7 @@ int msp_debug_conv_local_wp(int wp) {
 }
 
 int msp_debug_conv_local_ri(int ri) {
-  g_local_ri = ri < 0 ? 0 : (ri > 2 ? 2 : ri);
+  g_local_ri = ri < 0 ? 0 : (ri > 3 ? 3 : ri);
   return MSP_OK;
 }
 
@@ -2000,7 +2004,10 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int wr = g_local_wr;
   const int dd = g_local_abl == 0 ? g_local_d : 2;
   const int ri = g_local_abl == 0 && wp == 3 && dd == 2 ? g_local_ri : 0;
-  if (ri == 2 && wr == 2 && NT == 2)
+  if (ri == 3 && wr == 2 && NT == 2)
+    conv_x6s_kernel<2, 128, 2, 2, 0, 3, 2, 0><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start,
+                                                                   u_rows, perm, n_pad, n_y, out);
+  else if (ri == 2 && wr == 2 && NT == 2)
     conv_x6s_kernel<2, 128, 2, 2, 0, 3, 2><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start,
                                                                 u_rows, perm, n_pad, n_y, out);
   else if (ri && wr == 2 && NT == 2)

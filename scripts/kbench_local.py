@@ -86,7 +86,7 @@ for L, size in enumerate(sizes):
                 lib.msp_debug_conv_local(var[0], -1, var[2])
                 lib.msp_debug_conv_local_abl(-2 if len(var) > 3 and var[3] else -1)
                 lib.msp_debug_conv_local_wp(var[4] if len(var) > 4 else 3)
-                lib.msp_debug_conv_local_ri(var[5] if len(var) > 5 else 2)
+                lib.msp_debug_conv_local_ri(var[5] if len(var) > 5 else 3)
                 rules._locals[128] = loc_sorted if var[1] else loc_key
             f = lambda: ops.conv_tile(x, wt, 27, flip, cout, rules, V)
             ms = timeit(f)
@@ -106,6 +106,6 @@ for L, size in enumerate(sizes):
         lib.msp_debug_conv_local(2, 1, 0)
         lib.msp_debug_conv_local_abl(-3)
         lib.msp_debug_conv_local_wp(3)
-        lib.msp_debug_conv_local_ri(2)
+        lib.msp_debug_conv_local_ri(3)
         rules._locals[128] = loc_sorted
 ops.CONV_LOCAL = True
