@@ -59,27 +59,26 @@ static __global__ __launch_bounds__(256) void split_reduce_kernel(const floatx4*
 }
 
 // Shared-tile convolution on bf16 MFMA with exact three-piece operand splits
-// (msp_conv_x6.hip), used by msp_conv_tile for 128-row tiles.
+// (msp_conv_x6.hip), used by msp_conv_tile for 128-row tiles: nt 16-column groups per block, nb weight
+// buffers, split = blocks per tile on small grids (partials reduced in split order).
 struct PlanX6 {
-  int nt, ks, n_y, split, depth, abl, tr, nb;  // abl: timing experiments only (msp_debug_conv_x6)
+  int nt, n_y, split, nb;
 };
-PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks, int tile_rows = 128);
+PlanX6 plan_x6(int64_t n_rows, int c_out);
 size_t x6_ws_bytes(int64_t n_rows, int K, int c_in, int c_out, const PlanX6& p);
 int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s);
 
-// Per-wave split-bf16 form for narrow outputs (c_out <= 32, c_in <= 64); form 0:
-// weights reloaded per chunk, 1 / 2: per offset run, 2 / 3 register sets.
-int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
-               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
-               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s, int force_nt = 0,
-               int depth = 0, int form = 0);
+// Per-wave split-bf16 form for narrow outputs (c_out <= 32, c_in <= 64), 128-row tiles.
+int launch_x6r(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
+               const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
+               float* out, void* ws, hipStream_t s);
 size_t x6p_ws_bytes(int K, int c_in, int c_out);
 
 // Dense row-group split-bf16 form over the neighbour map (submanifold convs).
 int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
-               const int32_t* perm, int64_t n_rows, float* out, void* ws, hipStream_t s, int nt = 0, int g = 0);
+               const int32_t* perm, int64_t n_rows, float* out, void* ws, hipStream_t s);
 size_t x6g_ws_bytes(int K, int c_in, int c_out);
 
 // bf16-split weight gradient (msp_conv_x6.hip), used by msp_conv_wgrad.
@@ -87,14 +86,5 @@ int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const 
                     const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
                     hipStream_t s);
 void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb);
-
-// Banded submanifold weight gradient (msp_conv_x6.hip): rows staged in LDS.
-int64_t wgrad_band_n_sub(int64_t n_rows);
-int64_t wgrad_band_groups(int64_t n_rows, int c_in, int c_out, int& S);
-int launch_wgrad_band(const float* x, int c_in, const float* dy, int c_out, const int32_t* pin,
-                      const int32_t* pout, const int64_t* seg, int K, int64_t n_rows, int64_t n_groups, int S,
-                      float* slab, hipStream_t s);
-int launch_wgrad_band_seg(const int32_t* pout, const int64_t* off_start, int K, int64_t n_rows, int64_t* seg,
-                          hipStream_t s);
 
 }  // namespace msp

@@ -381,135 +381,12 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
 
 
 // ---------------------------------------------------------------- per-wave tiles
-// Narrow outputs (c_out <= 32, level 0 of m=32 nets): one wave owns one
-// 128-row output tile and all 16 NT output channels, no block barrier (the
-// f32 conv_tilep_kernel structure, msp_conv.hip).  With few chunks per offset
-// and tile there is nothing to share between waves; the f32 form was bound
-// by the f32 MFMA dependency chain (SQ_WAIT_INST_ANY 57-70 % of wave cycles,
-// profiles/r01/pmc_tilep_r01t.txt), which the bf16 split form shortens
-// 2.7x.  Per chunk the lane loads its row fragment X[src_r][32 kk + 8q .. +7]
-// and its weight fragments (three pieces, NT column groups, NKK k-steps) from
-// the per-step weight images of split_weights_kernel (KS = 32, NC = 16 NT:
-// one coalesced 1 KiB wave-load per fragment).  Chunk indices run two chunks
-// ahead of the values, values one; loads are branch-free (positions past the
-// tile's last chunk are clamped to it, their work skipped uniformly).
-template <int NT, int NKK, int TR = 128, int D = 2, int ABL = 0>
-__global__ __launch_bounds__(kThreads) void conv_x6p_kernel(
-    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
-    const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
-    const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
-    int64_t n_tiles, int n_y, float* __restrict__ out) {
-  constexpr int NC = 16 * NT;
-  constexpr int WU = 3 * 4 * NC;  // 16-byte units of one (offset, k-slice) image
-  __shared__ floatx4 lds4[kWaves][TR * NC / 4];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
-  const int64_t tile = (lb / n_y) * kWaves + wave;
-  if (tile >= n_tiles) return;  // wave-uniform; the kernel has no block barrier
-  float* acc_s = reinterpret_cast<float*>(lds4[wave]);
-  for (int i = lane; i < TR * NC / 4; i += 64) lds4[wave][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int cy = (int)(lb % n_y);
-  const int r = lane & 15, q = lane >> 4;
-  const int64_t cb = tile_start[tile], ce = tile_start[tile + 1];
-  const int64_t clast = ce > cb ? ce - 1 : cb;
-  const u32x4* wim_c = wimg + (int64_t)cy * NKK * WU + q * NC + r;  // lane's unit in image (o, cy, 0), piece 0
-
-  struct St {
-    int o, src, row;
-  };
-  struct Val {
-    floatx4 a[NKK][2];
-    u32x4 w[NKK][NT][3];
-  };
-  auto ld_idx = [&](int64_t c, St& d) {
-    const int64_t cc = c < clast ? c : clast;
-    d.o = chunk_off[cc];
-    d.src = chunk_src[cc * MSP_CHUNK + r];
-    d.row = chunk_row[cc * MSP_CHUNK + r];
-  };
-  auto ld_val = [&](const St& d, Val& v, bool first = false) {
-    const char* xs = reinterpret_cast<const char*>(x) + (uint32_t)d.src * (uint32_t)c_in * 4u;
-    const int ow = flip ? (K - 1 - d.o) : d.o;
-    const u32x4* wo = wim_c + (int64_t)ow * n_y * NKK * WU;
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {
-      const int k = min(32 * kk + 8 * q, c_in - 8);  // k past c_in: finite data times zero weights
-      const floatx4* pv = reinterpret_cast<const floatx4*>(xs + 4u * (uint32_t)k);
-      v.a[kk][0] = pv[0];
-      v.a[kk][1] = pv[1];
-      if (!(ABL & 2) || first) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int p = 0; p < 3; ++p) v.w[kk][t][p] = wo[kk * WU + p * 4 * NC + 16 * t];
-      }
-    }
-  };
-  auto run = [&](const Val& v, int row, bool live) {
-    if (live) {
-      floatx4 acc[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        u32x4 xp[3];
-        split8(v.a[kk][0], v.a[kk][1], xp);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          floatx4 c = acc[t];
-          c = mfma_bf16(v.w[kk][t][2], xp[0], c);
-          c = mfma_bf16(v.w[kk][t][1], xp[1], c);
-          c = mfma_bf16(v.w[kk][t][0], xp[2], c);
-          c = mfma_bf16(v.w[kk][t][1], xp[0], c);
-          c = mfma_bf16(v.w[kk][t][0], xp[1], c);
-          acc[t] = mfma_bf16(v.w[kk][t][0], xp[0], c);
-        }
-      }
-      if (row < TR) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          *reinterpret_cast<floatx4*>(acc_s + acc_pos<NC>(row, 4 * t + q)) += acc[t];
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {  // mark the set read on every path
-      asm volatile("" ::"v"(v.a[kk][0]), "v"(v.a[kk][1]));
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(v.w[kk][t][p]));
-    }
-  };
-  St J[D];
-  int rowR[D];
-  Val S[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    ld_idx(cb + k, J[k]);
-    rowR[k] = J[k].row;
-    ld_val(J[k], S[k], true);
-  }
-#pragma unroll
-  for (int k = 0; k < D; ++k) ld_idx(cb + D + k, J[k]);
-  for (int64_t c = cb; c < ce; c += D) {
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      run(S[k], rowR[k], c + k < ce);
-      ld_val(J[k], S[k]);  // chunk c+k+D
-      rowR[k] = J[k].row;
-      ld_idx(c + k + 2 * D, J[k]);
-    }
-  }
-  const int64_t row0 = tile * TR;
-  const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
-  constexpr int V4 = NC / 4;
-  const int c0 = cy * NC;
-  for (int i = lane; i < nr * V4; i += 64) {
-    const int rr = i / V4, g = i % V4;
-    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
-        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
-  }
-}
+// Narrow outputs (c_out <= 32, c_in <= 64: level 0 of m=32 nets): one wave owns one 128-row output tile and all
+// 16 NT output channels, accumulated in its own LDS tile, with no block barrier: with few chunks per offset and
+// tile there is nothing to share between waves.  Per chunk the lane loads its row fragment
+// X[src_r][32 kk + 8q .. +7] (split into the three bf16 pieces in registers) and reads the weight fragments
+// (three pieces, NT column groups, NKK k-steps) from the per-step weight images of split_weights_kernel
+// (KS = 32, NC = 16 NT: one coalesced 1 KiB wave-load per fragment).
 
 // Per-wave tiles with weight runs.  conv_x6p_kernel reloads the lane's weight
 // fragments with every chunk (6 of its 8 16-byte loads per chunk at
@@ -676,69 +553,33 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
   }
 }
 
-// Per-wave form for narrow outputs; ws holds the weight images (x6p_ws_bytes).
-// force_nt / depth: 0 = the plan's choice; tile_rows 64 or 128 (the rulebook's).
-int launch_x6p(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
-               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
-               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s, int force_nt,
-               int depth, int form) {
-  int NT = c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1;
-  if (force_nt > 0) NT = force_nt;
-  if (force_nt < 0) NT = 2;
-  const int D = depth > 0 ? depth : 2;
+// Per-wave form for narrow outputs; ws holds the weight images (x6p_ws_bytes).  Two weight register sets per
+// offset run, chunk values three deep (profiles/r01/kbench_x6r_r01u.log).
+int launch_x6r(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
+               const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
+               float* out, void* ws, hipStream_t s) {
+  const int NT = c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1;
   const int NKK = (c_in + 31) / 32;
-  if ((c_out / 16) % NT != 0) {
-    set_error("msp_conv_tile: per-wave x6: nt %d does not divide c_out/16 = %d", NT, c_out / 16);
-    return MSP_EINVAL;
-  }
   const int n_y = c_out / (16 * NT);
-  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
+  const int64_t n_tiles = ceil_div(n_rows, 128);
   u32x4* wimg = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)K * c_out * NKK * 32 * 6 / 16;
   split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg,
                                                                        (flip >> 1) & 1);
   flip &= 1;
   const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
-  bool launched = false;
-#define LP(N, C, R, DD)                                                                                      \
-  if (!launched && NT == N && NKK == C && tile_rows == R && D == DD) {                                       \
-    conv_x6p_kernel<N, C, R, DD><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,        \
-                                                           chunk_off, chunk_src, chunk_row, n_rows, n_tiles, \
-                                                           n_y, out);                                        \
-    launched = true;                                                                                          \
+#define LR(N, C)                                                                                               \
+  if (NT == N && NKK == C) {                                                                                   \
+    conv_x6r_kernel<N, C, 3, 2><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start, chunk_off, \
+                                                          chunk_src, chunk_row, n_rows, n_tiles, n_y, out);    \
+    return MSP_OK;                                                                                             \
   }
-#define LR(N, C, DD, NWW)                                                                                    \
-  if (!launched && form == NWW - 1 && NT == N && NKK == C && tile_rows == 128 && D == DD) {                   \
-    conv_x6r_kernel<N, C, DD, NWW><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,       \
-                                                             chunk_off, chunk_src, chunk_row, n_rows, n_tiles, \
-                                                             n_y, out);                                        \
-    launched = true;                                                                                            \
-  }
-  LR(2, 1, 3, 2) LR(2, 2, 3, 2) LR(1, 1, 3, 2) LR(1, 2, 3, 2) LR(2, 1, 2, 2) LR(2, 2, 2, 2) LR(2, 1, 4, 2)
+  LR(2, 1) LR(2, 2) LR(1, 1) LR(1, 2)
 #undef LR
-  if (!launched && force_nt < 0 && NKK <= 2) {  // ablation (timing only): weights loaded once per wave
-    if (NKK == 1)
-      conv_x6p_kernel<2, 1, 128, 2, 2><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,
-                                                                 chunk_off, chunk_src, chunk_row, n_rows, n_tiles,
-                                                                 n_y, out);
-    else
-      conv_x6p_kernel<2, 2, 128, 2, 2><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,
-                                                                 chunk_off, chunk_src, chunk_row, n_rows, n_tiles,
-                                                                 n_y, out);
-    launched = true;
-  }
-  LP(1, 1, 128, 2) LP(1, 2, 128, 2) LP(2, 1, 128, 2) LP(2, 2, 128, 2)
-  LP(1, 1, 64, 2) LP(1, 2, 64, 2) LP(2, 1, 64, 2) LP(2, 2, 64, 2)
-  LP(2, 1, 64, 3) LP(2, 2, 64, 3) LP(2, 1, 128, 3) LP(2, 2, 128, 3) LP(1, 1, 64, 3) LP(1, 2, 64, 3)
-  LP(2, 1, 64, 4) LP(1, 1, 64, 4)
-#undef LP
-  if (!launched) {
-    set_error("msp_conv_tile: no per-wave x6 kernel for c_in=%d c_out=%d nt=%d tile_rows=%d depth=%d", c_in, c_out,
-              NT, tile_rows, D);
-    return MSP_EINVAL;
-  }
-  return MSP_OK;
+  set_error("msp_conv_tile: no per-wave x6 kernel for c_in=%d c_out=%d", c_in, c_out);
+  return MSP_EINVAL;
 }
+
 
 size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c_in + 31) / 32) * 32 * 6; }
 
@@ -946,19 +787,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(OCC))) 
   }
 }
 
-// Dense row-group form; ws holds the split weight slices (x6g_ws_bytes).
+// Dense row-group form; ws holds the split weight slices (x6g_ws_bytes).  Column-group-outer MFMAs, one staging
+// slot, ONE 16-row group per wave at a 4-waves-per-SIMD budget (108 / 94 VGPRs, no spills): conv family +1.5 %
+// over two groups at 3 waves (profiles/r01/bench_ab_g1_r01.log); NT = 4 (3 for 96 channels)
+// (profiles/r01/kbench_nbr_r01v.log).
 int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int32_t* nbr,
-               const int32_t* perm, int64_t n_rows, float* out, void* ws, hipStream_t s, int nt, int g) {
+               const int32_t* perm, int64_t n_rows, float* out, void* ws, hipStream_t s) {
   const int n16 = c_out / 16;
-  // NT = 4 (3 for 96 channels) with G = 2: scripts/kbench_nbr.py,
-  // profiles/r01/kbench_nbr_r01v.log; g = 2: the base form (all fragments
-  // first, two staging slots)
-  if (nt <= 0) nt = n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1));
-  if (g <= 0) g = 141;
-  if (n16 % nt != 0) {
-    set_error("msp_conv_nbr: nt %d does not divide c_out/16 = %d", nt, n16);
-    return MSP_EINVAL;
-  }
+  const int nt = n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1));
   const int n_y = n16 / nt;
   const int nks = (c_in + 31) / 32;
   u32x4* wimg = static_cast<u32x4*>(ws);
@@ -966,45 +802,19 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * nt, 32, wimg,
                                                                        (flip >> 1) & 1);
   flip &= 1;
-  const int nw = g >= 1000 ? 8 : kWaves;  // g = 1000 + ...: 8-wave blocks
-  const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)nw * 16 * (g % 10)) * n_y);
-  bool launched = false;
-#define LG(N, GG)                                                                                             \
-  if (!launched && nt == N && g == GG) {                                                                      \
-    conv_x6g_kernel<N, GG><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, perm, n_rows, n_y,    \
-                                                     out);                                                    \
-    launched = true;                                                                                          \
+  const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)kWaves * 16) * n_y);
+#define LL(N)                                                                                                 \
+  if (nt == N) {                                                                                              \
+    conv_x6g_kernel<N, 1, 4, 1><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, perm, n_rows,    \
+                                                          n_y, out);                                          \
+    return MSP_OK;                                                                                            \
   }
-  LG(4, 2) LG(3, 2) LG(2, 2) LG(1, 2) LG(6, 2) LG(4, 3)
-#undef LG
-#define LL(N, GG, O)                                                                                          \
-  if (!launched && nt == N && g == GG + 10 * O + 100) {                                                       \
-    conv_x6g_kernel<N, GG, O, 1><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, perm, n_rows,  \
-                                                           n_y, out);                                         \
-    launched = true;                                                                                          \
-  }
-  // production (g = 0 -> 141): column-group-outer MFMAs, one staging slot, ONE 16-row group per wave at a
-  // 4-waves-per-SIMD budget (108 / 94 VGPRs, no spills): conv family +1.5 % TF/s over 132 (G = 2, 3 waves,
-  // 156 / 142 VGPRs) in three same-process A/B pairs (profiles/r01/bench_ab_g1_r01.log); 132 was 5-12 %
-  // over the G = 2 base form (profiles/r01/kbench_nbr_lr_r01w.log); g = 100 + G + 10 * waves per SIMD
-  // selects others
-  LL(4, 2, 3) LL(3, 2, 3) LL(2, 2, 3) LL(1, 2, 3) LL(4, 2, 1) LL(3, 2, 1)
-  LL(4, 1, 4) LL(3, 1, 4) LL(2, 1, 4) LL(1, 1, 4)
-#define L8(N, GG, O)                                                                                          \
-  if (!launched && nt == N && g == 1000 + GG + 10 * O + 100) {                                                \
-    conv_x6g_kernel<N, GG, O, 1, 8><<<grid, 512, 0, s>>>(x, c_in, wimg, K, flip, c_out, nbr, perm, n_rows,    \
-                                                         n_y, out);                                           \
-    launched = true;                                                                                          \
-  }
-  L8(4, 1, 4) L8(3, 1, 4)  // 8-wave blocks (128 rows share each step's weight slice)
-#undef L8  // G = 1: 108 / 94 VGPRs, 4-5 waves per SIMD (G = 2 at 4 waves spills)
+  LL(4) LL(3) LL(2) LL(1)
 #undef LL
-  if (!launched) {
-    set_error("msp_conv_nbr: no dense-group kernel for nt=%d g=%d", nt, g);
-    return MSP_EINVAL;
-  }
-  return MSP_OK;
+  set_error("msp_conv_nbr: no dense-group kernel for nt=%d", nt);
+  return MSP_EINVAL;
 }
+
 
 size_t x6g_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c_in + 31) / 32) * 32 * 6; }
 
@@ -1191,246 +1001,13 @@ __global__ __launch_bounds__(kThreads, D == 1 ? 4 : 1) void wgrad_x6_kernel(
   }
 }
 
-// ---------------------------------------------------------------- banded weight gradient
-// Submanifold weight gradients with the rows staged in LDS.  The pair-list
-// kernel above reads x and dy per pair from global memory; at levels 0-1 its
-// L2 hit rate is 0.17-0.23 and it fetches 7-8x the compulsory bytes from
-// HBM (profiles/r01/pmc_wgrad_pieces_r01zz.txt).  Here a block owns one
-// 32 x 32 dW tile (input channels m0.., output channels n0..) and a group of
-// S consecutive 256-row bands of output rows; per band it stages dy[band]
-// and x[band - 64 .. band + 256 + 64) (its 32-channel slices) in LDS once,
-// then every wave runs the pairs of its offsets (o = wave, wave + 4, ...)
-// whose output row is in the band -- the pair lists are sorted by output
-// row inside each offset, seg[o][band] gives the segment -- reading x and
-// dy from LDS (x rows outside the staged range from global memory).  MFMA
-// operands and split arithmetic as wgrad_x6_kernel<2, 2>: lane (r, q) takes
-// pairs 8q..8q+7 of a 32-pair step, input channels m0 + 2r + {0,1} and output
-// channels n0 + 2r + {0,1}; accumulator (oi, sa, sb) register j holds
-// dW[o][m0 + 2 (4q + j) + sa][n0 + 2r + sb].  Each block writes its tile of
-// every offset to slab[group][o] (reduced in group order by
-// wgrad_reduce_kernel: deterministic).
-constexpr int kBandRows = 256, kBandHalo = 64, kBandX = kBandRows + 2 * kBandHalo;
-
-__global__ __launch_bounds__(256) void wgrad_band_seg_kernel(const int32_t* __restrict__ pout,
-                                                             const int64_t* __restrict__ off_start, int K,
-                                                             int64_t n_sub, int64_t* __restrict__ seg) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)K * (n_sub + 1)) return;
-  const int o = (int)(t / (n_sub + 1));
-  const int64_t sb = t % (n_sub + 1);
-  int64_t lo = off_start[o], hi = off_start[o + 1];
-  const int64_t key = sb * kBandRows;
-  while (lo < hi) {  // first pair of offset o with output row >= key
-    const int64_t mid = (lo + hi) >> 1;
-    if ((int64_t)pout[mid] < key) lo = mid + 1;
-    else hi = mid;
-  }
-  seg[t] = lo;
-}
-
-template <int NO, int NW = kWaves>
-__global__ __launch_bounds__(64 * NW) void wgrad_band_kernel(
-    const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out,
-    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ seg, int K,
-    int64_t n_rows, int64_t n_sub, int S, int n_tiles, float* __restrict__ slab) {
-  __shared__ floatx2 xs[kBandX * 16];      // [row][16] float2 = 32 channels
-  __shared__ floatx2 ys[kBandRows * 16];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int r = lane & 15, q = lane >> 4;
-  const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
-  const int tile = (int)(lb % n_tiles);
-  const int64_t grp = lb / n_tiles;
-  const int n_tn = c_out / 32;
-  const int m0 = (tile / n_tn) * 32, n0 = (tile % n_tn) * 32;
-  const int64_t sb0 = grp * S;
-  const int64_t sb1 = sb0 + S < n_sub ? sb0 + S : n_sub;
-
-  floatx4 acc[NO][2][2];
-#pragma unroll
-  for (int oi = 0; oi < NO; ++oi)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc[oi][a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  for (int64_t sb = sb0; sb < sb1; ++sb) {
-    const int64_t j0 = sb * kBandRows, xlo = j0 - kBandHalo;
-    __syncthreads();  // the previous band's reads are done
-    for (int u = tid; u < kBandX * 8; u += 64 * NW) {
-      const int row = u >> 3, c4 = u & 7;
-      const int64_t gr = xlo + row;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gr >= 0 && gr < n_rows) v = *reinterpret_cast<const floatx4*>(x + gr * c_in + m0 + 4 * c4);
-      *reinterpret_cast<floatx4*>(&xs[row * 16 + 2 * c4]) = v;
-    }
-    for (int u = tid; u < kBandRows * 8; u += 64 * NW) {
-      const int row = u >> 3, c4 = u & 7;
-      const int64_t gr = j0 + row;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gr < n_rows) v = *reinterpret_cast<const floatx4*>(dy + gr * c_out + n0 + 4 * c4);
-      *reinterpret_cast<floatx4*>(&ys[row * 16 + 2 * c4]) = v;
-    }
-    __syncthreads();
-    // the wave's offsets o = wave + 4 oi; every offset's segment runs an even
-    // number of 32-pair steps (a trailing empty step at most) through two
-    // index slots, slot 0 holding even steps: the indices of the next step
-    // (the next offset's first at a segment's end) load one step ahead, with
-    // no register copies (static slots keep the wait counts exact)
-    int64_t pbs[NO], pes[NO];
-#pragma unroll
-    for (int oi = 0; oi < NO; ++oi) {
-      const int o = wave + NW * oi < K ? wave + NW * oi : K - 1;
-      const int64_t* so = seg + (int64_t)o * (n_sub + 1);
-      pbs[oi] = wave + NW * oi < K ? so[sb] : 0;
-      pes[oi] = wave + NW * oi < K ? so[sb + 1] : 0;
-    }
-    struct Ix {
-      int i[8], j[8];
-    };
-    auto ld_ix = [&](int64_t p, int64_t pe, Ix& d) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int64_t pp = p + 8 * q + k;
-        const int64_t pc = pp < pe ? pp : (pe > 0 ? pe - 1 : 0);
-        d.i[k] = pin[pc];
-        d.j[k] = pout[pc];
-      }
-    };
-    auto step = [&](int oi, int64_t p, int64_t pe, const Ix& d) {
-      float a[8][2], b[8][2];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bool live = p + 8 * q + k < pe;
-        const int xi = d.i[k] - (int)xlo;
-        const int jj = d.j[k] - (int)j0;
-        const bool inb = (unsigned)xi < (unsigned)kBandX;
-        const floatx2 xl = xs[(inb ? xi : 0) * 16 + r];  // LDS, or global for rows outside the staged range
-        floatx2 xg = {0.f, 0.f};
-        if (!inb) xg = *reinterpret_cast<const floatx2*>(x + (int64_t)d.i[k] * c_in + m0 + 2 * r);
-        const floatx2 xa = inb ? xl : xg;
-        const floatx2 yb = ys[((unsigned)jj < (unsigned)kBandRows ? jj : 0) * 16 + r];
-        a[k][0] = live ? xa[0] : 0.f;
-        a[k][1] = live ? xa[1] : 0.f;
-        b[k][0] = yb[0];
-        b[k][1] = yb[1];
-      }
-      u32x4 bp[2][3];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        split8(floatx4{b[0][t], b[1][t], b[2][t], b[3][t]}, floatx4{b[4][t], b[5][t], b[6][t], b[7][t]}, bp[t]);
-#pragma unroll
-      for (int sa = 0; sa < 2; ++sa) {
-        u32x4 ap[3];
-        split8(floatx4{a[0][sa], a[1][sa], a[2][sa], a[3][sa]}, floatx4{a[4][sa], a[5][sa], a[6][sa], a[7][sa]},
-               ap);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          floatx4 c = acc[oi][sa][t];
-          c = mfma_bf16(ap[2], bp[t][0], c);
-          c = mfma_bf16(ap[1], bp[t][1], c);
-          c = mfma_bf16(ap[0], bp[t][2], c);
-          c = mfma_bf16(ap[1], bp[t][0], c);
-          c = mfma_bf16(ap[0], bp[t][1], c);
-          acc[oi][sa][t] = mfma_bf16(ap[0], bp[t][0], c);
-        }
-      }
-    };
-    Ix S2[2];
-    ld_ix(pbs[0], pes[0], S2[0]);
-#pragma unroll
-    for (int oi = 0; oi < NO; ++oi) {
-      if (wave + NW * oi >= K) break;  // wave-uniform
-      const int64_t pb = pbs[oi], pe = pes[oi];
-      const int64_t nst = ((pe - pb + 31) / 32 + 1) & ~(int64_t)1;  // even step count
-      // where the step after this segment starts: the next offset's first
-      const int64_t nb = oi + 1 < NO ? pbs[oi + 1 < NO ? oi + 1 : oi] : 0;
-      const int64_t ne = oi + 1 < NO ? pes[oi + 1 < NO ? oi + 1 : oi] : 0;
-      if (nst == 0) {
-        ld_ix(nb, ne, S2[0]);
-        continue;
-      }
-      for (int64_t t = 0; t < nst; t += 2) {
-        const int64_t p = pb + 32 * t;
-        ld_ix(p + 32, pe, S2[1]);
-        if (p < pe) step(oi, p, pe, S2[0]);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S2[0].i[k]), "v"(S2[0].j[k]));
-        if (t + 2 < nst) ld_ix(p + 64, pe, S2[0]);
-        else ld_ix(nb, ne, S2[0]);
-        if (p + 32 < pe) step(oi, p + 32, pe, S2[1]);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(S2[1].i[k]), "v"(S2[1].j[k]));
-      }
-    }
-  }
-  const int64_t cc = (int64_t)c_in * c_out;
-#pragma unroll
-  for (int oi = 0; oi < NO; ++oi) {
-    const int o = wave + NW * oi;
-    if (o >= K) break;
-    float* so = slab + (grp * K + o) * cc;
-#pragma unroll
-    for (int sa = 0; sa < 2; ++sa)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          so[(int64_t)(m0 + 2 * (4 * q + j) + sa) * c_out + n0 + 2 * r + t] = acc[oi][sa][t][j];
-  }
-}
-
-int64_t wgrad_band_n_sub(int64_t n_rows) { return ceil_div(n_rows, (int64_t)kBandRows); }
-
-// band groups per launch: about 512 blocks (2 per CU at 80 KiB of LDS each)
-int64_t wgrad_band_groups(int64_t n_rows, int c_in, int c_out, int& S) {
-  const int64_t n_sub = wgrad_band_n_sub(n_rows);
-  const int64_t n_tiles = (int64_t)(c_in / 32) * (c_out / 32);
-  int64_t sp = ceil_div(n_sub * n_tiles, (int64_t)512);
-  if (sp < 1) sp = 1;
-  S = (int)sp;
-  return ceil_div(n_sub, sp);
-}
-
-int launch_wgrad_band(const float* x, int c_in, const float* dy, int c_out, const int32_t* pin,
-                      const int32_t* pout, const int64_t* seg, int K, int64_t n_rows, int64_t n_groups, int S,
-                      float* slab, hipStream_t s) {
-  const int n_tiles = (c_in / 32) * (c_out / 32);
-  const unsigned grid = (unsigned)(n_groups * n_tiles);
-  const int64_t n_sub = wgrad_band_n_sub(n_rows);
-  const int no = (K + 7) / 8;  // 8 waves per block, offsets o = wave + 8 oi
-#define LB(N)                                                                                                \
-  if (no <= N) {                                                                                             \
-    wgrad_band_kernel<N, 8><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, pin, pout, seg, K, n_rows, n_sub, S,      \
-                                                 n_tiles, slab);                                             \
-    return MSP_OK;                                                                                           \
-  }
-  LB(1) LB(4)
-#undef LB
-  return MSP_EINVAL;
-}
-
-int launch_wgrad_band_seg(const int32_t* pout, const int64_t* off_start, int K, int64_t n_rows, int64_t* seg,
-                          hipStream_t s) {
-  const int64_t n_sub = wgrad_band_n_sub(n_rows);
-  const int64_t n = (int64_t)K * (n_sub + 1);
-  wgrad_band_seg_kernel<<<(unsigned)ceil_div(n, (int64_t)256), 256, 0, s>>>(pout, off_start, K, n_sub, seg);
-  return MSP_OK;
-}
-
-// dW tile of the x6 weight gradient: WA in {4, 3, 2, 1} (largest dividing
-// c_in / 16), WB in {2, 1} (registers: two value sets of 8 pairs each).
-static int g_wgrad_wa = 0, g_wgrad_wb = 0;  // msp_debug_wgrad_tile: forced tile (experiments)
-
+// dW tile of the x6 weight gradient: WA in {4, 3, 2, 1} (largest dividing c_in / 16), WB in {2, 1} (registers:
+// two value sets of 8 pairs each).
 void wgrad_x6_tile(int c_in, int c_out, int& wa, int& wb) {
   const int a = c_in / 16, bb = c_out / 16;
   wa = a % 4 == 0 ? 4 : (a % 3 == 0 ? 3 : (a % 2 == 0 ? 2 : 1));
   wb = bb % 2 == 0 ? 2 : 1;
-  if (g_wgrad_wa > 0 && a % g_wgrad_wa == 0) wa = g_wgrad_wa;
-  if (g_wgrad_wb > 0 && bb % g_wgrad_wb == 0) wb = g_wgrad_wb;
 }
-
-static int g_wgrad_abl = 0;  // msp_debug_wgrad_abl: ablation variants of the x6 weight gradient
 
 int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
                     const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
@@ -1439,58 +1016,17 @@ int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const 
   wgrad_x6_tile(c_in, c_out, WA, WB);
   const int n_ty = (c_in / (16 * WA)) * (c_out / (16 * WB));
   const unsigned grid = (unsigned)(n_pieces * K * n_ty);
-  bool launched = false;
 #define LW(A, B)                                                                                          \
-  if (!launched && WA == A && WB == B) {                                                                  \
+  if (WA == A && WB == B) {                                                                               \
     wgrad_x6_kernel<A, B><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, K, \
                                                     n_pieces, n_ty, slab);                               \
-    launched = true;                                                                                      \
+    return MSP_OK;                                                                                        \
   }
-#define LWA(A, B, AB)                                                                                     \
-  if (!launched && WA == A && WB == B && g_wgrad_abl == AB) {                                             \
-    wgrad_x6_kernel<A, B, AB><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, \
-                                                        K, n_pieces, n_ty, slab);                         \
-    launched = true;                                                                                      \
-  }
-#define LWD(A, B)                                                                                             \
-  if (!launched && WA == A && WB == B && (g_wgrad_abl & 16)) {                                               \
-    wgrad_x6_kernel<A, B, 0, 1><<<grid, kThreads, 0, s>>>(x, c_in, dy, c_out, pair_in, pair_out, off_start, \
-                                                          K, n_pieces, n_ty, slab);                         \
-    launched = true;                                                                                         \
-  }
-  LWD(2, 2) LWD(3, 2) LWD(4, 2)
-#undef LWD
-  if (g_wgrad_abl) {
-    LWA(2, 2, 1) LWA(4, 2, 1) LWA(2, 2, 2) LWA(4, 2, 2) LWA(2, 2, 3) LWA(4, 2, 3)
-    LWA(2, 2, 4) LWA(4, 2, 4) LWA(2, 2, 8) LWA(4, 2, 8) LWA(2, 2, 12) LWA(4, 2, 12) LWA(2, 2, 15) LWA(4, 2, 15)
-  }
-#undef LWA
   LW(1, 1) LW(2, 1) LW(3, 1) LW(4, 1) LW(1, 2) LW(2, 2) LW(3, 2) LW(4, 2)
 #undef LW
-  return launched ? MSP_OK : MSP_EINVAL;
+  return MSP_EINVAL;
 }
 
-}  // namespace msp
-
-extern "C" int msp_debug_wgrad_tile(int wa, int wb) {
-  msp::g_wgrad_wa = wa;
-  msp::g_wgrad_wb = wb;
-  return MSP_OK;
-}
-
-extern "C" int msp_debug_wgrad_abl(int abl) {
-  msp::g_wgrad_abl = abl;
-  return MSP_OK;
-}
-
-namespace msp {
-
-
-}  // namespace msp
-
-using namespace msp;
-
-namespace msp {
 
 // Plan (measured on the headline batch's rulebooks, scripts/kbench_x6.py,
 // profiles/r01/kbench_x6_*.log): 32-deep k-slices everywhere (fewer
@@ -1500,10 +1036,10 @@ namespace msp {
 // divides) with double-buffered weights.  Small grids split each tile's
 // offsets over up to 8 blocks (partials reduced in split order).  Pipeline
 // depth 2 (3 and 4 measured no faster).
-PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks, int tile_rows) {
+PlanX6 plan_x6(int64_t n_rows, int c_out) {
   const int n16 = c_out / 16;
-  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
-  PlanX6 p{1, 32, 1, 1, 2, 0, tile_rows, 2};
+  const int64_t n_tiles = ceil_div(n_rows, 128);
+  PlanX6 p{1, 1, 1, 2};
   if (n16 % 4 == 0 && n_tiles * (n16 / 4) >= 256) {
     p.nt = 4;
     p.nb = 1;
@@ -1515,9 +1051,6 @@ PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks, int tile_r
       }
     }
   }
-  if (force_nt > 0) p.nt = force_nt;
-  if (force_ks > 0) p.ks = force_ks;
-  if (p.nt != 4) p.nb = 2;
   p.n_y = n16 / p.nt;
   const int64_t blocks = n_tiles * p.n_y;
   if (blocks < 1024) {
@@ -1528,15 +1061,15 @@ PlanX6 plan_x6(int64_t n_rows, int c_out, int force_nt, int force_ks, int tile_r
 }
 
 namespace {
-size_t x6_weight_bytes(int K, int c_in, int c_out, int ks) {
-  const int64_t c_pad = ceil_div(c_in, ks) * ks;
+size_t x6_weight_bytes(int K, int c_in, int c_out) {
+  const int64_t c_pad = ceil_div(c_in, 32) * 32;
   return (size_t)K * 3 * (size_t)c_out * (size_t)c_pad * 2;
 }
 size_t round256(size_t b) { return (b + 255) & ~(size_t)255; }
 }  // namespace
 
 size_t x6_ws_bytes(int64_t n_rows, int K, int c_in, int c_out, const PlanX6& p) {
-  size_t b = round256(x6_weight_bytes(K, c_in, c_out, p.ks));
+  size_t b = round256(x6_weight_bytes(K, c_in, c_out));
   if (p.split > 1) b += (size_t)p.split * (size_t)n_rows * (size_t)c_out * sizeof(float);
   return b;
 }
@@ -1544,40 +1077,27 @@ size_t x6_ws_bytes(int64_t n_rows, int K, int c_in, int c_out, const PlanX6& p) 
 int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
               const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
               const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s) {
-  const int64_t n_tiles = ceil_div(n_rows, p.tr);
+  const int64_t n_tiles = ceil_div(n_rows, 128);
   u32x4* wsp = static_cast<u32x4*>(ws);
-  const int64_t units = (int64_t)x6_weight_bytes(K, c_in, c_out, p.ks) / 16;
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * p.nt, p.ks, wsp,
+  const int64_t units = (int64_t)x6_weight_bytes(K, c_in, c_out) / 16;
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * p.nt, 32, wsp,
                                                                        (flip >> 1) & 1);
   flip &= 1;
-  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + round256(x6_weight_bytes(K, c_in, c_out, p.ks)));
+  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + round256(x6_weight_bytes(K, c_in, c_out)));
   float* dst = p.split > 1 ? part : out;
   const unsigned grid = (unsigned)(n_tiles * p.n_y * p.split);
   bool launched = false;
-#define LD(N, S, DD, B)                                                                                       \
-  if (!launched && p.nt == N && p.ks == S && p.depth == DD && p.nb == B && !p.abl && p.tr == 128) {          \
-    conv_x6d_kernel<N, S, DD, 128, 0, B><<<grid, kThreads, 0, s>>>(x, c_in, wsp, K, flip, c_out, tile_start,  \
+#define LD(N, B)                                                                                              \
+  if (!launched && p.nt == N && p.nb == B) {                                                                  \
+    conv_x6d_kernel<N, 32, 2, 128, 0, B><<<grid, kThreads, 0, s>>>(x, c_in, wsp, K, flip, c_out, tile_start,  \
                                                                    chunk_off, chunk_src, chunk_row, n_rows,  \
                                                                    p.n_y, p.split, dst);                     \
     launched = true;                                                                                          \
   }
-#define LA(A)                                                                                                 \
-  if (!launched && p.nt == 4 && p.ks == 32 && p.depth == 2 && p.abl == A) {                                  \
-    conv_x6d_kernel<4, 32, 2, 128, A><<<grid, kThreads, 0, s>>>(x, c_in, wsp, K, flip, c_out, tile_start,    \
-                                                                chunk_off, chunk_src, chunk_row, n_rows,     \
-                                                                p.n_y, p.split, dst);                        \
-    launched = true;                                                                                          \
-  }
-  if (p.abl) {
-    LA(1) LA(2) LA(4) LA(8) LA(16) LA(32) LA(48) LA(63)
-  }
-#undef LA
-  // production (plan_x6) and the variants scripts/kbench_x6.py compares
-  LD(4, 32, 2, 1) LD(4, 32, 2, 2) LD(3, 32, 2, 2) LD(2, 32, 2, 2) LD(1, 32, 2, 2)
-  LD(3, 64, 2, 2) LD(2, 64, 2, 2) LD(4, 32, 3, 1) LD(4, 64, 2, 1) LD(3, 64, 2, 1) LD(3, 32, 2, 1)
+  LD(4, 1) LD(4, 2) LD(3, 2) LD(2, 2) LD(1, 2)
 #undef LD
   if (!launched) {
-    set_error("msp_conv_tile: no x6 kernel for nt=%d ks=%d depth=%d", p.nt, p.ks, p.depth);
+    set_error("msp_conv_tile: no x6 kernel for nt=%d nb=%d", p.nt, p.nb);
     return MSP_EINVAL;
   }
   if (p.split > 1) {
@@ -1590,18 +1110,13 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
 
 }  // namespace msp
 
+using namespace msp;
+
 extern "C" {
 
-// Dense row-group form on the large levels with c_out >= 64 (measured against
-// msp_conv_tile on the headline batch, profiles/r01/kbench_nbr_r01v.log: L0
-// 32->64 -13 %, L1 64->64 -3 %, L2 96->96 -9 %, 192->96 -6 %; the narrow
-// per-wave form stays ahead for c_out = 32 and the shared tile below 10^5 rows).
-static int g_nbr_variant = 0;  // msp_debug_conv_nbr_variant (experiments: scripts/bench_ab.py)
-int msp_debug_conv_nbr_variant(int g) {
-  g_nbr_variant = g;
-  return 0;
-}
-
+// Dense row-group form on the large levels with c_out >= 64 (measured against msp_conv_tile on the headline
+// batch, profiles/r01/kbench_nbr_r01v.log: L0 32->64 -13 %, L1 64->64 -3 %, L2 96->96 -9 %, 192->96 -6 %; the
+// narrow per-wave form stays ahead for c_out = 32 and the shared tile below 10^5 rows).
 int msp_conv_nbr_preferred(int64_t n_rows, int c_in, int c_out) {
   (void)c_in;
   return n_rows >= 100000 && c_out >= 64 && c_out % 16 == 0 ? 1 : 0;
@@ -1622,55 +1137,8 @@ int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int
   MSP_REQUIRE(x && wt && nbr && out, "msp_conv_nbr: null pointer");
   const size_t need = x6g_ws_bytes(K, c_in, c_out);
   MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_nbr: workspace too small (%zu < %zu)", ws_bytes, need);
-  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream), 0,
-                            g_nbr_variant);
+  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream));
   return rc ? rc : check_launch("msp_conv_nbr");
-}
-
-// Experiment hook (not part of the public ABI; scripts/kbench_nbr.py): the
-// dense row-group form with NT / G forced (0 = the plan's choice).  With
-// ws == nullptr returns the workspace bytes needed.
-int64_t msp_debug_conv_nbr(int nt, int g, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
-                           const int32_t* nbr, const int32_t* perm, int64_t n_rows, float* out, void* ws,
-                           size_t ws_bytes, msp_stream_t stream) {
-  const size_t need = x6g_ws_bytes(K, c_in, c_out);
-  if (!ws) return (int64_t)need;
-  MSP_REQUIRE(ws_bytes >= need, "msp_debug_conv_nbr: workspace too small");
-  MSP_REQUIRE(c_in % 16 == 0 && c_out % 16 == 0, "msp_debug_conv_nbr: channels must be multiples of 16");
-  if (n_rows == 0) return 0;
-  const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream), nt, g);
-  return rc ? rc : check_launch("msp_debug_conv_nbr");
-}
-
-// Experiment hook (not part of the public ABI; scripts/kbench_conv.py): the
-// x6 shared-tile form with NT / KS forced (0 = the plan's choice).  With
-// ws == nullptr returns the workspace bytes needed.
-int64_t msp_debug_conv_x6(int nt, int ks, int depth, int abl, int tile_rows, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
-                          const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
-                          const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
-                          msp_stream_t stream) {
-  if (abl >= 512 && abl <= 514) {  // per-wave forms regardless of the channel counts (c_in <= 64)
-    const size_t needp = x6p_ws_bytes(K, c_in, c_out);
-    if (!ws) return (int64_t)needp;
-    const int rc = launch_x6p(x, c_in, wt, K, flip, c_out, tile_rows > 0 ? tile_rows : 128, tile_start,
-                              chunk_off, chunk_src, chunk_row, n_rows, out, ws, as_stream(stream), nt, depth,
-                              abl - 512);
-    return rc ? rc : check_launch("msp_debug_conv_x6");
-  }
-  PlanX6 p = plan_x6(n_rows, c_out, nt, ks, tile_rows > 0 ? tile_rows : 128);
-  if (depth > 0) p.depth = depth;
-  if (abl >= 256) {  // 256 + nb: weight buffer count forced
-    p.nb = abl - 256;
-  } else {
-    p.abl = abl;
-  }
-  MSP_REQUIRE((c_out / 16) % p.nt == 0, "msp_debug_conv_x6: nt %d does not divide c_out/16", p.nt);
-  const size_t need = x6_ws_bytes(n_rows, K, c_in, c_out, p);
-  if (!ws) return (int64_t)need;
-  MSP_REQUIRE(ws_bytes >= need, "msp_debug_conv_x6: workspace too small");
-  const int rc = launch_x6(p, x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows, out,
-                           ws, as_stream(stream));
-  return rc ? rc : check_launch("msp_debug_conv_x6");
 }
 
 }  // extern "C"

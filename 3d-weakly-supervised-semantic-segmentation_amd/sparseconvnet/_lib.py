@@ -37,19 +37,12 @@ PROTOTYPES = {
     "msp_tile_local_workspace_size": (SZ, [I64, I]),
     "msp_tile_local": (I, [P, I, I64, I, P, P, I64, P, P, P, SZ, P]),
     "msp_conv_local_preferred": (I, [I64, I, I]),
-    "msp_chunk_local_cap": (I64, [I]),
-    "msp_chunk_local": (I, [P, I64, I, I, P, P, P, P, P, P, P]),
-    "msp_conv_chunk_local_preferred": (I, [I64, I, I]),
     "msp_wgrad_chunk_ok": (I, [I64, I, I, I]),
     "msp_wgrad_chunk_preferred": (I, [I64, I, I, I]),
     "msp_wgrad_chunk_ranges": (I64, [I64, I, I]),
     "msp_wgrad_chunk_cap": (I64, []),
-    "msp_wgrad_chunk_index": (I, [P, P, P, I64, P, P, P, P]),
+    "msp_wgrad_chunk_index": (I, [P, P, P, I64, P, P, P, P, P]),
     "msp_conv_wgrad_chunk": (I, [P, I, P, I, I, I, P, P, P, P, P, I64, I64, P, P, P]),
-    "msp_conv_chunk_local": (I, [P, I, P, I, I, I, I, P, P, P, P, P, P, I64, P, P, SZ, P]),
-    "msp_wgrad_local_ok": (I, [I64, I, I, I]),
-    "msp_wgrad_local_ranges": (I64, [I64, I, I]),
-    "msp_conv_wgrad_local": (I, [P, I, P, I, I, I, P, P, P, P, I64, I64, P, P, P]),
     "msp_conv_local_workspace_size": (SZ, [I, I, I]),
     "msp_conv_local": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_tile_rows": (I, [I64, I, I]),
@@ -64,11 +57,6 @@ PROTOTYPES = {
     "msp_conv_pairs": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
     "msp_wgrad_pieces": (I64, [I64, I, I, I]),
     "msp_conv_wgrad": (I, [P, I, P, I, P, P, P, I, I64, P, P, P]),
-    "msp_wgrad_band_ok": (I, [I64, I, I, I]),
-    "msp_wgrad_band_groups": (I64, [I64, I, I]),
-    "msp_wgrad_band_seg_len": (I64, [I64, I]),
-    "msp_wgrad_band_segments": (I, [P, P, I, I64, P, P]),
-    "msp_conv_wgrad_band": (I, [P, I, P, I, P, P, P, I, I64, P, P, P]),
     "msp_bn_partials": (I64, [I64, I]),
     "msp_bn_stats": (I, [P, I64, I, P, P]),
     "msp_bn_finalize": (I, [P, I64, I, D, D, I, P, P, P, P, P, P]),

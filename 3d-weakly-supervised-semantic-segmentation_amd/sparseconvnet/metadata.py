@@ -79,31 +79,6 @@ def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS):
                 max_u=max_u)
 
 
-CHUNK_TILE_ROWS = 64   # rulebook tiles of msp_conv_chunk_local (two per 128-row unit)
-
-
-def chunk_local_index(tiles, n, device, s, with_max=False):
-    """msp_chunk_local over a tile rulebook (64-row tiles: two per 128-row unit, the convolution's index; 128-row
-    tiles: one per unit, the weight gradient's): per unit the sorted distinct input rows its chunks name (first
-    msp_chunk_local_cap of them, -1 after) and per chunk entry (position in that list | row in unit << 16).
-    with_max: also the largest unit's count (one host read)."""
-    tr = int(tiles["tile_rows"])
-    n_tiles = (n + tr - 1) // tr
-    n_units = (n_tiles + 128 // tr - 1) // (128 // tr)
-    cap = int(query("msp_chunk_local_cap", tr))
-    u_rows = torch.empty(max(n_units * cap, 1), dtype=torch.int32, device=device)
-    u_cnt = torch.empty(max(n_units, 1), dtype=torch.int32, device=device)
-    chunk_lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=device)  # uint32 bits
-    mx = torch.zeros(1, dtype=torch.int64, device=device) if with_max else None
-    if n_units:
-        call("msp_chunk_local", ptr(tiles["tile_start"]), I64(n), tr, int(tiles["max_chunks"]),
-             ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), ptr(u_rows), ptr(u_cnt), ptr(chunk_lr), ptr(mx), s)
-    out = dict(tiles=tiles, u_rows=u_rows, u_cnt=u_cnt, chunk_lr=chunk_lr, n_units=n_units, cap=cap)
-    if with_max:
-        out["max_u"] = int(mx.item()) if n_units else 0
-    return out
-
-
 class PairLists:
     """Per-offset (in, out) pair lists of an offset-major map, plus the chunk
     and block partitions used by msp_conv_pairs / msp_conv_wgrad.
@@ -113,7 +88,9 @@ class PairLists:
     `pair_in` / `pair_out` (recorded in the plan, so a prefetch of the next
     batch builds them ahead): at levels whose convolutions and weight gradients
     all run on the tile-local / chunk forms nothing reads them.  The fill needs
-    no host read, so a first use inside a graph capture is captured."""
+    no host read, so a first use inside a graph capture is captured; the fill reads the block offsets the
+    count left in its workspace, so the workspace stays on the object (and with it in Metadata.tensors(), which
+    a capturer keeps alive and a consumer stream marks) for as long as the lists may be filled."""
 
     def __init__(self, m, K, n, device, s, plan=None, key=None):
         nrb = max(1, (n + 2047) // 2048)
@@ -124,7 +101,8 @@ class PairLists:
         starts = self.off_start.tolist()
         self.total = int(starts[-1])
         self.counts = [starts[o + 1] - starts[o] for o in range(K)]
-        self._m, self._n, self._ws, self._dev = m, n, ws, device  # the filling call reuses the count's workspace
+        # the filling call reuses the count's workspace (kept: a fill captured into a graph reads it at replay)
+        self._m, self._n, self._ws, self._dev = m, n, ws, device
         self._plan, self._key = plan, key
         self._pin = self._pout = None
         self.K = K
@@ -144,7 +122,7 @@ class PairLists:
             if self.total:
                 call("msp_pair_lists", ptr(self._m), self.K, self._n, ptr(pin), ptr(pout), self.total,
                      ptr(self.off_start), ptr(self._ws), self._ws.numel(), _lib.stream(self._dev))
-            self._pin, self._pout, self._ws = pin, pout, None
+            self._pin, self._pout = pin, pout
         return self
 
     @property
@@ -173,7 +151,6 @@ class SubmRules:
                  ptr(self.nbr), s)
         self._tiles = {}
         self._locals = {}
-        self._chunk = None
         self._wchunk = None
         self._dense = None
         self._map, self._n = self.nbr, V
@@ -210,15 +187,6 @@ class SubmRules:
                                                          _lib.stream(self.nbr.device), tile_rows)
         return t
 
-    def chunk_local(self):
-        """Unit-local index of the 64-row tile rulebook (msp_chunk_local) for msp_conv_chunk_local, built on first
-        use: per 128-row unit the distinct input rows of its chunks, per chunk entry its position there."""
-        if self._chunk is None:
-            tiles = self.tiles_for(CHUNK_TILE_ROWS)
-            self._plan.append(("chunk", self._key))
-            self._chunk = chunk_local_index(tiles, self._n, self.nbr.device, _lib.stream(self.nbr.device))
-        return self._chunk
-
     def wgrad_index(self):
         """msp_wgrad_chunk_index over the 128-row tile rulebook and the tile-local rulebook (which lists each
         tile's distinct input rows) for msp_conv_wgrad_chunk, built on first use.  None when a tile names more
@@ -231,10 +199,10 @@ class SubmRules:
                 tiles = self.tiles_for(128)
                 self._plan.append(("wchunk", self._key))
                 lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=self.nbr.device)
-                if self._n:
+                if self._n:  # no rule can lie past the cap (checked above): no overflow count needed
                     call("msp_wgrad_chunk_index", ptr(tiles["tile_start"]), ptr(tiles["chunk_src"]),
                          ptr(tiles["chunk_row"]), I64(self._n), ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(lr),
-                         _lib.stream(self.nbr.device))
+                         None, _lib.stream(self.nbr.device))
                 self._wchunk = dict(tiles=tiles, chunk_lr=lr, u_start=loc["u_start"], u_rows=loc["u_rows"])
         return self._wchunk or None
 
@@ -452,7 +420,9 @@ class Metadata:
         from . import ops
         used = {e[1] for e in plan if e[0] == "use"}
         for entry in plan:
-            if entry[0] in ("tiles", "dense", "local", "chunk", "wchunk") and entry[1] in used:
+            # what the recorded uses select is rebuilt by ops.prepare; pair lists too (the weight gradient falls
+            # back to them only when its chunk form does not fit, the strided consumers record a "pairs" use)
+            if entry[0] in ("tiles", "dense", "local", "wchunk", "pairs") and entry[1] in used:
                 continue
             if entry[0] == "use":
                 rules = self._rules(entry[1])
@@ -468,8 +438,6 @@ class Metadata:
                 self._rules(entry[1]).dense_order()
             elif entry[0] == "local":
                 self._rules(entry[1]).local(entry[2])
-            elif entry[0] == "chunk":
-                self._rules(entry[1]).chunk_local()
             elif entry[0] == "wchunk":
                 self._rules(entry[1]).wgrad_index()
             elif entry[0] == "pairs":

@@ -55,15 +55,12 @@ def _record(kind, flops, fn, nbytes=0):
 
 # ------------------------------------------------------------------ convolution helpers
 def conv_form(rules, n_rows, c_in, c_out, K):
-    """Which form (and so which rulebook) the convolution over `rules` takes for these sizes: "local", "chunk",
-    "nbr", or the tile height of msp_conv_tile -- the library's preference queries."""
+    """Which form (and so which rulebook) the convolution over `rules` takes for these sizes: "local", "nbr", or
+    the tile height of msp_conv_tile -- the library's preference queries."""
     nbr = getattr(rules, "nbr", None)  # submanifold rules carry the neighbour map
-    if nbr is not None and n_rows and K <= 27 and CONV_LOCAL and \
+    if nbr is not None and n_rows and K <= 27 and \
             int(_lib.query("msp_conv_local_preferred", _lib.I64(n_rows), c_in, c_out)):
         return "local"
-    if nbr is not None and n_rows and K <= 27 and CONV_CHUNK and \
-            int(_lib.query("msp_conv_chunk_local_preferred", _lib.I64(n_rows), c_in, c_out)):
-        return "chunk"
     if nbr is not None and n_rows and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(n_rows), c_in, c_out)):
         return "nbr"
     return int(_lib.query("msp_conv_tile_rows", _lib.I64(n_rows), c_in, c_out))
@@ -79,20 +76,17 @@ def prepare(rules, purpose, c_in, c_out):
         f = conv_form(rules, n, c_in, c_out, K)
         if f == "local":
             rules.local()
-        elif f == "chunk":
-            rules.chunk_local()
         elif f == "nbr":
             rules.dense_order()
         else:
             rules.tiles_for(f)
     elif purpose == "wgrad":
-        if WGRAD_CHUNK and int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(n), K, c_in, c_out)):
+        if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(n), K, c_in, c_out)):
             if rules.wgrad_index() is not None:
                 return
-        if WGRAD_LOCAL and int(_lib.query("msp_wgrad_local_ok", _lib.I64(n), K, c_in, c_out)):
-            rules.local()
-        else:
-            rules.pairs.fill()
+        rules.pairs.fill()
+    elif purpose == "pairs":  # strided convolution backward, deconvolution: one contribution per pair
+        rules.pairs.fill()
 
 
 def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
@@ -104,8 +98,6 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     f = conv_form(rules, n_rows, c_in, c_out, K)
     if f == "local":
         return conv_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
-    if f == "chunk":
-        return conv_chunk_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
     if f == "nbr":
         perm, nbr_p = rules.dense_order()
         return conv_nbr(x, wt, K, flip, c_out, nbr_p, n_rows, kind, flops, perm)
@@ -130,10 +122,6 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
     return out[:n_rows]
 
 
-# tile-local submanifold convolution (msp_conv_local) where the library prefers it; False: the gather forms
-CONV_LOCAL = True
-
-
 def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0):
     """Submanifold convolution over the tile-local rulebook (SubmRules.local): each 128-row tile's distinct
     input rows staged in LDS and split once (msp_conv_local)."""
@@ -149,30 +137,6 @@ def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0)
         "msp_conv_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
         ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), n_rows, ptr(out), ptr(ws), wsb, _stream(x)),
         nbytes)
-    return out[:n_rows]
-
-
-# chunk-local submanifold convolution (msp_conv_chunk_local) where the library prefers it (level 0 of m = 32)
-CONV_CHUNK = True
-
-
-def conv_chunk_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_chunk", flops=0):
-    """Submanifold convolution over the 64-row tile rulebook with each 128-row unit's distinct input rows staged
-    in LDS (SubmRules.chunk_local, msp_conv_chunk_local)."""
-    c_in = x.size(1)
-    loc = rules.chunk_local()
-    tiles = loc["tiles"]
-    out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
-    wsb = int(_lib.query("msp_conv_local_workspace_size", K, c_in, c_out))
-    ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
-    # compulsory bytes: input rows, output rows, weights, the rulebook (chunk offsets, one packed word per
-    # chunk entry, tile starts) and the units' distinct-row lists
-    nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
-        tiles["n_chunks"] * (1 + 16 * 4) + 8 * tiles["tile_start"].numel() + 4 * loc["u_rows"].numel()
-    _record(kind + "/x6q", flops, lambda: call(
-        "msp_conv_chunk_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tiles["tile_rows"],
-        ptr(tiles["tile_start"]), ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(loc["chunk_lr"]),
-        ptr(loc["u_rows"]), ptr(loc["u_cnt"]), n_rows, ptr(out), ptr(ws), wsb, _stream(x)), nbytes)
     return out[:n_rows]
 
 
@@ -222,25 +186,6 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None, kind="wgrad"):
     return dw, join
 
 
-def conv_wgrad_band(x, dy, pairs, K, n_rows):
-    """Submanifold weight gradient with the rows staged in LDS per 256-row band
-    (msp_conv_wgrad_band); pairs = the rules' pair lists (ascending output row
-    per offset), their band segments cached on them."""
-    c_in, c_out = x.size(1), dy.size(1)
-    seg = getattr(pairs, "_band_seg", None)
-    if seg is None:
-        seg = torch.empty(int(_lib.query("msp_wgrad_band_seg_len", _lib.I64(n_rows), K)), dtype=torch.int64,
-                          device=x.device)
-        call("msp_wgrad_band_segments", ptr(pairs.pair_out), ptr(pairs.off_start), K, n_rows, ptr(seg), _stream(x))
-        pairs._band_seg = seg
-    dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
-    n_groups = int(_lib.query("msp_wgrad_band_groups", _lib.I64(n_rows), c_in, c_out))
-    slab = torch.empty((n_groups, K, c_in, c_out), dtype=torch.float32, device=x.device)
-    call("msp_conv_wgrad_band", ptr(x), c_in, ptr(dy), c_out, ptr(pairs.pair_in), ptr(pairs.pair_out), ptr(seg), K,
-         n_rows, ptr(slab), ptr(dw), _stream(x))
-    return dw
-
-
 def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
     c_in, c_out = x.size(1), dy.size(1)
     dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
@@ -254,36 +199,6 @@ def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
         "msp_conv_wgrad", ptr(x), c_in, ptr(dy), c_out, ptr(pin), ptr(pout), ptr(pairs.off_start), K,
         n_pieces, ptr(slab), ptr(dw), _stream(x)), nbytes)
     return dw
-
-
-# tile-local weight gradient (msp_conv_wgrad_local) instead of the pair-list form where it applies.  Off: on the
-# headline batch it ran 0.84-1.2x the pair-list form's speed (scripts/kbench_wgrad_local.py,
-# profiles/r02/kbench_wgrad_local_r02.log) -- its dense 32-row steps carry ~45 % zero rows, the pair lists none.
-WGRAD_LOCAL = False
-
-
-def conv_wgrad_local(x, dy, rules, K, kind="wgrad", flops=None):
-    """Submanifold weight gradient over the tile-local rulebook (SubmRules.local): per tile the distinct x rows
-    and the dy rows staged in LDS once; partial sums per tile range added in order (msp_conv_wgrad_local)."""
-    c_in, c_out = x.size(1), dy.size(1)
-    n = dy.size(0)
-    loc = rules.local()
-    ranges = int(_lib.query("msp_wgrad_local_ranges", _lib.I64(n), c_in, c_out))
-    dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
-    slab = torch.empty((ranges, K, c_in, c_out), dtype=torch.float32, device=x.device)
-    if flops is None:
-        flops = 2.0 * rules.n_rules * c_in * c_out
-    # compulsory bytes: x and dy rows, the tile-local rulebook, dW
-    nbytes = 4 * (x.size(0) * c_in + n * c_out + K * c_in * c_out) + \
-        4 * loc["total"] + 2 * K * loc["n_tiles"] * loc["tile_rows"] + 4 * loc["n_tiles"] * loc["tile_rows"]
-    _record(kind + "/x6t", flops, lambda: call(
-        "msp_conv_wgrad_local", ptr(x), c_in, ptr(dy), c_out, K, loc["tile_rows"], ptr(loc["lidx"]),
-        ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), n, ranges, ptr(slab), ptr(dw), _stream(x)), nbytes)
-    return dw
-
-
-# chunk-local weight gradient (msp_conv_wgrad_chunk) for submanifold convolutions where the library prefers it
-WGRAD_CHUNK = True
 
 
 def conv_wgrad_chunk(x, dy, rules, K, kind="wgrad", flops=None):
@@ -361,15 +276,9 @@ class SubmanifoldConvFunction(torch.autograd.Function):
             V = xp.size(0)
             dwp = None
             rules.note_use("wgrad", cin_p, cout_p)
-            if WGRAD_CHUNK and int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)):
+            if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)):
                 dwp = conv_wgrad_chunk(xp, g, rules, K, flops=2.0 * p.total * cin * cout)
-            if dwp is not None:
-                pass
-            elif WGRAD_LOCAL and int(_lib.query("msp_wgrad_local_ok", _lib.I64(V), K, cin_p, cout_p)):
-                dwp = conv_wgrad_local(xp, g, rules, K, flops=2.0 * p.total * cin * cout)
-            elif int(_lib.query("msp_wgrad_band_ok", _lib.I64(V), K, cin_p, cout_p)):
-                dwp = conv_wgrad_band(xp, g, p, K, V)  # rows staged in LDS per band
-            else:  # weight gradient beside the backward-data (opt-in)
+            if dwp is None:  # pair lists (beside the backward-data when WGRAD_CONCURRENT)
                 dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
@@ -403,6 +312,7 @@ class ConvolutionFunction(torch.autograd.Function):
         rules, (cin, cout) = ctx.rules, ctx.dims
         K, cin_p, cout_p = wp.shape
         g = _pad_cols(gout.contiguous(), cout_p)
+        rules.note_use("pairs", 0, 0)
         p = rules.pairs
         dx = dw = None
         join = None
@@ -431,6 +341,7 @@ class DeconvolutionFunction(torch.autograd.Function):
         xp = _pad_cols(x.contiguous(), cin_p)
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
         wt = wp.transpose(1, 2).contiguous()
+        rules.note_use("pairs", 0, 0)  # the forward and both backward passes run on the pair lists
         p = rules.pairs
         out = conv_pairs(xp, wt, K, cout_p, p, p.pair_out, p.pair_in, n_fine, "deconv_fwd", 2.0 * p.total * cin * cout)
         ctx.save_for_backward(xp, wp)

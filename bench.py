@@ -88,7 +88,7 @@ class KernelRecorder:
         self.active = False
         self.mode = mode
         # events created up front and reused: creating two per call inside the timed steps cost ~3 ms of host
-        # time per step (scripts/bench_ab.py norec vs rec)
+        # time per step
         self.pool = [torch.cuda.Event(enable_timing=True) for _ in range(pool if mode != "none" else 0)]
         self.used = 0
 
@@ -325,7 +325,7 @@ def main():
 
     _lib.load()
     from sparseconvnet import ops as scn_ops
-    scn_ops.WGRAD_CONCURRENT = bool(args.concurrent_wgrad)  # set both ways (scripts/bench_ab.py reruns main)
+    scn_ops.WGRAD_CONCURRENT = bool(args.concurrent_wgrad)
     # two distinct batches per rank, alternated step to step
     host_batches = [make_batch(args.batch, args.scale, seed=1000 * rank + k) for k in range(2)]
     contrastive = args.workload == "contrastive"

@@ -21,6 +21,10 @@
  *     to small device buffers that the caller copies back.
  *   - Return 0 on success, a negative MSP_E* code on failure; the message is
  *     thread-local and read with msp_last_error().
+ *   - Stateless and reentrant: no entry point reads or writes process-global
+ *     state (the only static is the cached CU count of the device); every
+ *     exported symbol is declared here (tests/test_abi.py checks the .so's
+ *     dynamic symbol table against this header).
  *   - Offset-major maps: a neighbour / child map with K filter offsets over n
  *     rows is stored [K][n] (entry -1 = absent).  Filter offsets follow SCN's
  *     last-axis-fastest order: o = ((dx*f) + dy)*f + dz over the f^3 box.
@@ -142,15 +146,15 @@ int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coo
  * Convolution / Deconvolution updateOutput + backward) */
 
 /* Output-stationary gather-MFMA convolution over a tile rulebook built with
- * the same tile_rows:
+ * tile_rows = 128 (msp_conv_tile_rows):
  *   out[r, :] = sum over chunks of r's tile: sum_j W'[o]^T x[src_j, :]
  * wt is [K][c_out][c_in] (k contiguous).  flip bit 0: offset o reads
  * wt[K-1-o] (submanifold backward-data with the forward weight layout);
  * bit 1 (128-row tiles): wt is given as [K][c_in][c_out] instead, the
  * module's own layout, so the forward needs no transposed copy.
- * c_in % 16 == 0, c_out % 16 == 0.  Every output row is written.
- * tile_rows 64: per-wave tiles; 128 / 256: one tile shared by the 4 waves of
- * a block.  With 128-row tiles and c_out > 32 (or c_in > 64) the contraction
+ * c_in % 16 == 0, c_out % 16 == 0.  Every output row is written.  Narrow
+ * outputs (c_out <= 32, c_in <= 64) run per-wave tiles, wider ones a tile
+ * shared by the 4 waves of a block; the contraction
  * runs on bf16 MFMA over exact three-piece bf16 splits of both fp32 operands
  * (six piece products, fp32 accumulation: fp32-class error, checked against
  * fp64 in tests/test_gpu_ops.py); the split weights and, on small grids, the
@@ -161,8 +165,7 @@ int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coo
 int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out);
 /* Contraction form msp_conv_tile runs for these sizes: 1 = per-wave split-bf16
  * tile (conv_x6r: c_out <= 32, c_in <= 64), 2 = shared split-bf16 tile (conv_x6d,
- * split over offsets on small grids), 3 = f32-MFMA tile forms (tile_rows 64 /
- * 256), 0 = nothing to do. */
+ * split over offsets on small grids), 0 = nothing to do (or tile_rows != 128). */
 int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows);
 
 /* Tile-local submanifold convolution (replaces the gather forms where
@@ -175,44 +178,21 @@ int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows);
  * msp_conv_local_workspace_size (the split weight image). */
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out);
 
-/* Submanifold weight gradient over the same tile-local rulebook: dW[o][ci][co] = sum over rows i of
- * x[nbr(i, o)][ci] dy[i][co] (the forward's [K][c_in][c_out] layout), each tile's distinct x rows and its dy
- * rows staged in LDS once.  Channels in multiples of 32, K <= 27 (msp_wgrad_local_ok).  Blocks run
- * n_ranges contiguous tile ranges (msp_wgrad_local_ranges) per 32 x 32 channel slice; slab holds
- * n_ranges x K x c_in x c_out floats of partial sums, added in range order into dw. */
-int msp_wgrad_local_ok(int64_t n_rows, int K, int c_in, int c_out);
-int64_t msp_wgrad_local_ranges(int64_t n_rows, int c_in, int c_out);
-int msp_conv_wgrad_local(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
-                         const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
-                         int64_t n_rows, int64_t n_ranges, float* slab, float* dw, msp_stream_t stream);
 size_t msp_conv_local_workspace_size(int K, int c_in, int c_out);
 int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                    const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
                    int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
-/* Chunk-local submanifold convolution (the narrow large levels: msp_conv_chunk_local_preferred, level 0 of the
- * m = 32 UNet).  Same sum as msp_conv_tile over a tile rulebook with tile_rows = 64 (K <= 27), with rows grouped
- * in 128-row units (two rulebook tiles): msp_chunk_local lists per unit u the distinct input rows its chunks
- * name, ascending, the first msp_chunk_local_cap() of them at u_rows[u * cap ..] and their count at u_cnt[u],
- * and writes per chunk entry e the word chunk_lr[e] = (position in that list, 0xFFFF past the cap) | (row
- * inside the unit, 128 for a padding slot) << 16; max_chunks = the rulebook's largest tile (<= 128).
- * tile_rows 128: a unit is one rulebook tile (cap msp_chunk_local_cap(128)).  max_count (device int64,
- * nullable) gets the largest unit's count.  The
- * convolution stages each unit's listed rows in LDS once per 32 input channels and accumulates the chunks'
- * partial products in LDS (entries past the cap read chunk_src from global memory).  c_in % 16 == 0,
- * c_out % 32 == 0; flip and weight layouts as msp_conv_tile; workspace msp_conv_local_workspace_size. */
-int64_t msp_chunk_local_cap(int tile_rows);
-int msp_chunk_local(const int64_t* tile_start, int64_t n_rows, int tile_rows, int max_chunks,
-                    const int32_t* chunk_src, const uint16_t* chunk_row, int32_t* u_rows, int32_t* u_cnt,
-                    uint32_t* chunk_lr, int64_t* max_count, msp_stream_t stream);
-int msp_conv_chunk_local_preferred(int64_t n_rows, int c_in, int c_out);
 /* Submanifold weight gradient over a 128-row tile rulebook (msp_tile_rulebook, tile_rows = 128) and the
  * tile-local rulebook of the same map (msp_tile_local, tile_rows = 128): dW[o][ci][co] = sum over the rules
  * (i, j) of offset o of x[i][ci] dy[j][co] (the forward's [K][c_in][c_out] layout).  msp_wgrad_chunk_index
  * writes per chunk entry e chunk_lr[e] = (position of its input row in its tile's u_rows list) | (row in the
  * tile, 128 for a padding slot) << 16.  msp_conv_wgrad_chunk stages per tile the listed x rows and the 128 dy
  * rows in LDS once per 32 x 32 channel slice (exact bf16 pieces); the rulebook's chunks are the MFMA k-steps.
- * Needs every tile's list (msp_tile_local's largest count) <= msp_wgrad_chunk_cap(), K <= 27, channels in
- * multiples of 32 (msp_wgrad_chunk_ok; msp_wgrad_chunk_preferred: the shapes the library takes it for).
+ * Needs every tile's list (msp_tile_local's largest count, u_start[n_tiles + 1]) <= msp_wgrad_chunk_cap(): a rule
+ * whose input row lies past the cap is marked 0xFFFF and contributes nothing, so the caller checks the largest
+ * count first and otherwise takes the pair-list form (msp_conv_wgrad); n_far (device int64, nullable) receives
+ * the number of such rules (0 when the cap holds).  K <= 27, channels in multiples of 32 (msp_wgrad_chunk_ok;
+ * msp_wgrad_chunk_preferred: the shapes the library takes it for).
  * Blocks run n_ranges contiguous tile ranges (msp_wgrad_chunk_ranges) per slice; slab holds n_ranges x K x
  * c_in x c_out floats of partial sums, added in range order into dw. */
 int64_t msp_wgrad_chunk_cap(void);
@@ -221,15 +201,11 @@ int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out);
 int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out);
 int msp_wgrad_chunk_index(const int64_t* tile_start, const int32_t* chunk_src, const uint16_t* chunk_row,
                           int64_t n_rows, const int64_t* u_start, const int32_t* u_rows, uint32_t* chunk_lr,
-                          msp_stream_t stream);
+                          int64_t* n_far, msp_stream_t stream);
 int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
                          const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
                          const int64_t* u_start, const int32_t* u_rows, int64_t n_rows, int64_t n_ranges,
                          float* slab, float* dw, msp_stream_t stream);
-int msp_conv_chunk_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
-                         const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
-                         const uint32_t* chunk_lr, const int32_t* u_rows, const int32_t* u_cnt, int64_t n_rows,
-                         float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows);
 int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
@@ -278,26 +254,6 @@ int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out);
 int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
                    const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
                    float* dw, msp_stream_t stream);
-
-/* Banded weight gradient for submanifold rules (pairs of each offset in
- * ascending pair_out, as msp_pair_lists makes them): a block owns a 32 x 32
- * dW tile and a group of 256-row bands of output rows, stages each band's dy
- * rows and the x rows around it in LDS once and runs every offset's pairs of
- * the band from there (instead of one global load per pair).  seg[K][n_sub+1]
- * (msp_wgrad_band_segments, once per pair lists) = first pair of offset o
- * with output row >= 256 s.  slab: msp_wgrad_band_groups(...) x K x c_in x
- * c_out floats; the groups are reduced in order (deterministic).
- * Requires K <= 32 and c_in, c_out multiples of 32.  msp_wgrad_band_ok says
- * whether the library prefers it for a shape: not yet (measured slower than
- * msp_conv_wgrad), so it answers 0. */
-int msp_wgrad_band_ok(int64_t n_rows, int K, int c_in, int c_out);
-int64_t msp_wgrad_band_groups(int64_t n_rows, int c_in, int c_out);
-int64_t msp_wgrad_band_seg_len(int64_t n_rows, int K);
-int msp_wgrad_band_segments(const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_rows, int64_t* seg,
-                            msp_stream_t stream);
-int msp_conv_wgrad_band(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
-                        const int32_t* pair_out, const int64_t* seg, int K, int64_t n_rows, float* slab, float* dw,
-                        msp_stream_t stream);
 
 /* ---------------- batch norm + (leaky) ReLU (replaces SCN BatchNormalization
  * with leakiness; scn.BatchNormReLU / BatchNormLeakyReLU).

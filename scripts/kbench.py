@@ -1,0 +1,152 @@
+"""Kernel micro-benchmark on the headline batch's real rulebooks (BASELINE configs[2]: 8 synthetic scenes at
+scale 50 = 2 cm, the m = 32 UNet's levels): every submanifold convolution form the library has, for the channel
+pairs the network runs at each level (a -> a, 2a -> a forward; a -> 2a backward-data), and the weight-gradient
+forms.  Prints time (median of N launches, HIP events), algorithmic TF/s (2 rules c_in c_out per rule) and the
+max error of each against an fp64 evaluation on a row subset (relative to the subset's max |out|).
+
+Usage: python scripts/kbench.py   env: LEVELS=0,1,2 (default 0-4)  PASSES=fwd,bwd,wgrad  FORMS=local,tile,nbr,...
+       N=10 (timed launches)  SCENES=8"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..'))
+import __graft_entry__ as g_  # noqa: E402
+g_.add_path()
+import torch  # noqa: E402
+import sparseconvnet as scn  # noqa: E402
+from sparseconvnet import _lib, ops  # noqa: E402
+from sparseconvnet._lib import ptr  # noqa: E402
+from wsss3d.synthetic import make_batch  # noqa: E402
+
+LEVELS = [int(v) for v in os.environ.get("LEVELS", "0,1,2,3,4").split(",")]
+PASSES = os.environ.get("PASSES", "fwd,bwd,wgrad").split(",")
+FORMS = os.environ.get("FORMS", "")
+N = int(os.environ.get("N", "10"))
+M = int(os.environ.get("M", "32"))
+NSUB = 4096
+DEV = "cuda"
+
+
+def timeit(f, n=N):
+    for _ in range(2):
+        f()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in ev:
+        a.record()
+        f()
+        b.record()
+    torch.cuda.synchronize()
+    t = sorted(a.elapsed_time(b) for a, b in ev)
+    return t[len(t) // 2]
+
+
+def conv_forms(rules, V, cin, cout):
+    """name -> f(x, wt, flip) for every form that applies (wt: [K][c_out][c_in], or [K][c_in][c_out] with flip 2)."""
+    forms = {}
+
+    def tile(x, wt, flip):
+        tl = rules.tiles_for(128)
+        out = torch.empty(V, cout, device=DEV)
+        wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(V), 27, cin, cout, 128))
+        ws = torch.empty(max(wsb // 4, 1), device=DEV)
+        _lib.call("msp_conv_tile", ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]),
+                  ptr(tl["chunk_off"]), ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), ptr(ws), wsb,
+                  _lib.stream())
+        return out
+    forms["tile"] = tile
+    forms["local"] = lambda x, wt, flip: ops.conv_local(x, wt, 27, flip, cout, rules, V)
+
+    def nbr(x, wt, flip):
+        perm, nbr_p = rules.dense_order()
+        return ops.conv_nbr(x, wt, 27, flip, cout, nbr_p, V, perm=perm)
+    forms["nbr"] = nbr
+    if hasattr(ops, "conv_unit") and cout <= 64:
+        forms["unit"] = lambda x, wt, flip: ops.conv_unit(x, wt, 27, flip, cout, rules, V)
+    if FORMS:
+        forms = {k: v for k, v in forms.items() if k in FORMS.split(",")}
+    return forms
+
+
+def main():
+    b = make_batch(int(os.environ.get("SCENES", "8")), 50, seed=1)
+    t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).to(DEV), torch.from_numpy(b["feats"]).to(DEV)])
+    meta = t.metadata
+    sizes = [4096 >> i for i in range(max(LEVELS) + 1)]
+    for s_ in sizes[:-1]:
+        meta.downsample(s_, 2)
+    for L in LEVELS:
+        lvl = meta.level(sizes[L])
+        rules = lvl.subm_rules(3)
+        V = lvl.n
+        loc = rules.local()
+        us = loc["u_start"][:loc["n_tiles"] + 1]
+        cnt = (us[1:] - us[:-1]).float()
+        tl = rules.tiles_for(128)
+        fill = rules.n_rules / max(tl["n_chunks"] * 16, 1)
+        print(f"L{L} V={V} R={rules.n_rules} ({rules.n_rules / V:.1f}/row) tiles={loc['n_tiles']} distinct rows "
+              f"per tile {cnt.mean().item() / 128:.2f}x128 (max {loc['max_u']}) chunk fill {fill:.2f}", flush=True)
+        a = M * (L + 1)
+        rows = torch.arange(min(NSUB, V), device=DEV)
+        nb = rules.nbr[:, :len(rows)].long()
+        shapes = []
+        if "fwd" in PASSES:
+            shapes += [("fwd", a, a), ("fwd", 2 * a, a)]
+        if "bwd" in PASSES:
+            shapes += [("bwd", a, a), ("bwd", a, 2 * a)]
+        for pas, cin, cout in shapes:
+            torch.manual_seed(L * 7 + cin + cout)
+            x = torch.randn(V, cin, device=DEV)
+            w = torch.randn(27, cin if pas == "fwd" else cout, cout if pas == "fwd" else cin, device=DEV)
+            w *= 1.0 / (27 * cin) ** 0.5  # the module's layout [K][c_in][c_out] of the conv this pass belongs to
+            flops = 2.0 * rules.n_rules * cin * cout
+            x64 = torch.cat([x.double(), torch.zeros(1, cin, device=DEV, dtype=torch.float64)])
+            g64 = x64[torch.where(nb >= 0, nb, V)]
+            if pas == "fwd":  # forward: the module's weights as they are (flip bit 1)
+                wt, flip = w, 2
+                ref = torch.einsum("onc,ocd->nd", g64, w.double())
+            else:  # backward-data: the same [K][c_out][c_in] tensor read as W^T with offsets mirrored (flip bit 0)
+                wt, flip = w, 1
+                ref = torch.einsum("onc,odc->nd", g64, w.double().flip(0))
+            scale = ref.abs().max().item()
+            res = []
+            for name, f in conv_forms(rules, V, cin, cout).items():
+                try:
+                    ms = timeit(lambda: f(x, wt, flip))
+                    out = f(x, wt, flip)
+                    err = (out[:len(rows)].double() - ref).abs().max().item() / scale
+                    res.append(f"{name} {ms:6.3f}ms {flops / ms / 1e9:6.1f}TF {err:.0e}")
+                except Exception as e:  # a form that does not take this shape
+                    res.append(f"{name} n/a ({str(e)[:40]})")
+            print(f"  {pas} {cin:3d}->{cout:3d}  " + "  ".join(res), flush=True)
+        if "wgrad" in PASSES:
+            for cin, cout in ((a, a), (2 * a, a), (a, 2 * a)):
+                torch.manual_seed(L + cin * 3 + cout)
+                x = torch.randn(V, cin, device=DEV)
+                dy = torch.randn(V, cout, device=DEV)
+                flops = 2.0 * rules.n_rules * cin * cout
+                ref = torch.empty(27, cin, cout, dtype=torch.float64, device=DEV)
+                nbl = rules.nbr.long()
+                for o in range(27):
+                    m = nbl[o] >= 0
+                    ref[o] = x.double()[nbl[o][m]].t() @ dy.double()[m]
+                scale = ref.abs().max().item()
+                p = rules.pairs
+                fs = {"pairs": lambda: ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)}
+                if int(_lib.query("msp_wgrad_chunk_ok", _lib.I64(V), 27, cin, cout)) and rules.wgrad_index() is not None:
+                    fs["chunk"] = lambda: ops.conv_wgrad_chunk(x, dy, rules, 27)
+                if hasattr(ops, "conv_wgrad_unit"):
+                    fs["unit"] = lambda: ops.conv_wgrad_unit(x, dy, rules, 27)
+                res = []
+                for name, f in fs.items():
+                    try:
+                        ms = timeit(f)
+                        err = (f().double() - ref).abs().max().item() / scale
+                        res.append(f"{name} {ms:6.3f}ms {flops / ms / 1e9:6.1f}TF {err:.0e}")
+                    except Exception as e:
+                        res.append(f"{name} n/a ({str(e)[:40]})")
+                print(f"  wgrad {cin:3d}x{cout:3d}  " + "  ".join(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

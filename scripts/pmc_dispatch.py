@@ -23,7 +23,18 @@ for key in order:
     out = [f"{key[0]} grid={key[1]} dur={c['_dur_ns'] / 1e3:.0f}us"]
     g = c.get("GRBM_GUI_ACTIVE")
     if g and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
-        out.append(f"mfma_util={c['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * 1024):.2f}")
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back): the kernel's cycles
+        # are g / 8; SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed over the 1024 SIMDs (16 per 16x16x32 bf16 MFMA)
+        out.append(f"mfma_busy={c['SQ_VALU_MFMA_BUSY_CYCLES'] / (g / 8 * 1024):.2f}")
+        out.append(f"clk={g / 8 / c['_dur_ns']:.2f}GHz")
+    if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c:
+        out.append(f"lds_conflict={c['SQ_LDS_BANK_CONFLICT'] / max(c['SQ_LDS_IDX_ACTIVE'], 1):.2f}")
+    if "SQ_LDS_IDX_ACTIVE" in c and g:
+        out.append(f"lds_busy={c['SQ_LDS_IDX_ACTIVE'] / (g / 8 * 256):.2f}")
+    if "SQ_WAIT_INST_LDS" in c and "SQ_WAVE_CYCLES" in c:
+        out.append(f"wait_lds={c['SQ_WAIT_INST_LDS'] / c['SQ_WAVE_CYCLES']:.2f}")
+    if "SQ_WAVES" in c and "SQ_INSTS_LDS" in c:
+        out.append(f"lds/wave={c['SQ_INSTS_LDS'] / c['SQ_WAVES']:.0f}")
     if "SQ_WAVE_CYCLES" in c:
         w = c["SQ_WAVE_CYCLES"]
         out.append(f"wait_any={c['SQ_WAIT_ANY'] / w:.2f} wait_inst={c['SQ_WAIT_INST_ANY'] / w:.2f} "

@@ -107,9 +107,12 @@ def test_ddp_world2_hip_model():
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
 
 
-def _graph_worker(rank, world, port, out):
+def _graph_worker(rank, world, port, out, cfg=None):
     """bench.py's N-rank graph path: forward + backward captured into a HIP graph on the prefetched metadata,
-    gradients as views of one flat buffer (dp.GradSync), one all-reduce + Adam eagerly after the replay."""
+    gradients as views of one flat buffer (dp.GradSync), one all-reduce + Adam eagerly after the replay.
+    cfg: m, reps, scale, scenes (per rank) and oracle (rank 0 also checks the per-point features of one of
+    its scenes against the fp64 oracle under shared ReLU decisions, at the 1e-4 bar)."""
+    cfg = dict(dict(m=16, reps=2, scale=20, scenes=2, oracle=False), **(cfg or {}))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "3d-weakly-supervised-semantic-segmentation_amd"), root):
@@ -125,7 +128,7 @@ def _graph_worker(rank, world, port, out):
 
     try:
         r, w, _, dev = dp.init_from_env("cuda", backend="gloo", device_index=0)
-        pc = EasyDict(name="SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=2,
+        pc = EasyDict(name="SparseConvUNet", m=cfg["m"], dimension=3, full_scale=4096, block_reps=cfg["reps"],
                       residual_blocks=True)
         cls, _ = MODEL_REGISTRY.get("MultiLabel")
         torch.manual_seed(0)
@@ -134,7 +137,7 @@ def _graph_worker(rank, world, port, out):
         model = cls(pc).to(dev)
         gsync = dp.GradSync(model, dev)
         ok = all(torch.equal(p, q) for p, q in zip(model.parameters(), local.parameters()))
-        bs = [make_batch(2, 20, seed=10 * r + k) for k in range(2)]
+        bs = [make_batch(cfg["scenes"], cfg["scale"], seed=10 * r + k) for k in range(2)]
         xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(dev), feature=torch.from_numpy(b["feats"]).to(dev),
                        batch_offsets=b["batch_offsets"]) for b in bs]
         ys = [torch.from_numpy(b["scene_labels"]).to(dev) for b in bs]
@@ -177,6 +180,26 @@ def _graph_worker(rank, world, port, out):
         ok &= torch.equal(flat, ref)
         torch.cuda.synchronize()
         del g
+        if cfg["oracle"] and r == 0:  # one whole scene of this rank's batch against the fp64 oracle
+            from oracle.encoders import OracleEncoder
+            from oracle.parity import run_shared_masks
+            b0 = bs[1]
+            n0 = int(b0["batch_offsets"][1])
+            c0 = torch.from_numpy(b0["coords"][:n0])
+            f0 = torch.from_numpy(b0["feats"][:n0])
+            enc = model.pc_encoder
+            oref = OracleEncoder("SparseConvUNet", m=cfg["m"], block_reps=cfg["reps"], residual_blocks=True).double()
+            oref.load_state_dict({k: v.double().cpu() for k, v in enc.state_dict().items()})
+            with torch.no_grad():
+                og, oo, st = run_shared_masks(enc, oref, EasyDict(coords=c0.to(dev), feature=f0.to(dev),
+                                                                  batch_offsets=[0, n0]),
+                                              dict(coords=c0, feature=f0.double(), batch_offsets=[0, n0]),
+                                              istrain=False)
+            err = (og.double().cpu() - oo).abs().max().item()
+            lim = 1e-4 * max(1.0, oo.abs().max().item())
+            print(f"rank 0: scene 0 ({n0} points) per-point features max err {err:.3e} (bar {lim:.3e}), "
+                  f"flip margin {st['max_flip_margin']:.2e}", flush=True)
+            ok &= err <= lim and st["max_flip_margin"] < 1e-4
         out[rank] = bool(ok)
         dist.destroy_process_group()
     except Exception as e:  # report instead of hanging the parent
@@ -184,21 +207,34 @@ def _graph_worker(rank, world, port, out):
         raise
 
 
-def test_graph_dp_world2_hip_model():
+def _run_graph_world2(cfg=None, timeout=300):
     ctx = mp.get_context("spawn")
     manager = ctx.Manager()
     out = manager.dict()
     port = _free_port()
-    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, out)) for r in range(2)]
+    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, out, cfg)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(timeout=300)
+        p.join(timeout=timeout)
     for p in procs:
         if p.is_alive():
             p.kill()
     assert dict(out) == {0: True, 1: True}, dict(out)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_graph_dp_world2_hip_model():
+    _run_graph_world2()
+
+
+@pytest.mark.timeout(900)
+def test_c4_per_rank_workload_graph_dp():
+    """BASELINE configs[3] per-rank workload (SparseConvUNet m=32, block_reps=2, residual, scale 50 = 2 cm,
+    5 whole scenes per rank) through bench.py's N-rank graph path on two ranks sharing cuda:0 over gloo:
+    averaged gradients = the mean of the ranks' local gradients, parameters equal after Adam, and rank 0's
+    per-point features of one of its scenes within 1e-4 of the fp64 oracle."""
+    _run_graph_world2(dict(m=32, reps=2, scale=50, scenes=5, oracle=True), timeout=600)
 
 
 def test_bench_graph_path_over_rccl():

@@ -285,18 +285,29 @@ def test_residual_block_grads(n, cin):
         close(pg[k].grad, p.grad, 1e-4, "grad " + k)
 
 
+def _subm_ref(x, wt, nbr, flip, dtype):
+    """sum over offsets of x[nbr(., o)] W'[o]^T evaluated by torch in `dtype` (fp64: the reference; fp32: a plain
+    fp32 evaluation whose error the split-bf16 kernels are held to); wt [K][c_out][c_in], flip mirrors offsets."""
+    V, K = nbr.size(1), nbr.size(0)
+    xd = torch.cat([x.to(dtype), torch.zeros(1, x.size(1), dtype=dtype, device=x.device)])
+    wd = wt.to(dtype).flip(0) if flip else wt.to(dtype)
+    nb = nbr.long()
+    ref = torch.zeros(V, wt.size(1), dtype=dtype, device=x.device)
+    for o in range(K):
+        ref += xd[torch.where(nb[o] >= 0, nb[o], x.size(0))] @ wd[o].t()
+    return ref
+
+
 @pytest.mark.parametrize("cin,cout,flip", [(64, 64, 0), (96, 96, 1), (48, 96, 0), (256, 128, 0), (224, 32, 1),
                                            (32, 32, 0), (64, 32, 1), (48, 16, 0)])
 def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
     """msp_conv_tile on 128-row tiles runs the contraction as six bf16 MFMA
     products of exact three-piece splits (msp_conv_x6.hip).  Its error against
-    an fp64 evaluation must be fp32-class: at most 2x that of the f32-input
-    MFMA kernel (one fmaf chain, exact fp32) on the same rulebook, and below
+    an fp64 evaluation must be fp32-class: at most 2x that of a plain fp32
+    evaluation (torch gather + fp32 GEMM) of the same sum, and below
     1e-6 of the output scale.  c_out <= 32 with c_in <= 64 takes the per-wave
     form (conv_x6r_kernel: weights per offset run), the rest the shared-tile form."""
-    import ctypes
-    from sparseconvnet import _lib, ops
-    from sparseconvnet._lib import ptr
+    from sparseconvnet import ops
     torch.manual_seed(cin + cout)
     coords, feats = _inputs(20000, 40, n_batch=2)
     t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
@@ -306,25 +317,8 @@ def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
     x = torch.randn(V, cin, device=DEV)
     wt = torch.randn(27, cout, cin, device=DEV) / (27 * cin) ** 0.5
     y = ops.conv_tile(x, wt, 27, flip, cout, rules, V)
-    # f32-MFMA shared-tile kernel on the same rulebook (debug hook; split 1)
-    lib = _lib.load()
-    fn = lib.msp_debug_conv_tile
-    P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
-    fn.restype = I
-    fn.argtypes = [I, I, P, I, P, I, I, I, I, P, P, P, P, I64, P, P, P]
-    tl = rules.tiles_for(128)
-    nt = 2 if (cout // 16) % 2 == 0 else 1
-    y32 = torch.empty(V, cout, device=DEV)
-    rc = fn(81, nt, ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
-            ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(y32), None, _lib.stream(x.device))
-    assert rc == 0, lib.msp_last_error()
-    # fp64 reference from the neighbour map
-    nb = rules.nbr.long()
-    x64 = torch.cat([x.double(), torch.zeros(1, cin, dtype=torch.float64, device=DEV)])
-    w64 = wt.double().flip(0) if flip else wt.double()
-    ref = torch.zeros(V, cout, dtype=torch.float64, device=DEV)
-    for o in range(27):
-        ref += x64[torch.where(nb[o] >= 0, nb[o], V)] @ w64[o].t()
+    ref = _subm_ref(x, wt, rules.nbr, flip, torch.float64)
+    y32 = _subm_ref(x, wt, rules.nbr, flip, torch.float32)
     scale = ref.abs().max().item()
     e_x6 = (y.double() - ref).abs().max().item() / scale
     e_f32 = (y32.double() - ref).abs().max().item() / scale
@@ -336,12 +330,11 @@ def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
 def test_conv_nbr_accuracy(cin, cout, flip):
     """msp_conv_nbr (dense row groups over the neighbour map, register
     accumulators) against an fp64 evaluation of the same convolution: the
-    error bar of the split-bf16 tile form (at most 2x the f32-input MFMA
-    kernel's error on the same rulebook, and below 1e-6 of the output
-    scale), and agreement with msp_conv_tile; the mask-sorted row order
+    error bar of the split-bf16 tile form (at most 2x a plain fp32
+    evaluation's error, and below 1e-6 of the output scale), and agreement
+    with msp_conv_tile; the mask-sorted row order
     (msp_dense_order) gives bitwise the same rows.  Includes c_in not a
     multiple of 32 (zero k-padding) and a last group of rows past the level."""
-    import ctypes
     from sparseconvnet import _lib, ops
     from sparseconvnet._lib import ptr
     torch.manual_seed(cin * 7 + cout)
@@ -365,22 +358,8 @@ def test_conv_nbr_accuracy(cin, cout, flip):
     _lib.call("msp_conv_tile", ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]),
               ptr(tl["chunk_off"]), ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(yt), ptr(ws), wsb,
               _lib.stream(x.device))
-    lib = _lib.load()
-    fn = lib.msp_debug_conv_tile
-    P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
-    fn.restype = I
-    fn.argtypes = [I, I, P, I, P, I, I, I, I, P, P, P, P, I64, P, P, P]
-    nt = 2 if (cout // 16) % 2 == 0 else 1
-    y32 = torch.empty(V, cout, device=DEV)
-    rc = fn(81, nt, ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
-            ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(y32), None, _lib.stream(x.device))
-    assert rc == 0, lib.msp_last_error()
-    nb = rules.nbr.long()
-    x64 = torch.cat([x.double(), torch.zeros(1, cin, dtype=torch.float64, device=DEV)])
-    w64 = wt.double().flip(0) if flip else wt.double()
-    ref = torch.zeros(V, cout, dtype=torch.float64, device=DEV)
-    for o in range(27):
-        ref += x64[torch.where(nb[o] >= 0, nb[o], V)] @ w64[o].t()
+    ref = _subm_ref(x, wt, rules.nbr, flip, torch.float64)
+    y32 = _subm_ref(x, wt, rules.nbr, flip, torch.float32)
     scale = ref.abs().max().item()
     e_g = (y.double() - ref).abs().max().item() / scale
     e_f32 = (y32.double() - ref).abs().max().item() / scale
@@ -436,7 +415,7 @@ def test_weight_layout_flag(cin, cout, nbr_form):
     """flip bit 1 (weights in the module's [K][c_in][c_out] layout, no
     transposed copy) gives bitwise the same output as the [K][c_out][c_in]
     layout, with and without the flip bit, on every 128-row-tile form and on
-    msp_conv_nbr; 64-row tiles reject it."""
+    msp_conv_nbr; msp_conv_tile rejects any tile height but 128."""
     from sparseconvnet import _lib, ops
     from sparseconvnet._lib import ptr
     torch.manual_seed(cin + 3 * cout)
@@ -460,46 +439,7 @@ def test_weight_layout_flag(cin, cout, nbr_form):
     rc = _lib.load().msp_conv_tile(ptr(x), cin, ptr(w), 27, 2, cout, 64, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
                                    ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), None, 0,
                                    _lib.stream(x.device))
-    assert rc != 0 and b"128-row" in _lib.load().msp_last_error()
-
-
-@pytest.mark.parametrize("cin,cout,size", [(32, 32, 4096), (64, 32, 4096), (32, 64, 64), (96, 96, 64),
-                                           (64, 128, 64), (160, 96, 64)])
-def test_conv_wgrad_band(cin, cout, size):
-    """msp_conv_wgrad_band (rows staged in LDS per 256-row band) against fp64
-    per-offset x^T dy sums and against the pair-list form: fp32-class error
-    (< 2e-6 of each offset's max), on a multi-band level with a partial last
-    band and pairs whose input row lies outside the staged halo."""
-    from sparseconvnet import ops, _lib
-    _lib.load().msp_debug_wgrad_band(1)
-    torch.manual_seed(cin + cout + size)
-    if size == 4096:
-        b = make_batch(1, 50, seed=9)
-        coords, feats = torch.from_numpy(b["coords"]), torch.from_numpy(b["feats"])
-    else:
-        coords, feats = _inputs(20000, 40, n_batch=2)
-    t = scn.InputLayer(3, size, mode=4)([coords.to(DEV), feats.to(DEV)])
-    lvl = t.metadata.level(size)
-    V = lvl.n
-    p = lvl.subm_rules(3).pairs
-    x = torch.randn(V, cin, device=DEV)
-    dy = torch.randn(V, cout, device=DEV)
-    dw = ops.conv_wgrad_band(x, dy, p, 27, V)
-    dw2 = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
-    offs = p.off_start.cpu().tolist()
-    pin, pout = p.pair_in.long(), p.pair_out.long()
-    far = 0
-    for o in range(27):
-        s0, s1 = offs[o], offs[o + 1]
-        ref = x[pin[s0:s1]].double().T @ dy[pout[s0:s1]].double()
-        scale = ref.abs().max().clamp_min(1e-30)
-        assert ((dw[o].double() - ref).abs().max() / scale).item() < 2e-6, o
-        assert ((dw2[o].double() - ref).abs().max() / scale).item() < 2e-6, o
-        band0 = (pout[s0:s1] // 256) * 256
-        far += int(((pin[s0:s1] < band0 - 64) | (pin[s0:s1] >= band0 + 256 + 64)).sum())
-    if size == 4096:
-        assert V > 256 * 8 and V % 256 != 0 and far > 0, (V, far)
-    _lib.load().msp_debug_wgrad_band(0)
+    assert rc != 0 and b"must be 128" in _lib.load().msp_last_error()
 
 
 @pytest.mark.parametrize("V,C", [(5000, 32), (3001, 64), (777, 36), (1200, 6), (0, 32)])
@@ -608,6 +548,21 @@ def _local_ref(x, wt, nbr, flip):
     return ref
 
 
+def _gather_form(x, wt, flip, cout, rules, V):
+    """msp_conv_tile on the 128-row tile rulebook (the gather forms), called directly."""
+    from sparseconvnet import _lib
+    from sparseconvnet._lib import ptr
+    cin = x.size(1)
+    tl = rules.tiles_for(128)
+    out = torch.empty(V, cout, device=DEV)
+    wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(V), 27, cin, cout, 128))
+    ws = torch.empty(max(wsb // 4, 1), device=DEV)
+    _lib.call("msp_conv_tile", ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(tl["tile_start"]),
+              ptr(tl["chunk_off"]), ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), ptr(ws), wsb,
+              _lib.stream(x.device))
+    return out
+
+
 def _check_local_rulebook(nbr, loc, n):
     K = nbr.size(0)
     T, nt = loc["tile_rows"], loc["n_tiles"]
@@ -633,23 +588,15 @@ def _check_local_rulebook(nbr, loc, n):
         assert torch.equal(u[li[~absent]], ent[~absent])
 
 
-@pytest.mark.parametrize("order", [1, 0])
-def test_tile_local_rulebook(order):
+def test_tile_local_rulebook():
     """msp_tile_local: per 128-row tile the sorted distinct input rows, the rows' order inside the tile
-    (by neighbour mask, or key order) and the local index of every neighbour, checked entry by entry."""
-    import ctypes
+    (by neighbour mask) and the local index of every neighbour, checked entry by entry."""
     from sparseconvnet import _lib, metadata
-    lib = _lib.load()
-    lib.msp_debug_conv_local.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     coords, feats = _inputs(20000, 40, n_batch=2)
     t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
     lvl = t.metadata.level(64)
     rules = lvl.subm_rules(3)
-    try:
-        lib.msp_debug_conv_local(-1, order, -1)
-        loc = metadata.local_rulebook(rules.nbr, 27, lvl.n, rules.nbr.device, _lib.stream(), 128)
-    finally:
-        lib.msp_debug_conv_local(-1, 1, -1)
+    loc = metadata.local_rulebook(rules.nbr, 27, lvl.n, rules.nbr.device, _lib.stream(), 128)
     assert lvl.n % 128 != 0
     _check_local_rulebook(rules.nbr, loc, lvl.n)
 
@@ -677,18 +624,14 @@ def test_tile_local_rulebook_maps(T, K, mode):
         assert loc["max_u"] == K * T
 
 
-@pytest.mark.parametrize("form", [-1, -2], ids=["x6s", "x6l"])
 @pytest.mark.parametrize("cin,cout,flip", [(64, 64, 2), (64, 64, 1), (96, 96, 2), (192, 96, 1), (48, 64, 2),
                                            (64, 48, 1), (128, 16, 2), (32, 160, 1)])
-def test_conv_local_accuracy(cin, cout, flip, form):
+def test_conv_local_accuracy(cin, cout, flip):
     """msp_conv_local (tile-local staging, split-bf16 MFMA) against an fp64 evaluation: below 1e-6 of the
     output scale (the x6 forms' bar), and against the production gather form.  flip 2 = forward with the
     module's [K][c_in][c_out] weights, 1 = backward-data ([K][c_out][c_in], offsets mirrored); c_in 48 has a
     half-empty 32-channel slice, c_out 48 / 16 / 160 run one 16-column tile per wave."""
-    import ctypes
-    from sparseconvnet import _lib, ops
-    lib = _lib.load()
-    lib.msp_debug_conv_local_abl.argtypes = [ctypes.c_int]
+    from sparseconvnet import ops
     torch.manual_seed(cin * 7 + cout + flip)
     coords, feats = _inputs(20000, 40, n_batch=2)
     t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
@@ -698,20 +641,12 @@ def test_conv_local_accuracy(cin, cout, flip, form):
     x = torch.randn(V, cin, device=DEV)
     w = torch.randn(27, cin, cout, device=DEV) / (27 * cin) ** 0.5
     wt = w if flip == 2 else w.transpose(1, 2).contiguous()
-    lib.msp_debug_conv_local_abl(form)  # -1: tile-per-block form (x6s), -2: persistent form (x6l) where it applies
-    try:
-        y = ops.conv_local(x, wt, 27, flip, cout, rules, V)
-    finally:
-        lib.msp_debug_conv_local_abl(-3)
+    y = ops.conv_local(x, wt, 27, flip, cout, rules, V)
     ref = _local_ref(x, w.transpose(1, 2), rules.nbr, flip & 1)  # [K][c_out][c_in], offsets mirrored for flip 1
     scale = ref.abs().max().item()
     err = (y.double() - ref).abs().max().item() / scale
     assert err < 1e-6, err
-    ops.CONV_LOCAL = False
-    try:
-        yg = ops.conv_tile(x, wt, 27, flip, cout, rules, V)
-    finally:
-        ops.CONV_LOCAL = True
+    yg = _gather_form(x, wt, flip, cout, rules, V)
     assert (y - yg).abs().max().item() / scale < 2e-6
 
 
@@ -740,42 +675,6 @@ def test_conv_local_overflow_rows():
     assert (y.double() - ref).abs().max().item() / ref.abs().max().item() < 1e-6
 
 
-@pytest.mark.parametrize("cin,cout,flip", [(32, 32, 2), (64, 32, 2), (32, 64, 1), (48, 32, 1)])
-def test_conv_chunk_local_accuracy(cin, cout, flip):
-    """msp_conv_chunk_local (64-row tile rulebook, each 128-row unit's distinct rows staged in LDS, LDS
-    accumulators) against fp64 (< 1e-6 of the output scale) and the gather form; c_in 48 has a half-empty
-    32-channel slice, flip 1 = backward-data layout."""
-    import ctypes
-    from sparseconvnet import _lib, ops
-    lib = _lib.load()
-    lib.msp_debug_conv_chunk.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    torch.manual_seed(cin * 5 + cout + flip)
-    coords, feats = _inputs(20000, 40, n_batch=2)
-    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
-    rules = t.metadata.level(64).subm_rules(3)
-    V = t.metadata.level(64).n
-    x = torch.randn(V, cin, device=DEV)
-    w = torch.randn(27, cin, cout, device=DEV) / (27 * cin) ** 0.5
-    wt = w if flip == 2 else w.transpose(1, 2).contiguous()
-    y = ops.conv_chunk_local(x, wt, 27, flip, cout, rules, V)
-    ref = _local_ref(x, w.transpose(1, 2), rules.nbr, flip & 1)
-    scale = ref.abs().max().item()
-    assert (y.double() - ref).abs().max().item() / scale < 1e-6
-    lib.msp_debug_conv_chunk(2, 0, 0)
-    try:
-        yg = ops.conv_tile(x, wt, 27, flip, cout, rules, V)
-    finally:
-        lib.msp_debug_conv_chunk(2, -1, 0)
-    assert (y - yg).abs().max().item() / scale < 2e-6
-    loc = rules.chunk_local()  # the unit lists: sorted, distinct, -1 past the count
-    n_u, cap = loc["n_units"], loc["cap"]
-    rows = loc["u_rows"][:n_u * cap].view(n_u, cap).cpu()
-    cnt = loc["u_cnt"][:n_u].cpu()
-    for u in range(0, n_u, max(1, n_u // 16)):
-        k = min(int(cnt[u]), cap)
-        assert bool((rows[u, 1:k] > rows[u, :k - 1]).all()) and bool((rows[u, k:] == -1).all())
-
-
 @pytest.mark.parametrize("cin,cout", [(32, 32), (64, 32), (32, 64), (96, 64)])
 def test_conv_wgrad_chunk_accuracy(cin, cout):
     """msp_conv_wgrad_chunk (chunk-compacted tile-local weight gradient, transposing LDS reads, split-bf16
@@ -802,50 +701,48 @@ def test_conv_wgrad_chunk_accuracy(cin, cout):
     assert (dw - dwp).abs().max().item() / scale < 2e-6
 
 
-def test_conv_chunk_local_overflow_rows():
-    """Units naming more distinct input rows than the LDS stage holds (320): a random map over a large input
-    sends most rows down the global-memory path; results still match fp64."""
+def test_conv_wgrad_chunk_over_cap_falls_back():
+    """A map whose 128-row tiles name more distinct input rows than the chunk weight gradient stages
+    (msp_wgrad_chunk_cap, 448): SubmRules.wgrad_index refuses it (None), the module's backward takes the
+    pair-list weight gradient, and that gradient matches fp64; msp_wgrad_chunk_index reports the rules it would
+    drop through its n_far count (no silent loss at the C ABI)."""
     from sparseconvnet import _lib, metadata, ops
-
-    class R:  # a SubmRules stand-in over an arbitrary map
-        pass
-    torch.manual_seed(7)
-    V, n_in, K = 1000, 50000, 27
-    nbr = torch.randint(0, n_in, (K, V), dtype=torch.int32, device=DEV)
-    nbr[torch.rand(K, V, device=DEV) < 0.5] = -1
-    r = R()
-    r.nbr, r.K = nbr, K
-    tiles = metadata.tile_rulebook(nbr, K, V, nbr.device, _lib.stream(), 64)
-    loc = metadata.chunk_local_index(tiles, V, nbr.device, _lib.stream())
-    assert int(loc["u_cnt"][:loc["n_units"]].max()) > 1000
-    r.chunk_local = lambda: loc
-    x = torch.randn(n_in, 64, device=DEV)
-    w = torch.randn(K, 64, 32, device=DEV) / (K * 64) ** 0.5
-    y = ops.conv_chunk_local(x, w, K, 2, 32, r, V)
-    ref = _local_ref(x, w.transpose(1, 2), nbr, 0)
-    assert (y.double() - ref).abs().max().item() / ref.abs().max().item() < 1e-6
-
-
-@pytest.mark.parametrize("cin,cout", [(32, 32), (64, 32), (96, 64), (64, 128)])
-def test_conv_wgrad_local_accuracy(cin, cout):
-    """msp_conv_wgrad_local (tile-local weight gradient, split-bf16 MFMA) against an fp64 evaluation of
-    dW[o] = sum_i x[nbr(i, o)]^T dy[i], and against the pair-list form."""
-    from sparseconvnet import ops
-    torch.manual_seed(cin + 3 * cout)
-    coords, feats = _inputs(20000, 40, n_batch=2)
-    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
-    rules = t.metadata.level(64).subm_rules(3)
-    V = t.metadata.level(64).n
-    x = torch.randn(V, cin, device=DEV)
-    dy = torch.randn(V, cout, device=DEV)
-    dw = ops.conv_wgrad_local(x, dy, rules, 27)
-    nb = rules.nbr.long()
-    ref = torch.empty(27, cin, cout, dtype=torch.float64, device=DEV)
-    for o in range(27):
+    from sparseconvnet._lib import ptr
+    torch.manual_seed(9)
+    V, K = 20000, 27  # >= 2^14 rows: the module's backward asks for the chunk form first
+    # the SubmRules machinery over this map (square: inputs are rows of the same level), through a stand-in
+    r = metadata.SubmRules.__new__(metadata.SubmRules)
+    r._plan, r._key, r.K, r.filter_size = [], ("subm", 0, 3), K, 3
+    r.nbr = torch.randint(0, V, (K, V), dtype=torch.int32, device=DEV)
+    r.nbr[torch.rand(K, V, device=DEV) < 0.2] = -1
+    r.nbr[13] = torch.arange(V, dtype=torch.int32, device=DEV)  # the centre offset
+    r._tiles, r._locals, r._wchunk, r._dense = {}, {}, None, None
+    r._map, r._n = r.nbr, V
+    r.pairs = metadata.PairLists(r.nbr, K, V, DEV, _lib.stream(), r._plan, r._key)
+    r.n_rules = r.pairs.total
+    loc = r.local()
+    assert loc["max_u"] > int(_lib.query("msp_wgrad_chunk_cap"))  # random rows: ~27 x 0.8 x 128 per tile
+    assert r.wgrad_index() is None
+    # the C ABI: the over-cap rules are counted, not silently dropped
+    tiles = r.tiles_for(128)
+    lr = torch.empty(tiles["n_chunks"] * 16, dtype=torch.int32, device=DEV)
+    n_far = torch.full((1,), -1, dtype=torch.int64, device=DEV)
+    _lib.call("msp_wgrad_chunk_index", ptr(tiles["tile_start"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]),
+              _lib.I64(V), ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(lr), ptr(n_far), _lib.stream())
+    u = loc["u_start"][:loc["n_tiles"] + 1].cpu()
+    cap = int(_lib.query("msp_wgrad_chunk_cap"))
+    assert int(n_far.item()) > 0 and bool(((u[1:] - u[:-1]) > cap).any())
+    # the fallback weight gradient through the autograd Function
+    assert int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, 32, 64))
+    x = torch.randn(V, 32, device=DEV, requires_grad=True)
+    w = (torch.randn(K, 1, 32, 64, device=DEV) / (K * 32) ** 0.5).requires_grad_(True)
+    y = ops.SubmanifoldConvFunction.apply(x, w, r)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    nb = r.nbr.long()
+    ref = torch.empty(K, 32, 64, dtype=torch.float64, device=DEV)
+    for o in range(K):
         m = nb[o] >= 0
-        ref[o] = x.double()[nb[o][m]].t() @ dy.double()[m]
-    scale = ref.abs().max().item()
-    assert (dw.double() - ref).abs().max().item() / scale < 1e-6
-    p = rules.pairs
-    dwp = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
-    assert (dw - dwp).abs().max().item() / scale < 3e-6
+        ref[o] = x.detach().double()[nb[o][m]].t() @ dy.double()[m]
+    dw = w.grad.reshape(K, 32, 64).double()
+    assert (dw - ref).abs().max().item() / ref.abs().max().item() < 1e-6
