@@ -138,6 +138,17 @@ def max_over_ranks(x: float) -> float:
     return float(t.item())
 
 
+def gather_floats(x: float) -> list:
+    """[x of rank 0, x of rank 1, ...] (a one-element list without a process group)."""
+    if not dist.is_initialized():
+        return [x]
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 def sum_over_ranks(x: float) -> float:
     if not dist.is_initialized():
         return x

@@ -235,6 +235,18 @@ def cpu_baseline(args, batch, iters=3):
                       f"({', '.join(f'{t:.2f}' for t in times)} s)"}
 
 
+def balanced_batch(args, rank, world, k):
+    """Batch k of this rank under LPT assignment: the same pool of world x batch procedural rooms on every rank
+    (seeded by k), sharded by point count with wsss3d.dp.balanced_shards, then this rank's rooms through the
+    trainMerge transform (dataset/data.py:135-238) as make_batch does."""
+    from wsss3d import dp
+    from wsss3d.synthetic import make_room, train_merge
+    pool = [make_room((100 + k) * 1000 + i) for i in range(world * args.batch)]
+    sizes = [len(room[0]) for room in pool]
+    shard = dp.balanced_shards(sizes, world)[rank]
+    return train_merge([pool[i] for i in shard], args.scale, 4096, 1000 * rank + k)
+
+
 def launch_ranks(n):
     """Start n ranks (torch.distributed.run child, one process per GPU) before this process touches the
     GPU; rank 0 prints the JSON line.  Returns the child's exit code."""
@@ -285,6 +297,11 @@ def main():
                          "prefetched, replayed on the compute stream while the next step is prefetched and "
                          "captured; N ranks: forward + backward captured, the gradient all-reduce and Adam eager after each "
                          "replay) -- removes the per-kernel launch gaps; default 1")
+    ap.add_argument("--balance", choices=["none", "lpt"], default="none",
+                    help="scene assignment over ranks: none = every rank draws its own scenes (weak scaling, the "
+                         "default); lpt = all ranks' scenes drawn from one pool and assigned by point count, "
+                         "longest first, to the lightest rank (wsss3d.dp.balanced_shards), so the slowest rank's "
+                         "step is as short as the pool allows")
     ap.add_argument("--workload", choices=["unet", "contrastive"], default=None,
                     help="unet: the headline config (BASELINE configs[2]); contrastive: configs[4] per GPU -- "
                          "MultiLabelContrastive = SparseConvFCNet m=32 r1 at scale 20 + TextTransformer "
@@ -327,7 +344,13 @@ def main():
     from sparseconvnet import ops as scn_ops
     scn_ops.WGRAD_CONCURRENT = bool(args.concurrent_wgrad)
     # two distinct batches per rank, alternated step to step
-    host_batches = [make_batch(args.batch, args.scale, seed=1000 * rank + k) for k in range(2)]
+    if args.balance == "lpt" and world > 1:
+        host_batches = [balanced_batch(args, rank, world, k) for k in range(2)]
+        scene_note = ("LPT over a pool of world x scenes_per_gpu scenes per batch (wsss3d.dp.balanced_shards by "
+                      "point count)")
+    else:
+        host_batches = [make_batch(args.batch, args.scale, seed=1000 * rank + k) for k in range(2)]
+        scene_note = "independent random scenes per rank (seed 1000 rank + k)"
     contrastive = args.workload == "contrastive"
     n_text, seq_len, vocab = 10, 120, 49408
     batches = []
@@ -465,7 +488,7 @@ def main():
         if gsync is not None:  # N ranks: the gradient exchange and Adam after the replayed backward
             gsync.average()
             opt.step()
-        done = torch.cuda.Event(enable_timing=host_t is not None)
+        done = torch.cuda.Event(enable_timing=True)
         done.record(cur)
         if host_t is not None:
             replay_ev[-1] = (replay_ev[-1][0], done)
@@ -483,12 +506,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     rec.active = True
+    # step boundaries on the compute stream: device time per step (median reported beside the mean)
+    bounds = [torch.cuda.Event(enable_timing=True)]
+    bounds[0].record(cur)
     t0 = time.perf_counter()
     if use_graph:
         inflight, done_prev = [], None
         for i in range(args.steps):
             h0 = time.perf_counter()
             done = replay(entry)
+            bounds.append(done)
             inflight.append((entry, done, i))
             h1 = time.perf_counter()
             # batch i + 1 on the side stream, after step i - 1's graph on the device: the build's count reads
@@ -519,10 +546,13 @@ def main():
     else:
         for i in range(args.steps):
             step(i)
+            bounds.append(torch.cuda.Event(enable_timing=True))
+            bounds[-1].record(cur)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    step_ms = [a.elapsed_time(b) for a, b in zip(bounds[:-1], bounds[1:])]
     rec.active = False
     if use_graph:
         inflight = entry = None
@@ -533,6 +563,8 @@ def main():
               f"optimizer {med[2]:.2f}  prefetch {med[3]:.2f}  sum {sum(med):.2f}", file=sys.stderr)
     vox = sum(batches[i % len(batches)][2] for i in range(args.steps))
     dt_max, vox_all = dp.max_over_ranks(dt), dp.sum_over_ranks(float(vox))
+    med_step = dp.max_over_ranks(statistics.median(step_ms))
+    rank_vox = dp.gather_floats(float(vox) / args.steps)  # level-0 voxels per step of every rank
     _lib.set_recorder(None)
     fams = rec.summary()
     fam_steps = args.family_steps if (args.record != "all" or use_graph) else 0
@@ -587,6 +619,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
+            "ms_per_step_median": med_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -596,7 +629,16 @@ def main():
             "config": {
                 "workload": workload,
                 "preset": preset,
+                "timed_step": "zero_grad -> forward (metadata from raw device coordinates) -> loss -> backward -> "
+                              "Adam step; BASELINE.md's metric excludes the optimizer step, so including it is "
+                              "conservative.  ms_per_step = wall time over the timed steps / steps (max over "
+                              "ranks); ms_per_step_median = median device time between consecutive step "
+                              "completions on the compute stream (max over ranks)",
                 "scenes_per_gpu": args.batch,
+                "scene_assignment": scene_note,
+                "rank_l0_voxels_per_step": {"min": min(rank_vox), "max": max(rank_vox),
+                                            "mean": sum(rank_vox) / len(rank_vox),
+                                            "max_over_mean": max(rank_vox) / (sum(rank_vox) / len(rank_vox))},
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world}",
                 "grad_exchange": None if not dist.is_initialized() else (

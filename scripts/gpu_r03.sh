@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-3 GPU session: STEPS (comma list) of test | kbench | pmc | bench | prof, each under its own time limit,
+# stopping at the first failure.  Outputs under gpurun_out/ (TAG names them).
+set -o pipefail
+TAG=${TAG:-r03}
+STEPS=${STEPS:-test,kbench,pmc}
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+for st in ${STEPS//,/ }; do
+  case $st in
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+        > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu_$TAG.log ;;
+    kbench)
+      timeout -k 10 400 python -u scripts/kbench.py > gpurun_out/kbench_$TAG.log 2>&1; rc=$?; cat gpurun_out/kbench_$TAG.log | tail -40 ;;
+    pmc)
+      TAG=$TAG bash scripts/gpu_pmc_r03.sh; rc=$? ;;
+    bench)
+      timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$TAG.log 2>&1; rc=$?; tail -3 gpurun_out/bench_$TAG.log | cut -c1-3000 ;;
+    prof)
+      TAG=$TAG STEPS=5 bash scripts/gpu_profile_r02.sh > gpurun_out/profsum_$TAG.log 2>&1; rc=$?; tail -40 gpurun_out/profsum_$TAG.log ;;
+    *) echo "unknown step $st"; rc=2 ;;
+  esac
+  echo "== step $st rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done

@@ -130,3 +130,28 @@ def test_grad_sync_world2():
         if p.is_alive():
             p.kill()
     assert dict(out) == {0: True, 1: True}, dict(out)
+
+
+def test_bench_lpt_balanced_batches():
+    """bench.py --balance lpt: every rank builds the same pool of world x batch rooms and takes its
+    balanced_shards share; the shares are disjoint, cover the pool and their point counts are close."""
+    import argparse
+    import bench
+    args = argparse.Namespace(batch=3, scale=20.0)
+    world = 2
+    bs = [bench.balanced_batch(args, r, world, 0) for r in range(world)]
+    n = [int(b["batch_offsets"][-1]) for b in bs]
+    assert all(len(b["batch_offsets"]) == args.batch + 1 for b in bs)
+    from wsss3d.synthetic import make_room
+    from wsss3d import dp
+    sizes = [len(make_room(100 * 1000 + i)[0]) for i in range(world * args.batch)]
+    shards = dp.balanced_shards(sizes, world)
+    assert sorted(sum(shards, [])) == list(range(world * args.batch))
+    loads = [sum(sizes[i] for i in s) for s in shards]
+    assert max(loads) - min(loads) <= max(sizes)
+    assert max(n) <= max(loads)  # the transform only crops points
+
+
+def test_gather_floats_world1():
+    from wsss3d import dp
+    assert dp.gather_floats(3.5) == [3.5]
