@@ -87,16 +87,29 @@ class GradSync:
 
     DDP all-reduces from autograd hooks while backward runs; a HIP graph that
     captures the backward would capture those collectives as well.  Here the
-    step's forward + backward is the graph and the exchange stays outside it:
-    the parameters start equal on every rank (broadcast from rank 0, as DDP's
-    constructor does), every gradient is a view of one flat fp32 buffer (so
+    parameters start equal on every rank (broadcast from rank 0, as DDP's
+    constructor does) and every gradient is a view of one flat fp32 buffer (so
     the captured backward writes it in place and the step zeroes it with
-    ``zero_grad(set_to_none=False)``), and `average()` issues ONE all-reduce
-    over the whole buffer (120 MB for the headline UNet: one large RCCL ring
-    all-reduce over xGMI, ~1 ms) followed by the 1/world scaling -- the same
-    mean DDP computes.  BN buffers stay local (as `wrap`, broadcast_buffers=False)."""
+    ``zero_grad(set_to_none=False)``).  The buffer is laid out in reverse
+    parameter order -- the order backward finalises gradients -- and cut into
+    buckets of about `bucket_mb`.  Two ways to exchange it:
 
-    def __init__(self, model, device):
+    * ``average()`` after the replay: ONE all-reduce over the whole buffer
+      (120 MB for the headline UNet) and the 1/world scaling, eagerly.
+    * overlapped (``overlap=True``, RCCL): post-accumulate-grad hooks count
+      each bucket's gradients; once a bucket's last gradient is final, and
+      every earlier bucket has gone out (the same order on every rank), its
+      all-reduce and scaling are issued on a side stream ordered after the
+      work queued so far -- inside a graph capture they are captured as graph
+      nodes that run beside the rest of the backward.  ``join()`` (called at
+      the end of the captured body) issues any bucket still pending and makes
+      the compute stream wait for the side stream, so the optimizer after the
+      replay sees the averaged gradients.
+
+    The mean is DDP's either way (BN buffers stay local, as `wrap`,
+    broadcast_buffers=False)."""
+
+    def __init__(self, model, device, overlap: bool = False, bucket_mb: float = 32.0):
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.params = [p for p in model.parameters() if p.requires_grad]
         if self.world > 1:
@@ -105,22 +118,84 @@ class GradSync:
                     dist.broadcast(p.data, 0)
         total = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(total, device=device, dtype=torch.float32)
-        off = 0
-        for p in self.params:
+        # reverse parameter order: the buckets backward completes first come first
+        order = list(reversed(self.params))
+        self.buckets, self._bucket_of = [], {}
+        cap = max(1, int(bucket_mb * 2 ** 20 / 4))
+        off, b0, n_in = 0, 0, 0
+        for p in order:
             if p.dtype != torch.float32:
                 raise TypeError("GradSync: fp32 parameters only")
             p.grad = self.flat[off:off + p.numel()].view_as(p)
+            self._bucket_of[p] = len(self.buckets)
             off += p.numel()
+            n_in += 1
+            if off - b0 >= cap:
+                self.buckets.append((b0, off, n_in))
+                b0, n_in = off, 0
+        if n_in:
+            self.buckets.append((b0, off, n_in))
+        self.overlap = bool(overlap) and self.world >= 1 and dist.is_initialized()
+        self._side = torch.cuda.Stream(device) if (self.overlap and device.type == "cuda") else None
+        self._pending = None
+        self._next = 0
+        self._hooks = []
+        if self.overlap:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
     def check_views(self):
         """The gradients must still be the flat buffer's views (a zero_grad(set_to_none=True) or a
         non-accumulating backward would have replaced them)."""
         off = 0
-        for p in self.params:
+        for p in reversed(self.params):
             g = p.grad
             if g is None or g.data_ptr() != self.flat[off:off + p.numel()].data_ptr():
                 raise RuntimeError("GradSync: a gradient is no longer a view of the flat buffer")
             off += p.numel()
+
+    # ---------------------------------------------------------------- overlapped exchange
+    def begin(self):
+        """Start of a step's backward (overlap mode): every bucket waits for all of its gradients again."""
+        self._pending = [n for (_, _, n) in self.buckets]
+        self._next = 0
+
+    def _issue(self, b):
+        b0, b1, _ = self.buckets[b]
+        view = self.flat[b0:b1]
+        if self._side is None:  # CPU (gloo): in place, in order
+            dist.all_reduce(view)
+            if self.world > 1:
+                view.mul_(1.0 / self.world)
+            return
+        cur = torch.cuda.current_stream(self.flat.device)
+        self._side.wait_stream(cur)  # the bucket's gradients (and everything queued before) are final
+        with torch.cuda.stream(self._side):
+            dist.all_reduce(view)
+            if self.world > 1:
+                view.mul_(1.0 / self.world)
+
+    def _on_grad(self, p):
+        if self._pending is None:
+            return
+        b = self._bucket_of[p]
+        self._pending[b] -= 1
+        # buckets go out strictly in index order (every rank issues the same collectives in the same order)
+        while self._next < len(self.buckets) and self._pending[self._next] <= 0:
+            self._issue(self._next)
+            self._next += 1
+
+    def join(self):
+        """End of the step's backward (overlap mode): issue what is still pending, in order, and order the
+        current stream after the exchange."""
+        if self._pending is None:
+            return
+        while self._next < len(self.buckets):
+            self._issue(self._next)
+            self._next += 1
+        if self._side is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
+        self._pending = None
 
     def average(self):
         if dist.is_initialized():

@@ -392,7 +392,12 @@ def main():
     n_params = sum(p.numel() for p in model.parameters())
     # the reference's optimizer (train.py:39, Adam lr 1e-3); one fused multi-tensor kernel per step
     # (--foreach-adam: torch's default foreach form, ~21 launches per step)
-    gsync = dp.GradSync(model, dev) if graph_dp else None
+    # N ranks over RCCL: the bucket all-reduces are captured into the step's graph, issued as each bucket's
+    # gradients become final, so they run beside the rest of the backward (dp.GradSync overlap);
+    # BENCH_GRAD_OVERLAP=0 restores one all-reduce over the whole buffer after each replay
+    overlap = graph_dp and dist.is_initialized() and dist.get_backend() == "nccl" and \
+        os.environ.get("BENCH_GRAD_OVERLAP", "1") != "0"
+    gsync = dp.GradSync(model, dev, overlap=overlap) if graph_dp else None
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
                                                            {"fused": True, "capturable": use_graph}))
     cls_loss, _ = LOSS_REGISTRY.get("Classification")
@@ -421,10 +426,15 @@ def main():
         loss = cls_loss(logits, y)
         if contrastive:
             loss = loss + con_loss(*meta)
+        if gsync is not None and gsync.overlap:
+            gsync.begin()
         loss.backward()
         h2 = time.perf_counter()
         if gsync is not None:
-            gsync.average()
+            if gsync.overlap:
+                gsync.join()
+            else:
+                gsync.average()
         opt.step()
         h3 = time.perf_counter()
         if not args.no_prefetch and args.prefetch_at == "end":
@@ -450,9 +460,13 @@ def main():
         loss = cls_loss(logits, y)
         if contrastive:
             loss = loss + con_loss(*meta)
+        if gsync is not None and gsync.overlap:
+            gsync.begin()
         loss.backward()
         if gsync is None:
             opt.step()
+        elif gsync.overlap:
+            gsync.join()  # the exchange's graph nodes rejoin the captured stream
         return loss
 
     def capture(i):
@@ -485,8 +499,9 @@ def main():
             replay_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
             replay_ev[-1][0].record(cur)
         g.replay()
-        if gsync is not None:  # N ranks: the gradient exchange and Adam after the replayed backward
-            gsync.average()
+        if gsync is not None:  # N ranks: Adam after the replayed backward (+ the exchange unless captured)
+            if not gsync.overlap:
+                gsync.average()
             opt.step()
         done = torch.cuda.Event(enable_timing=True)
         done.record(cur)
@@ -642,7 +657,10 @@ def main():
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world}",
                 "grad_exchange": None if not dist.is_initialized() else (
-                    "one all-reduce over a flat gradient buffer after each graph replay, then Adam (dp.GradSync)"
+                    (f"dp.GradSync: {len(gsync.buckets)} bucket all-reduces captured into each step's graph, issued "
+                     "as each bucket's gradients become final (overlapped with the rest of backward), then Adam"
+                     if gsync.overlap else
+                     "dp.GradSync: one all-reduce over a flat gradient buffer after each graph replay, then Adam")
                     if graph_dp else "DDP, 64 MB buckets overlapped with backward"),
                 "comm_backend": dist.get_backend() if dist.is_initialized() else None,
                 "input_pipeline": "none" if args.no_prefetch else

@@ -237,6 +237,81 @@ def test_c4_per_rank_workload_graph_dp():
     _run_graph_world2(dict(m=32, reps=2, scale=50, scenes=5, oracle=True), timeout=600)
 
 
+def _overlap_worker(port, out):
+    """One-rank RCCL group: the bucket all-reduces of dp.GradSync(overlap=True) captured into the step's graph
+    (issued from post-accumulate-grad hooks during the captured backward) must leave exactly the local
+    gradients (a one-rank mean) after the replay, bit for bit."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "3d-weakly-supervised-semantic-segmentation_amd"), root):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    import sparseconvnet as scn
+    from sparseconvnet import metadata as scn_meta
+    from wsss3d import EasyDict, MODEL_REGISTRY, dp
+    from wsss3d.synthetic import make_batch
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        pc = EasyDict(name="SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=2, residual_blocks=True)
+        cls, _ = MODEL_REGISTRY.get("MultiLabel")
+        torch.manual_seed(0)
+        local = cls(pc).to(dev)
+        torch.manual_seed(0)
+        model = cls(pc).to(dev)
+        gs = dp.GradSync(model, dev, overlap=True, bucket_mb=0.25)
+        assert gs.overlap and len(gs.buckets) >= 3
+        bs = [make_batch(2, 20, seed=k) for k in range(2)]
+        xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(dev), feature=torch.from_numpy(b["feats"]).to(dev),
+                       batch_offsets=b["batch_offsets"]) for b in bs]
+        ys = [torch.from_numpy(b["scene_labels"]).to(dev) for b in bs]
+
+        def loss_of(net, k):
+            logits, _ = net((xs[k], None), istrain=True)
+            return F.multilabel_soft_margin_loss(logits, ys[k])
+
+        model.zero_grad(set_to_none=False)
+        loss_of(model, 0).backward()
+        torch.cuda.synchronize()
+        assert scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False) is not None
+        ev = scn_meta.prefetch_event(dev)
+        g = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(dev)
+        with torch.cuda.stream(cap):
+            g.capture_begin(capture_error_mode="relaxed")
+            model.zero_grad(set_to_none=False)
+            gs.begin()
+            loss_of(model, 1).backward()
+            gs.join()
+            g.capture_end()
+        assert scn_meta.captured_metadata()
+        torch.cuda.current_stream(dev).wait_event(ev)
+        g.replay()
+        loss_of(local, 1).backward()
+        torch.cuda.synchronize()
+        ok = all(torch.equal(p.grad, q.grad) for p, q in zip(model.parameters(), local.parameters()))
+        del g
+        out[0] = bool(ok)
+        dist.destroy_process_group()
+    except Exception as e:
+        out[0] = f"{type(e).__name__}: {e}"
+        raise
+
+
+def test_grad_overlap_captured_rccl():
+    ctx = mp.get_context("spawn")
+    manager = ctx.Manager()
+    out = manager.dict()
+    p = ctx.Process(target=_overlap_worker, args=(_free_port(), out))
+    p.start()
+    p.join(timeout=240)
+    if p.is_alive():
+        p.kill()
+    assert dict(out) == {0: True}, dict(out)
+
+
 def test_bench_graph_path_over_rccl():
     """The exact code path the driver's multi-GPU bench runs (HIP-graph steps, dp.GradSync's all-reduce over
     RCCL between replays, eager Adam), on a one-rank RCCL group (BENCH_DP_SELFTEST): a small workload must
@@ -253,6 +328,6 @@ def test_bench_graph_path_over_rccl():
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
     assert d["config"]["comm_backend"] == "nccl"
-    assert d["config"]["grad_exchange"] and "GradSync" in d["config"]["grad_exchange"]
+    assert d["config"]["grad_exchange"] and "captured" in d["config"]["grad_exchange"]
     assert "HIP graph" in d["config"]["launch"]
     assert d["value"] > 0
