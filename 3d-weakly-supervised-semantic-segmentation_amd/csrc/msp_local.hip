@@ -263,12 +263,15 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 // masks of groups with the offset and with rows past the staged capacity, and per active group three LDS
 // reads and 6 NT MFMAs.  Weight fragments come from the lane-ordered image two steps ahead (two register
 // sets).  The four classes' partial sums are added in class order through LDS at the end (deterministic).
-template <int NT>
+// D: weight register sets (prefetch distance in steps); XP: the next active group's pieces read from LDS
+// before the current group's MFMAs (production: D = 2, XP = 0 -- the other forms are measured through the
+// MSP_EXPERIMENTS build, scripts/kbench.py)
+template <int NT, int D = 2, int XP = 0>
 __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
     const int32_t* __restrict__ perm, int64_t n_pad, int n_y, float* __restrict__ out) {
-  constexpr int T = 128, NTH = 512, D = 2;
+  constexpr int T = 128, NTH = 512;
   constexpr int G = T / 16 / 2;  // row groups per wave
   constexpr int NC = 16 * NT;
   static_assert(4 * T * NC * 4 <= kXR * kXU * 16, "partial sums must fit the staging area");
@@ -381,11 +384,17 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       act |= (ballot64(pres) != 0 ? 1u : 0u) << g;
       far |= (ballot64(pres && li[g] >= kUCap) != 0 ? 1u : 0u) << g;
     }
+    u32x4 xa[3], xb[3];  // XP: two piece sets, the next group's read ahead (inactive groups are read and skipped)
+    if constexpr (XP) xload(li[0], xa);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+      u32x4(&cur)[3] = (XP && (g & 1)) ? xb : xa;
+      u32x4(&nxt)[3] = (XP && (g & 1)) ? xa : xb;
+      if constexpr (XP) {
+        if (g + 1 < G) xload(li[g + 1], nxt);
+      }
       if ((act >> g) & 1) {  // wave-uniform
-        u32x4 cur[3];
-        xload(li[g], cur);  // the group's pieces read right before its MFMAs (no look-ahead: registers)
+        if constexpr (!XP) xload(li[g], cur);  // the group's pieces read right before its MFMAs
         if ((far >> g) & 1) {  // rows past the staged capacity: straight from global memory (rare)
           const bool f = li[g] != kAbsent && li[g] >= kUCap;
           const int k = 32 * ks + 8 * q;
@@ -918,5 +927,38 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
                                             n_y, out);
   return check_launch("msp_conv_local");
 }
+
+#ifdef MSP_EXPERIMENTS
+// Kernel-variant entry for scripts/kbench.py (built only into lib/libmi3dsparse_exp.so by
+// scripts/build_exp.sh; the product library has no such symbol): msp_conv_local with the conv_x6s
+// template form selected by `variant` = 10 D + XP.
+int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+                       int tile_rows, const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows,
+                       const int32_t* perm, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                       msp_stream_t stream) {
+  MSP_REQUIRE(tile_rows == 128 && c_out % 32 == 0 && c_in % 16 == 0, "msp_exp_conv_local: shape");
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
+  if (n_tiles == 0) return MSP_OK;
+  MSP_REQUIRE(ws && ws_bytes >= msp_conv_local_workspace_size(K, c_in, c_out), "msp_exp_conv_local: ws");
+  hipStream_t s = as_stream(stream);
+  const int NT = 2, n_y = c_out / 32, nks = (c_in + 31) / 32;
+  u32x4* img = static_cast<u32x4*>(ws);
+  const int64_t lanes = (int64_t)K * n_y * nks * NT * 64;
+  split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                           (flip >> 1) & 1);
+  const unsigned grid = (unsigned)(n_tiles * n_y);
+  const int64_t n_pad = n_tiles * tile_rows;
+#define EV(DD, X)                                                                                              \
+  if (variant == 10 * DD + X) {                                                                                \
+    conv_x6s_kernel<2, DD, X><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows,    \
+                                                   perm, n_pad, n_y, out);                                     \
+    return check_launch("msp_exp_conv_local");                                                                 \
+  }
+  EV(2, 0) EV(2, 1) EV(1, 0) EV(1, 1)
+#undef EV
+  set_error("msp_exp_conv_local: no variant %d", variant);
+  return MSP_EINVAL;
+}
+#endif
 
 }  // extern "C"

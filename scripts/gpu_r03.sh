@@ -13,6 +13,9 @@ for st in ${STEPS//,/ }; do
         > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu_$TAG.log ;;
     kbench)
       timeout -k 10 400 python -u scripts/kbench.py > gpurun_out/kbench_$TAG.log 2>&1; rc=$?; cat gpurun_out/kbench_$TAG.log | tail -40 ;;
+    kbexp)  # the experiment build's kernel variants (lib/libmi3dsparse_exp.so, scripts/build_exp.sh)
+      MI3DSPARSE_LIB=$GRAFT_REPO_ROOT/3d-weakly-supervised-semantic-segmentation_amd/lib/libmi3dsparse_exp.so \
+        timeout -k 10 400 python -u scripts/kbench.py > gpurun_out/kbexp_$TAG.log 2>&1; rc=$?; cat gpurun_out/kbexp_$TAG.log | tail -40 ;;
     pmc)
       TAG=$TAG bash scripts/gpu_pmc_r03.sh; rc=$? ;;
     bench)

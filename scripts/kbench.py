@@ -61,6 +61,28 @@ def conv_forms(rules, V, cin, cout):
         perm, nbr_p = rules.dense_order()
         return ops.conv_nbr(x, wt, 27, flip, cout, nbr_p, V, perm=perm)
     forms["nbr"] = nbr
+    lib = _lib.load()
+    if hasattr(lib, "msp_exp_conv_local") and cout % 32 == 0:  # the MSP_EXPERIMENTS build: conv_x6s variants
+        import ctypes
+        fn = lib.msp_exp_conv_local
+        P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        fn.restype = I
+        fn.argtypes = [I, P, I, P, I, I, I, I, P, P, P, P, I64, P, P, ctypes.c_size_t, P]
+
+        def exp(variant):
+            def f(x, wt, flip):
+                loc = rules.local()
+                out = torch.empty(V, cout, device=DEV)
+                wsb = int(_lib.query("msp_conv_local_workspace_size", 27, cin, cout))
+                ws = torch.empty(max(wsb // 4, 1), device=DEV)
+                rc = fn(variant, ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(loc["lidx"]), ptr(loc["u_start"]),
+                        ptr(loc["u_rows"]), ptr(loc["perm"]), V, ptr(out), ptr(ws), wsb, _lib.stream())
+                if rc:
+                    raise RuntimeError(lib.msp_last_error().decode())
+                return out
+            return f
+        for v in [int(t) for t in os.environ.get("EXP_VARIANTS", "20,21,10,11").split(",") if t]:
+            forms[f"x6s_v{v}"] = exp(v)
     if hasattr(ops, "conv_unit") and cout <= 64:
         forms["unit"] = lambda x, wt, flip: ops.conv_unit(x, wt, 27, flip, cout, rules, V)
     if FORMS:
