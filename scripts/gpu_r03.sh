@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for st in ${STEPS//,/ }; do
   case $st in
     test)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
         > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu_$TAG.log ;;
     kbench)
       timeout -k 10 400 python -u scripts/kbench.py > gpurun_out/kbench_$TAG.log 2>&1; rc=$?; cat gpurun_out/kbench_$TAG.log | tail -40 ;;
