@@ -266,20 +266,23 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 // D: weight register sets (prefetch distance in steps); XP: the next active group's pieces read from LDS
 // before the current group's MFMAs (production: D = 2, XP = 0 -- the other forms are measured through the
 // MSP_EXPERIMENTS build, scripts/kbench.py)
-template <int NT, int D = 2, int XP = 0>
+// OC: offset classes (4: two row halves per class, G = 4 groups per wave; 8: one class per wave over all 8
+// groups -- each weight fragment loaded by one wave instead of two)
+template <int NT, int D = 2, int XP = 0, int OC = 4>
 __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
     const int32_t* __restrict__ perm, int64_t n_pad, int n_y, float* __restrict__ out) {
   constexpr int T = 128, NTH = 512;
-  constexpr int G = T / 16 / 2;  // row groups per wave
+  constexpr int RP = 8 / OC;      // row parts
+  constexpr int G = T / 16 / RP;  // row groups per wave
   constexpr int NC = 16 * NT;
   static_assert(4 * T * NC * 4 <= kXR * kXU * 16, "partial sums must fit the staging area");
   __shared__ u32x4 xs[kXR * kXU];
   __shared__ __attribute__((aligned(16))) uint16_t ls[kKMax * T];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int oc = wave & 3, rp = wave >> 2;  // offset class, row half (rows 16 G rp ..)
+  const int oc = wave % OC, rp = wave / OC;  // offset class, row part (rows 16 G rp ..)
   const int r = lane & 15, q = lane >> 4;
   const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
   const int cy = (int)(lb % n_y);
@@ -309,8 +312,8 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
   }
   if (tid < kXU) xs[kUCap * kXU + tid] = u32x4{0u, 0u, 0u, 0u};
 
-  // this wave's offsets o = oc + 4 j, j < kNJ (slots past K are empty steps), kNJ per input-channel slice
-  constexpr int kNJ = 8;
+  // this wave's offsets o = oc + OC j, j < kNJ (slots past K are empty steps), kNJ per input-channel slice
+  constexpr int kNJ = ((kKMax + OC - 1) / OC + D - 1) / D * D;
   const int n_steps = nks * kNJ;
   floatx4 acc[G][NT];
 #pragma unroll
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
   auto ld_w = [&](int s, u32x4 (&w)[NT][3]) {
     const int sc = s < n_steps ? s : n_steps - 1;
     const int ks = sc / kNJ, j = sc - ks * kNJ;
-    const int o = oc + 4 * j < K ? oc + 4 * j : oc;
+    const int o = oc + OC * j < K ? oc + OC * j : oc;
     const int ow = flip ? K - 1 - o : o;
     const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * 3 * 64 + lane;
 #pragma unroll
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
   // one (k-slice, offset) step of this wave over its row groups
   auto run = [&](int s, const u32x4 (&w)[NT][3]) {
     const int ks = s / kNJ, j = s - ks * kNJ;
-    const int o = oc + 4 * j;
+    const int o = oc + OC * j;
     if (o >= K) return;  // empty slot (wave-uniform)
     const uint16_t* lo = ls + o * T + 16 * G * rp + r;
     int li[G];
@@ -445,15 +448,35 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       }
     }
   }
-  // the four offset classes' partial sums, added in class order
+  // the offset classes' partial sums, added in a fixed order (OC = 8: classes 4-7 are first added into
+  // classes 0-3 through LDS, then the four sums as for OC = 4)
   __syncthreads();
   float* red = reinterpret_cast<float*>(xs);
+  auto slot = [&](int c, int g, int t) {
+    return reinterpret_cast<floatx4*>(red + ((int64_t)(c * T + 16 * (G * rp + g) + r)) * NC + 16 * t + 4 * q);
+  };
+  if constexpr (OC == 8) {
+    if (oc >= 4) {
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+      for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-      *reinterpret_cast<floatx4*>(red + ((int64_t)(oc * T + 16 * (G * rp + g) + r)) * NC + 16 * t + 4 * q) =
-          acc[g][t];
+        for (int t = 0; t < NT; ++t) *slot(oc - 4, g, t) = acc[g][t];
+    }
+    __syncthreads();
+    if (oc < 4) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] += *slot(oc, g, t);
+    }
+    __syncthreads();
+  }
+  if (oc < 4) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) *slot(oc, g, t) = acc[g][t];
+  }
   __syncthreads();
   constexpr int QPR = NC / 4;  // float4 quads per row
   for (int i = tid; i < T * QPR; i += NTH) {
@@ -920,10 +943,10 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int64_t n_pad = n_tiles * tile_rows;
   const unsigned grid = (unsigned)(n_tiles * n_y);
   if (NT == 2)
-    conv_x6s_kernel<2><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad,
+    conv_x6s_kernel<2, 1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad,
                                             n_y, out);
   else
-    conv_x6s_kernel<1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad,
+    conv_x6s_kernel<1, 1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad,
                                             n_y, out);
   return check_launch("msp_conv_local");
 }
@@ -956,6 +979,7 @@ int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, i
   }
   EV(2, 0) EV(2, 1) EV(1, 0) EV(1, 1)
 #undef EV
+
   set_error("msp_exp_conv_local: no variant %d", variant);
   return MSP_EINVAL;
 }
