@@ -857,11 +857,12 @@ int msp_wgrad_chunk_ok(int64_t n_rows, int K, int c_in, int c_out) {
   return (n_rows > 0 && K >= 1 && K <= 27 && c_in % 32 == 0 && c_out % 32 == 0) ? 1 : 0;
 }
 
-// Measured against the pair lists on the headline batch (profiles/r02/kbench_wgrad_chunk_r02.log): 0.59 vs
-// 0.65 ms at level 1 64 -> 64, 0.40 vs 0.46 at level 2, 0.59 vs 0.68 at level 0 32 -> 64; behind at level 0's
-// 32 and 64 -> 32 (0.36 / 0.60 vs 0.35 / 0.55 ms); the few-tile levels (< 2^14 rows) stay on the pair lists.
+// Measured against the pair lists on the headline batch's rulebooks (scripts/kbench.py, profiles/r03/kbench_r03*.log):
+// ahead for 64+ output channels at every level (level 1 64 -> 64 0.62 vs 0.64 ms, level 4 160 -> 160 0.082 vs
+// 0.107, level 5 192 -> 192 0.041 vs 0.052, level 6 224 -> 224 0.027 vs 0.036); behind at level 0's 32 output
+// channels (32 -> 32 0.36 vs 0.34 ms), which stay on the pair lists.
 int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out) {
-  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && c_out >= 64 && n_rows >= (1 << 14) ? 1 : 0;
+  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && c_out >= 64 ? 1 : 0;
 }
 
 int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out) {

@@ -297,7 +297,7 @@ def test_graph_captured_step_matches_eager():
 
 def test_graph_capture_after_a_smaller_batch():
     """The prefetched plan comes from the previous batch, whose level sizes may select other rulebooks (the
-    tile-local form from 4096 rows at 64 channels, the chunk-local weight gradient from 2^14 rows): replay
+    tile-local form from 4096 rows at 64 channels): replay
     prepares what THIS batch's sizes select (recorded uses, ops.prepare), so a capture after a much smaller
     batch builds nothing on demand (a host read there would abort the capture), and it matches eager."""
     import copy

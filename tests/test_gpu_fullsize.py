@@ -4,7 +4,7 @@ whole synthetic scenes): the HIP path against the fp64 CPU oracle with shared Re
 convolution (msp_conv_nbr, >= 1e5 rows and c_out >= 64: level 0's 32 -> 64 backward-data), the tile-local
 convolution (msp_conv_local, 64+ channels from 4096 rows: levels 1-4), the NetworkInNetwork kernel
 (msp_nin_gemm, >= 2^18 rows), the per-wave split-bf16 tile at level 0 (conv_x6r) and the chunk-local weight gradient
-(msp_conv_wgrad_chunk, c_out >= 64 from 2^14 rows) beside the pair-list one.  The test records which forms ran
+(msp_conv_wgrad_chunk, c_out >= 64) beside the pair-list one.  The test records which forms ran
 (through the same hook bench.py times them with) and requires each to have fired.
 
 Bars (tests/test_gpu_encoders.py explains them): per-point and scene features within 1e-4 of

@@ -709,7 +709,7 @@ def test_conv_wgrad_chunk_over_cap_falls_back():
     from sparseconvnet import _lib, metadata, ops
     from sparseconvnet._lib import ptr
     torch.manual_seed(9)
-    V, K = 20000, 27  # >= 2^14 rows: the module's backward asks for the chunk form first
+    V, K = 20000, 27  # the module's backward asks for the chunk form first (c_out = 64)
     # the SubmRules machinery over this map (square: inputs are rows of the same level), through a stand-in
     r = metadata.SubmRules.__new__(metadata.SubmRules)
     r._plan, r._key, r.K, r.filter_size = [], ("subm", 0, 3), K, 3
