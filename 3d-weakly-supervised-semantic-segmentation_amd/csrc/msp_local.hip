@@ -62,25 +62,6 @@ __device__ void bitonic_i32(int32_t* a) {
   }
 }
 
-template <int N>
-__device__ void bitonic_u64(uint64_t* a) {
-  for (int k = 2; k <= N; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < N; i += kLT) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t u = a[i], v = a[ixj];
-          if ((u > v) == ((i & k) == 0)) {
-            a[i] = v;
-            a[ixj] = u;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
 // The tile's distinct input rows, unordered: its K x T neighbour entries (all loads in flight first) go
 // into an open-addressing hash set in LDS (2 N2 int32 slots, load <= 0.42, linear probing by LDS CAS); each
 // first insertion appends the row to uq.  Returns the count.  (Round 2 replaced a bitonic sort of all
@@ -157,14 +138,110 @@ __global__ __launch_bounds__(kLT) void local_count_kernel(const int32_t* __restr
   }
 }
 
+// Rows of a tile into 16-row groups that share filter offsets (one wave, T / 64 rows per lane): each group is
+// seeded with the free row of most neighbours and grown by the row that adds the fewest offsets to the group's
+// union (ties: more neighbours, then the lower row).  conv_x6s runs one 16-row MFMA per (group, offset in the
+// union), so the union sizes are its work: on the headline batch this fills 0.66 / 0.69 / 0.68 of those rows at
+// levels 1-3 against 0.61 / 0.66 / 0.66 for rows sorted by mask (scripts/tile_fill.py).  Rows past nv (the
+// padding of the last tile) come last.  ord[i] = tile row at position i; gmask[g] = group g's offset union.
+template <int T>
+__device__ void group_rows(const uint32_t* __restrict__ msk, int nv, uint8_t* __restrict__ ord,
+                           uint32_t* __restrict__ gmask) {
+  constexpr int RPL = T / 64;
+  const int lane = threadIdx.x & 63;
+  uint32_t m[RPL];
+  int pc[RPL];
+  bool fr[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int p = lane + 64 * j;
+    m[j] = msk[p];
+    pc[j] = __popc(m[j]);
+    fr[j] = p < nv;
+  }
+  uint32_t um = 0;
+  for (int pos = 0; pos < nv; ++pos) {
+    const bool seed = (pos & 15) == 0;
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int score = seed ? 64 - pc[j] : __popc(um | m[j]) * 64 - pc[j];
+      const uint32_t key = ((uint32_t)score << 8) | (uint32_t)(lane + 64 * j);
+      best = fr[j] && key < best ? key : best;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)best, off);
+      best = o < best ? o : best;
+    }
+    const int p = (int)(best & 0xFF);
+#pragma unroll
+    for (int j = 0; j < RPL; ++j)
+      if (p == lane + 64 * j) fr[j] = false;
+    um = (seed ? 0u : um) | msk[p];
+    if (lane == 0) ord[pos] = (uint8_t)p;
+    if ((pos & 15) == 15 || pos == nv - 1) {
+      if (lane == 0) gmask[pos >> 4] = um;
+    }
+  }
+  for (int pos = nv + lane; pos < T; pos += 64) ord[pos] = (uint8_t)pos;
+  for (int g = (nv + 15) / 16 + lane; g < T / 16; g += 64) gmask[g] = 0u;
+}
+
+// conv_x6s's offset lists of one 128-row tile: for row half h (groups h, h + 2, h + 4, h + 6) the offsets with
+// at least one row in those groups, dealt to the half's 4 waves longest-first onto the least-loaded wave (load
+// = 4 x groups + 1 per offset; at most 8 offsets a wave).  Interleaving the halves over the groups evens them
+// out, and the lists even out the waves: the slowest of the 8 waves carries 0.94 of the mean against 0.86 for
+// offsets dealt round-robin (headline batch, levels 1-3).  wo[h][c][k]: offset k of wave c (0xFF: none).
+__device__ void deal_offsets(const uint32_t* __restrict__ gmask, int K, int h, uint8_t* __restrict__ item,
+                             int* __restrict__ cost, uint8_t* __restrict__ wo) {
+  int n = 0;  // item / cost: this half's LDS scratch, the offsets by cost descending (ties: lower offset first)
+  for (int o = 0; o < K; ++o) {
+    int a = 0;
+    for (int g = h; g < 8; g += 2) a += (gmask[g] >> o) & 1u;
+    if (a == 0) continue;
+    int i = n++;
+    while (i > 0 && cost[i - 1] < a) {
+      cost[i] = cost[i - 1];
+      item[i] = item[i - 1];
+      --i;
+    }
+    cost[i] = a;
+    item[i] = (uint8_t)o;
+  }
+  int l0 = 0, l1 = 0, l2 = 0, l3 = 0, n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // load and count per wave
+  for (int i = 0; i < n; ++i) {
+    int c = -1, lc = 0;
+    if (n0 < 8) c = 0, lc = l0;
+    if (n1 < 8 && (c < 0 || l1 < lc)) c = 1, lc = l1;
+    if (n2 < 8 && (c < 0 || l2 < lc)) c = 2, lc = l2;
+    if (n3 < 8 && (c < 0 || l3 < lc)) c = 3, lc = l3;
+    const int add = 4 * cost[i] + 1;
+    const int k = c == 0 ? n0++ : c == 1 ? n1++ : c == 2 ? n2++ : n3++;
+    if (c == 0) l0 += add;
+    else if (c == 1) l1 += add;
+    else if (c == 2) l2 += add;
+    else l3 += add;
+    wo[c * 8 + k] = item[i];
+  }
+  for (int k = n0; k < 8; ++k) wo[k] = 0xFF;
+  for (int k = n1; k < 8; ++k) wo[8 + k] = 0xFF;
+  for (int k = n2; k < 8; ++k) wo[16 + k] = 0xFF;
+  for (int k = n3; k < 8; ++k) wo[24 + k] = 0xFF;
+}
+
 template <int T, int N2>
 __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
                                                          int64_t n_pad, const int64_t* __restrict__ u_start,
                                                          int32_t* __restrict__ u_rows, uint16_t* __restrict__ lidx,
-                                                         int32_t* __restrict__ perm) {
+                                                         int32_t* __restrict__ perm, uint8_t* __restrict__ wave_off) {
   __shared__ int32_t h[2 * N2];
   __shared__ int32_t uq[N2];
-  __shared__ uint64_t mk[T];
+  __shared__ uint32_t msk[T];
+  __shared__ uint8_t ord[T];
+  __shared__ uint32_t gmask[T / 16];
+  __shared__ uint8_t ditem[2][kKMax];
+  __shared__ int dcost[2][kKMax];
   __shared__ int c;
   const int64_t t = blockIdx.x;
   const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c);
@@ -176,27 +253,24 @@ __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restri
   bitonic_i32_n(uq, n2);
   const int64_t u0 = u_start[t];
   for (int i = threadIdx.x; i < tot; i += kLT) u_rows[u0 + i] = uq[i];
-  // rows of the tile ordered by neighbour mask (padding rows last)
+  // rows of the tile grouped by shared offsets (padding rows last)
+  const int nv = (int)(n - t * T < T ? n - t * T : T);
   for (int p = threadIdx.x; p < T; p += kLT) {
-    const int64_t row = t * T + p;
-    uint64_t m = ~0ull >> 8;
-    if (row < n) {
-      m = 0;
-      for (int o = 0; o < K; ++o) m |= (uint64_t)(nbr[(int64_t)o * n + row] >= 0) << o;
-    }
-    mk[p] = (m << 8) | (uint64_t)p;
+    uint32_t m = 0;
+    if (p < nv)
+      for (int o = 0; o < K; ++o) m |= (uint32_t)(nbr[(int64_t)o * n + t * T + p] >= 0) << o;
+    msk[p] = m;
   }
   __syncthreads();
-  bitonic_u64<T>(mk);
-  for (int i = threadIdx.x; i < T; i += kLT) {
-    const int64_t row = t * T + (int)(mk[i] & 0xFF);
-    perm[t * T + i] = row < n ? (int32_t)row : -1;
-  }
+  if (threadIdx.x < 64) group_rows<T>(msk, nv, ord, gmask);
+  __syncthreads();
+  if (T == 128 && wave_off && K <= kKMax && threadIdx.x < 2)
+    deal_offsets(gmask, K, threadIdx.x, ditem[threadIdx.x], dcost[threadIdx.x], wave_off + (t * 2 + threadIdx.x) * 32);
+  for (int i = threadIdx.x; i < T; i += kLT) perm[t * T + i] = i < nv ? (int32_t)(t * T + ord[i]) : -1;
   // local index of every (offset, ordered row): binary search in the distinct list
   for (int idx = threadIdx.x; idx < K * T; idx += kLT) {
     const int o = idx / T, i = idx - o * T;
-    const int64_t row = t * T + (int)(mk[i] & 0xFF);
-    const int32_t v = row < n ? nbr[(int64_t)o * n + row] : -1;
+    const int32_t v = i < nv ? nbr[(int64_t)o * n + t * T + ord[i]] : -1;
     uint16_t li = kAbsent;
     if (v >= 0) {
       int lo = 0, hi = tot;
@@ -256,33 +330,33 @@ __global__ __launch_bounds__(256) void split_weights_lane_kernel(const float* __
 // j mod 16 over the 16 bank quads
 __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + p * 4 + (qq ^ ((j >> 2) & 3)); }
 
-// conv_x6s: block = 8 waves = 4 offset classes x 2 row halves on one 128-row tile and 16 NT output columns.
-// Per 32-input-channel slice the tile's distinct rows (row indices loaded once per tile and kept in
-// registers; the slice's value loads all in flight at once) are staged as exact bf16 pieces; a wave then walks
-// its offsets o = class + 4 j: the 16 local indices of each of its G = 4 row groups (one LDS wait), wave-uniform
-// masks of groups with the offset and with rows past the staged capacity, and per active group three LDS
-// reads and 6 NT MFMAs.  Weight fragments come from the lane-ordered image two steps ahead (two register
-// sets).  The four classes' partial sums are added in class order through LDS at the end (deterministic).
-// D: weight register sets (prefetch distance in steps); XP: the next active group's pieces read from LDS
-// before the current group's MFMAs (production: D = 2, XP = 0 -- the other forms are measured through the
-// MSP_EXPERIMENTS build, scripts/kbench.py)
-// OC: offset classes (4: two row halves per class, G = 4 groups per wave; 8: one class per wave over all 8
-// groups -- each weight fragment loaded by one wave instead of two)
-template <int NT, int D = 2, int XP = 0, int OC = 4>
+// conv_x6s: block = 8 waves = 2 row halves x 4 waves on one 128-row tile and 16 NT output columns.  Half h
+// holds the tile's 16-row groups h, h + 2, h + 4, h + 6 (the groups are ordered by how many offsets they
+// carry, so interleaving evens the halves out); wave c of half h walks the offsets wave_off lists for it
+// (msp_tile_local: every offset some row of the half has, dealt longest-first; NULL: o = c + 4 j), keeping its
+// G = 4 groups x NT column tiles of accumulators in registers.  Per 32-input-channel slice the tile's distinct
+// rows (row indices loaded once per tile and kept in registers; the slice's value loads all in flight at once)
+// are staged as exact bf16 pieces; per offset a wave reads its groups' 16 local indices (one LDS wait), takes
+// wave-uniform masks of the groups with the offset and with rows past the staged capacity, and per active
+// group issues three LDS reads and 6 NT MFMAs.  Weight fragments come from the lane-ordered image one offset
+// ahead.  The four waves' partial sums of a half are added in wave order through LDS at the end (deterministic).
+// AB (experiments build only; wrong results): bit 0 stages without the global value loads, bit 2 keeps the
+// first offset's weight fragments -- the ablations that price the staging and weight-load latencies.
+template <int NT, int AB = 0>
 __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
-    const int32_t* __restrict__ perm, int64_t n_pad, int n_y, float* __restrict__ out) {
-  constexpr int T = 128, NTH = 512;
-  constexpr int RP = 8 / OC;      // row parts
-  constexpr int G = T / 16 / RP;  // row groups per wave
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ wave_off, int64_t n_pad, int n_y,
+    float* __restrict__ out) {
+  constexpr int T = 128, NTH = 512, G = 4;
   constexpr int NC = 16 * NT;
   static_assert(4 * T * NC * 4 <= kXR * kXU * 16, "partial sums must fit the staging area");
   __shared__ u32x4 xs[kXR * kXU];
   __shared__ __attribute__((aligned(16))) uint16_t ls[kKMax * T];
+  __shared__ uint32_t wl[16];  // the tile's offset lists, [half][wave][8 bytes]
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int oc = wave % OC, rp = wave / OC;  // offset class, row part (rows 16 G rp ..)
+  const int wc = wave & 3, rp = wave >> 2;  // wave of the half, row half
   const int r = lane & 15, q = lane >> 4;
   const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
   const int cy = (int)(lb % n_y);
@@ -304,27 +378,46 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
         wv[b] = lw[((int64_t)o * n_pad + tile * T + pp) >> 1];
       }
     }
+    uint32_t lv = 0u;
+    if (tid < 16) {
+      if (wave_off) {
+        lv = reinterpret_cast<const uint32_t*>(wave_off)[tile * 16 + tid];
+      } else {  // word tid: half tid / 8, wave (tid / 2) % 4, slots 4 (tid % 2) .. + 3 of o = wave + 4 j
+        const int c = (tid >> 1) & 3, j0 = 4 * (tid & 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int o = c + 4 * (j0 + k);
+          lv |= (uint32_t)(o < K ? o : 0xFF) << (8 * k);
+        }
+      }
+    }
 #pragma unroll
     for (int b = 0; b < LW; ++b) {
       const int i = tid + NTH * b;
       if (i < K * T / 2) reinterpret_cast<uint32_t*>(ls)[i] = wv[b];
     }
+    if (tid < 16) wl[tid] = lv;
   }
   if (tid < kXU) xs[kUCap * kXU + tid] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();  // index tile, offset lists, zero row
+  // this wave's offsets (wave-uniform): up to 8 bytes, packed from the first, 0xFF past the last
+  const uint64_t list = (uint64_t)__builtin_amdgcn_readfirstlane(wl[rp * 8 + wc * 2]) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane(wl[rp * 8 + wc * 2 + 1]) << 32);
+  int n_j = 0;
+  while (n_j < 8 && ((list >> (8 * n_j)) & 0xFF) != 0xFF) ++n_j;
+  auto off_of = [&](int j) { return (int)((list >> (8 * j)) & 0xFF); };
 
-  // this wave's offsets o = oc + OC j, j < kNJ (slots past K are empty steps), kNJ per input-channel slice
-  constexpr int kNJ = ((kKMax + OC - 1) / OC + D - 1) / D * D;
-  const int n_steps = nks * kNJ;
   floatx4 acc[G][NT];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[g][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  auto ld_w = [&](int s, u32x4 (&w)[NT][3]) {
+  const int n_steps = nks * n_j;
+  auto ld_w = [&](int s, u32x4 (&w)[NT][3]) {  // fragments of step s = (slice, list position)
     const int sc = s < n_steps ? s : n_steps - 1;
-    const int ks = sc / kNJ, j = sc - ks * kNJ;
-    const int o = oc + OC * j < K ? oc + OC * j : oc;
+    const int ks = sc / n_j, j = sc - ks * n_j;
+    const int o = off_of(j);
     const int ow = flip ? K - 1 - o : o;
     const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * 3 * 64 + lane;
 #pragma unroll
@@ -350,9 +443,13 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       const int k = k0 + 8 * (i & 3);
       v[b][0] = v[b][1] = floatx4{0.f, 0.f, 0.f, 0.f};
       if (i < Us * 4 && k < c_in) {
-        const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + k);
-        v[b][0] = src[0];
-        v[b][1] = src[1];
+        if constexpr (AB & 1) {
+          v[b][0] = v[b][1] = floatx4{(float)srow[b], 1.f, 2.f, 3.f};
+        } else {
+          const floatx4* src = reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + k);
+          v[b][0] = src[0];
+          v[b][1] = src[1];
+        }
       }
     }
 #pragma unroll
@@ -366,20 +463,12 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       }
     }
   };
-  auto xload = [&](int li, u32x4 (&xp)[3]) {
-    const int jr = li < kUCap ? li : kUCap;  // absent (0xFFFF) and far rows -> zero row
-#pragma unroll
-    for (int p = 0; p < 3; ++p) xp[p] = xs[xs_unit(jr, p, q)];
-  };
   // one (k-slice, offset) step of this wave over its row groups
-  auto run = [&](int s, const u32x4 (&w)[NT][3]) {
-    const int ks = s / kNJ, j = s - ks * kNJ;
-    const int o = oc + OC * j;
-    if (o >= K) return;  // empty slot (wave-uniform)
-    const uint16_t* lo = ls + o * T + 16 * G * rp + r;
+  auto run = [&](int ks, int o, const u32x4 (&w)[NT][3]) {
+    const uint16_t* lo = ls + o * T + 16 * rp + r;
     int li[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) li[g] = lo[16 * g];
+    for (int g = 0; g < G; ++g) li[g] = lo[32 * g];  // group 2 g + rp
     uint32_t act = 0, far = 0;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -387,17 +476,13 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       act |= (ballot64(pres) != 0 ? 1u : 0u) << g;
       far |= (ballot64(pres && li[g] >= kUCap) != 0 ? 1u : 0u) << g;
     }
-    u32x4 xa[3], xb[3];  // XP: two piece sets, the next group's read ahead (inactive groups are read and skipped)
-    if constexpr (XP) xload(li[0], xa);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      u32x4(&cur)[3] = (XP && (g & 1)) ? xb : xa;
-      u32x4(&nxt)[3] = (XP && (g & 1)) ? xa : xb;
-      if constexpr (XP) {
-        if (g + 1 < G) xload(li[g + 1], nxt);
-      }
       if ((act >> g) & 1) {  // wave-uniform
-        if constexpr (!XP) xload(li[g], cur);  // the group's pieces read right before its MFMAs
+        u32x4 cur[3];
+        const int jr = li[g] < kUCap ? li[g] : kUCap;  // absent (0xFFFF) and far rows -> zero row
+#pragma unroll
+        for (int p = 0; p < 3; ++p) cur[p] = xs[xs_unit(jr, p, q)];
         if ((far >> g) & 1) {  // rows past the staged capacity: straight from global memory (rare)
           const bool f = li[g] != kAbsent && li[g] >= kUCap;
           const int k = 32 * ks + 8 * q;
@@ -431,52 +516,26 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     }
   };
 
-  static_assert(kNJ % D == 0, "steps per slice must be a multiple of the weight register sets");
-  u32x4 wf[D][NT][3];
-#pragma unroll
-  for (int d = 0; d < D; ++d) ld_w(d, wf[d]);
+  u32x4 wf[NT][3];
+  if (n_j) ld_w(0, wf);
   for (int ks = 0; ks < nks; ++ks) {
-    __syncthreads();  // previous slice's readers done (and the index tile / zero row written)
+    if (ks) __syncthreads();  // previous slice's readers done
     stage(ks);
     __syncthreads();
-    for (int j = 0; j < kNJ; j += D) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int st = ks * kNJ + j + d;
-        run(st, wf[d]);
-        ld_w(st + D, wf[d]);
-      }
+    for (int j = 0; j < n_j; ++j) {
+      run(ks, off_of(j), wf);
+      if constexpr (!(AB & 4)) ld_w(ks * n_j + j + 1, wf);
     }
   }
-  // the offset classes' partial sums, added in a fixed order (OC = 8: classes 4-7 are first added into
-  // classes 0-3 through LDS, then the four sums as for OC = 4)
+  // the four waves' partial sums of each half, added in wave order
   __syncthreads();
   float* red = reinterpret_cast<float*>(xs);
-  auto slot = [&](int c, int g, int t) {
-    return reinterpret_cast<floatx4*>(red + ((int64_t)(c * T + 16 * (G * rp + g) + r)) * NC + 16 * t + 4 * q);
-  };
-  if constexpr (OC == 8) {
-    if (oc >= 4) {
 #pragma unroll
-      for (int g = 0; g < G; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) *slot(oc - 4, g, t) = acc[g][t];
-    }
-    __syncthreads();
-    if (oc < 4) {
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[g][t] += *slot(oc, g, t);
-    }
-    __syncthreads();
-  }
-  if (oc < 4) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) *slot(oc, g, t) = acc[g][t];
-  }
+    for (int t = 0; t < NT; ++t)
+      *reinterpret_cast<floatx4*>(red + ((int64_t)(wc * T + 16 * (2 * g + rp) + r)) * NC + 16 * t + 4 * q) =
+          acc[g][t];
   __syncthreads();
   constexpr int QPR = NC / 4;  // float4 quads per row
   for (int i = tid; i < T * QPR; i += NTH) {
@@ -816,7 +875,8 @@ size_t msp_tile_local_workspace_size(int64_t n, int tile_rows) {
 }
 
 int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t* u_start, int32_t* u_rows,
-                   int64_t u_cap, uint16_t* lidx, int32_t* perm, void* ws, size_t ws_bytes, msp_stream_t stream) {
+                   int64_t u_cap, uint16_t* lidx, int32_t* perm, uint8_t* wave_off, void* ws, size_t ws_bytes,
+                   msp_stream_t stream) {
   MSP_REQUIRE(K >= 1 && K <= 32 && n >= 0, "msp_tile_local: K must be in [1, 32] (got %d)", K);
   MSP_REQUIRE(tile_rows == 64 || tile_rows == 128 || tile_rows == 256,
               "msp_tile_local: tile_rows must be 64, 128 or 256 (got %d)", tile_rows);
@@ -844,11 +904,14 @@ int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t*
   } else {
     MSP_REQUIRE(u_rows && lidx && perm, "msp_tile_local: NULL output");
     if (tile_rows == 64)
-      local_fill_kernel<64, 2048><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm);
+      local_fill_kernel<64, 2048><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm,
+                                                        wave_off);
     else if (tile_rows == 128)
-      local_fill_kernel<128, 4096><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm);
+      local_fill_kernel<128, 4096><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm,
+                                                        wave_off);
     else
-      local_fill_kernel<256, 8192><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm);
+      local_fill_kernel<256, 8192><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm,
+                                                        wave_off);
   }
   return check_launch("msp_tile_local");
 }
@@ -924,7 +987,8 @@ size_t msp_conv_local_workspace_size(int K, int c_in, int c_out) {
 
 int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                    const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
-                   int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream) {
+                   const uint8_t* wave_off, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                   msp_stream_t stream) {
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_local: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= kKMax, "msp_conv_local: K must be in [1, %d] (got %d)", kKMax, K);
@@ -944,22 +1008,22 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int64_t n_pad = n_tiles * tile_rows;
   const unsigned grid = (unsigned)(n_tiles * n_y);
   if (NT == 2)
-    conv_x6s_kernel<2, 1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad,
-                                            n_y, out);
+    conv_x6s_kernel<2><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, wave_off,
+                                         n_pad, n_y, out);
   else
-    conv_x6s_kernel<1, 1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, n_pad,
-                                            n_y, out);
+    conv_x6s_kernel<1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, wave_off,
+                                         n_pad, n_y, out);
   return check_launch("msp_conv_local");
 }
 
 #ifdef MSP_EXPERIMENTS
 // Kernel-variant entry for scripts/kbench.py (built only into lib/libmi3dsparse_exp.so by
 // scripts/build_exp.sh; the product library has no such symbol): msp_conv_local with the conv_x6s
-// template form selected by `variant` = 10 D + XP.
+// template form selected by `variant` = 100 AB + RR (RR = 1: offsets dealt round-robin, wave_off ignored).
 int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
                        int tile_rows, const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows,
-                       const int32_t* perm, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
-                       msp_stream_t stream) {
+                       const int32_t* perm, const uint8_t* wave_off, int64_t n_rows, float* out, void* ws,
+                       size_t ws_bytes, msp_stream_t stream) {
   MSP_REQUIRE(tile_rows == 128 && c_out % 32 == 0 && c_in % 16 == 0, "msp_exp_conv_local: shape");
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
@@ -972,13 +1036,14 @@ int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, i
                                                                            (flip >> 1) & 1);
   const unsigned grid = (unsigned)(n_tiles * n_y);
   const int64_t n_pad = n_tiles * tile_rows;
-#define EV(DD, X)                                                                                              \
-  if (variant == 10 * DD + X) {                                                                                \
-    conv_x6s_kernel<2, DD, X><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows,    \
-                                                   perm, n_pad, n_y, out);                                     \
+  const uint8_t* wo = variant % 10 == 1 ? nullptr : wave_off;
+#define EV(A)                                                                                                  \
+  if (variant / 100 == A) {                                                                                    \
+    conv_x6s_kernel<2, A><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm,  \
+                                               wo, n_pad, n_y, out);                                           \
     return check_launch("msp_exp_conv_local");                                                                 \
   }
-  EV(2, 0) EV(2, 1) EV(1, 0) EV(1, 1)
+  EV(0) EV(1) EV(4) EV(5)
 #undef EV
 
   set_error("msp_exp_conv_local: no variant %d", variant);

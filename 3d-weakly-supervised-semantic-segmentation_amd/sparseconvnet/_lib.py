@@ -35,7 +35,7 @@ PROTOTYPES = {
     "msp_tile_rulebook": (I, [P, I, I64, I, P, P, P, P, I64, P, SZ, P]),
     "msp_decode_keys": (I, [P, I64, I, P, P]),
     "msp_tile_local_workspace_size": (SZ, [I64, I]),
-    "msp_tile_local": (I, [P, I, I64, I, P, P, I64, P, P, P, SZ, P]),
+    "msp_tile_local": (I, [P, I, I64, I, P, P, I64, P, P, P, P, SZ, P]),
     "msp_conv_local_preferred": (I, [I64, I, I]),
     "msp_wgrad_chunk_ok": (I, [I64, I, I, I]),
     "msp_wgrad_chunk_preferred": (I, [I64, I, I, I]),
@@ -44,7 +44,7 @@ PROTOTYPES = {
     "msp_wgrad_chunk_index": (I, [P, P, P, I64, P, P, P, P, P]),
     "msp_conv_wgrad_chunk": (I, [P, I, P, I, I, I, P, P, P, P, P, I64, I64, P, P, P]),
     "msp_conv_local_workspace_size": (SZ, [I, I, I]),
-    "msp_conv_local": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P]),
+    "msp_conv_local": (I, [P, I, P, I, I, I, I, P, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_tile_rows": (I, [I64, I, I]),
     "msp_conv_tile_form": (I, [I64, I, I, I]),
     "msp_conv_tile_workspace_size": (SZ, [I64, I, I, I, I]),
@@ -66,8 +66,9 @@ PROTOTYPES = {
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),
     "msp_nin_gemm_ok": (I, [I64, I, I]),
-    "msp_nin_gemm_preferred": (I, [I64, I, I]),
-    "msp_nin_gemm": (I, [P, I64, I, P, I, P, P]),
+    "msp_nin_gemm_form": (I, [I64, I, I]),
+    "msp_nin_gemm_workspace_size": (SZ, [I, I]),
+    "msp_nin_gemm": (I, [P, I64, I, P, I, P, P, SZ, P]),
     "msp_input_avg_fwd": (I, [P, I, P, P, I64, P, P]),
     "msp_input_avg_bwd": (I, [P, I, P, P, I64, P, P]),
     "msp_output_fwd": (I, [P, I, P, I64, P, P]),

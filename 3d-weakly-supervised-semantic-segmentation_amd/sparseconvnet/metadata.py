@@ -67,16 +67,18 @@ def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS):
     n_tiles = (n + T - 1) // T
     u_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=device)
     ws = _ws(query("msp_tile_local_workspace_size", I64(n), T), device)
-    call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), None, 0, None, None, ptr(ws), ws.numel(), s)
+    call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), None, 0, None, None, None, ptr(ws), ws.numel(), s)
     total, max_u = (int(v) for v in u_start[n_tiles:].tolist()) if n_tiles else (0, 0)
     u_rows = torch.empty(max(total, 1), dtype=torch.int32, device=device)
     lidx = torch.empty((K, max(n_tiles * T, 1)), dtype=torch.int16, device=device)  # uint16 bits
     perm = torch.empty(max(n_tiles * T, 1), dtype=torch.int32, device=device)
+    # conv_x6s's per-tile offset lists (128-row tiles, K <= 27)
+    wave_off = torch.empty(max(n_tiles * 64, 1), dtype=torch.uint8, device=device) if T == 128 and K <= 27 else None
     if n_tiles:
         call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), ptr(u_rows), max(total, 1), ptr(lidx), ptr(perm),
-             ptr(ws), ws.numel(), s)
-    return dict(u_start=u_start, u_rows=u_rows, lidx=lidx, perm=perm, tile_rows=T, n_tiles=n_tiles, total=total,
-                max_u=max_u)
+             ptr(wave_off) if wave_off is not None else None, ptr(ws), ws.numel(), s)
+    return dict(u_start=u_start, u_rows=u_rows, lidx=lidx, perm=perm, wave_off=wave_off, tile_rows=T,
+                n_tiles=n_tiles, total=total, max_u=max_u)
 
 
 class PairLists:

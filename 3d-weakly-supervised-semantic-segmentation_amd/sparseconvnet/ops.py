@@ -135,7 +135,8 @@ def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0)
         4 * loc["total"] + 2 * K * loc["n_tiles"] * loc["tile_rows"] + 4 * loc["n_tiles"] * loc["tile_rows"]
     _record(kind + "/x6s", flops, lambda: call(
         "msp_conv_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
-        ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), n_rows, ptr(out), ptr(ws), wsb, _stream(x)),
+        ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), ptr(loc.get("wave_off")), n_rows, ptr(out),
+        ptr(ws), wsb, _stream(x)),
         nbytes)
     return out[:n_rows]
 
@@ -388,32 +389,39 @@ class _IdentityPairs:
         self.pair = ar[:max(n, 1)]
 
 
-def nin_gemm(a, b, force=False, kind="nin"):
-    """a[M][K] @ b[K][N] on msp_nin_gemm (HBM-bound tall-skinny product) where the library prefers it
-    (msp_nin_gemm_preferred: >= 2^18 rows); other shapes run torch's device GEMM (hipBLASLt)."""
+def nin_gemm(a, b, kind="nin"):
+    """a[M][K] @ b[K][N] on msp_nin_gemm (HBM-bound tall-skinny product: fp32 MFMA from 2^18 rows, split-bf16
+    MFMA below); channel counts that are not multiples of 16 are zero-padded around the call."""
     M, K = a.shape
     N = b.size(1)
+    Kp, Np = _pad16(K), _pad16(N)
+    if Kp != K:
+        a, b = _pad_cols(a.contiguous(), Kp), torch.cat([b, b.new_zeros(Kp - K, N)])
+    if Np != N:
+        b = _pad_cols(b, Np)
+    a, b = a.contiguous(), b.contiguous()
     flops, nbytes = 2.0 * M * K * N, 4 * (M * K + M * N + K * N)
-    q = "msp_nin_gemm_ok" if force else "msp_nin_gemm_preferred"
-    if not _lib.query(q, _lib.I64(M), K, N) or a.data_ptr() % 16 or b.data_ptr() % 16:
-        return _record(kind + "/blas", flops, lambda: a @ b, nbytes)
-    out = torch.empty((M, N), dtype=torch.float32, device=a.device)
-    _record(kind + "/hip", flops, lambda: call("msp_nin_gemm", ptr(a), M, K, ptr(b), N, ptr(out), _stream(a)), nbytes)
-    return out
+    out = torch.empty((max(M, 1), Np), dtype=torch.float32, device=a.device)
+    wsb = int(_lib.query("msp_nin_gemm_workspace_size", Kp, Np))
+    ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=a.device)
+    form = "/f32" if int(_lib.query("msp_nin_gemm_form", _lib.I64(M), Kp, Np)) == 1 else "/x6"
+    _record(kind + form, flops, lambda: call("msp_nin_gemm", ptr(a), M, Kp, ptr(b), Np, ptr(out), ptr(ws), wsb,
+                                             _stream(a)), nbytes)
+    out = out[:M]
+    return out if Np == N else out[:, :N].contiguous()
 
 
 class NetworkInNetworkFunction(torch.autograd.Function):
-    """out = x W (§8(a) a11).  Forward and backward-data are dense GEMMs on
-    hipBLASLt through torch; the weight gradient x^T dy (contraction over all
-    V rows, where the library GEMMs pick skinny split-free tiles) runs on
-    msp_conv_wgrad as a one-offset convolution with identity pairs."""
+    """out = x W (§8(a) a11).  Forward and backward-data on msp_nin_gemm (W, then W^T); the weight gradient
+    x^T dy (a contraction over all V rows) runs on msp_conv_wgrad as a one-offset convolution with identity
+    pairs."""
 
     @staticmethod
     def forward(ctx, x, weight):
         _check_feats(x)
         x = x.contiguous()
         ctx.save_for_backward(x, weight)
-        return nin_gemm(x, weight.contiguous(), kind="nin_fwd")
+        return nin_gemm(x, weight, kind="nin_fwd")
 
     @staticmethod
     def backward(ctx, gout):
@@ -421,7 +429,7 @@ class NetworkInNetworkFunction(torch.autograd.Function):
         g = gout.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = nin_gemm(g, weight.t().contiguous(), kind="nin_bwd_data")
+            dx = nin_gemm(g, weight.t(), kind="nin_bwd_data")
         if ctx.needs_input_grad[1]:
             cin, cout = weight.shape
             cin_p, cout_p = _pad16(cin), _pad16(cout)

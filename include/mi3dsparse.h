@@ -129,16 +129,23 @@ int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64
  * rows are cut into tiles of tile_rows (64, 128 or 256); per tile t the
  * distinct input rows its neighbour entries name are listed in ascending order
  * at u_rows[u_start[t] .. u_start[t+1]); perm[t*T + i] is the tile's i-th row
- * (rows ordered inside the tile by their neighbour mask, so 16-row groups share
- * offsets; -1 past n) and lidx[o][t*T + i] (uint16, [K][n_tiles*T]) the
- * position in the tile's list of that row's neighbour at offset o (0xFFFF:
- * none).  K <= 32.  Count-then-fill like msp_pair_lists: the counting call
- * (u_cap = 0) writes u_start[0..n_tiles] (u_start[n_tiles] = total) and
- * u_start[n_tiles+1] = the largest tile's count; the filling call (u_cap >=
- * total) reuses u_start.  Workspace: msp_tile_local_workspace_size. */
+ * (rows grouped inside the tile so that each 16-row group's rows share
+ * offsets: greedy, by fewest offsets added to the group's union; -1 past n)
+ * and lidx[o][t*T + i] (uint16, [K][n_tiles*T]) the position in the tile's
+ * list of that row's neighbour at offset o (0xFFFF: none).  K <= 32.
+ * wave_off (nullable; written for tile_rows = 128 and K <= 27, n_tiles x 64
+ * bytes): msp_conv_local's offset lists -- for row half h (16-row groups h,
+ * h+2, h+4, h+6) and wave c < 4, wave_off[t*64 + h*32 + c*8 + k] = the k-th
+ * offset that wave walks (0xFF: none), every offset some row of the half has
+ * listed once, dealt longest-first onto the least-loaded wave.
+ * Count-then-fill like msp_pair_lists: the counting call (u_cap = 0) writes
+ * u_start[0..n_tiles] (u_start[n_tiles] = total) and u_start[n_tiles+1] = the
+ * largest tile's count; the filling call (u_cap >= total) reuses u_start.
+ * Workspace: msp_tile_local_workspace_size. */
 size_t msp_tile_local_workspace_size(int64_t n, int tile_rows);
 int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t* u_start, int32_t* u_rows,
-                   int64_t u_cap, uint16_t* lidx, int32_t* perm, void* ws, size_t ws_bytes, msp_stream_t stream);
+                   int64_t u_cap, uint16_t* lidx, int32_t* perm, uint8_t* wave_off, void* ws, size_t ws_bytes,
+                   msp_stream_t stream);
 /* Decode keys back to (x, y, z, batch) int64 rows (SparseToDense, locations). */
 int msp_decode_keys(const uint64_t* keys, int64_t n, int log2_size, int64_t* coords, msp_stream_t stream);
 
@@ -174,14 +181,17 @@ int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows);
  * distinct input rows are staged in LDS once per 32 input channels and split
  * into exact bf16 pieces once; the rules read them from LDS.  flip and the
  * weight layouts as msp_conv_tile (bit 0: offset K-1-o, bit 1: wt is
- * [K][c_in][c_out], else [K][c_out][c_in]).  Workspace:
- * msp_conv_local_workspace_size (the split weight image). */
+ * [K][c_in][c_out], else [K][c_out][c_in]).  wave_off: msp_tile_local's
+ * offset lists of the same rulebook (NULL: offsets dealt round-robin, o = c +
+ * 4 j to wave c of each row half).  Workspace: msp_conv_local_workspace_size
+ * (the split weight image). */
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out);
 
 size_t msp_conv_local_workspace_size(int K, int c_in, int c_out);
 int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                    const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
-                   int64_t n_rows, float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
+                   const uint8_t* wave_off, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                   msp_stream_t stream);
 /* Submanifold weight gradient over a 128-row tile rulebook (msp_tile_rulebook, tile_rows = 128) and the
  * tile-local rulebook of the same map (msp_tile_local, tile_rows = 128): dW[o][ci][co] = sum over the rules
  * (i, j) of offset o of x[i][ci] dy[j][co] (the forward's [K][c_in][c_out] layout).  msp_wgrad_chunk_index
@@ -289,14 +299,20 @@ int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* su
 
 /* ---------------- NetworkInNetwork products (replaces SCN's NetworkInNetwork
  * forward / backward-data, scn.NetworkInNetwork in the UNet/FCN residual
- * shortcuts): C[M][N] = A[M][K] B[K][N], row-major fp32,
- * fp32 products and accumulation (f32 MFMA).  Forward: A = x, B = W[c_in][c_out];
- * backward-data: A = dy, B = W^T.  msp_nin_gemm_ok says whether the shape is
- * supported (K % 16 == 0, N % 16 == 0, K <= 1024); A and B 16-byte aligned. */
+ * shortcuts): C[M][N] = A[M][K] B[K][N], row-major fp32.
+ * Forward: A = x, B = W[c_in][c_out]; backward-data: A = dy, B = W^T.  Below
+ * 2^18 rows bf16 MFMA over exact three-piece splits of both operands (six
+ * piece products, fp32 accumulation), from 2^18 rows fp32 MFMA: fp32-class
+ * error either way, checked against fp64 in tests/test_gpu_ops.py.
+ * msp_nin_gemm_ok: K % 16 == 0, N % 16 == 0, K <= 1024; A, B and C 16-byte
+ * aligned.  Workspace (B's split fragment image):
+ * msp_nin_gemm_workspace_size(K, N) bytes. */
 int msp_nin_gemm_ok(int64_t M, int K, int N);
-/* whether msp_nin_gemm beats the library GEMM for this shape (measured: M >= 2^18 rows) */
-int msp_nin_gemm_preferred(int64_t M, int K, int N);
-int msp_nin_gemm(const float* A, int64_t M, int K, const float* B, int N, float* C, msp_stream_t stream);
+/* the form msp_nin_gemm runs: 1 = fp32 MFMA, 2 = split-bf16 MFMA, 0 = unsupported shape */
+int msp_nin_gemm_form(int64_t M, int K, int N);
+size_t msp_nin_gemm_workspace_size(int K, int N);
+int msp_nin_gemm(const float* A, int64_t M, int K, const float* B, int N, float* C, void* ws, size_t ws_bytes,
+                 msp_stream_t stream);
 
 /* ---------------- input / output / pooling layers */
 /* mode-4 average: out[v] = mean of feats[perm[j]] for j in [vstart[v], vstart[v+1]) */

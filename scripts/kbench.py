@@ -28,7 +28,7 @@ DEV = "cuda"
 
 
 def timeit(f, n=N):
-    for _ in range(2):
+    for _ in range(max(2, n // 2)):
         f()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
@@ -67,7 +67,7 @@ def conv_forms(rules, V, cin, cout):
         fn = lib.msp_exp_conv_local
         P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
         fn.restype = I
-        fn.argtypes = [I, P, I, P, I, I, I, I, P, P, P, P, I64, P, P, ctypes.c_size_t, P]
+        fn.argtypes = [I, P, I, P, I, I, I, I, P, P, P, P, P, I64, P, P, ctypes.c_size_t, P]
 
         def exp(variant):
             def f(x, wt, flip):
@@ -76,12 +76,13 @@ def conv_forms(rules, V, cin, cout):
                 wsb = int(_lib.query("msp_conv_local_workspace_size", 27, cin, cout))
                 ws = torch.empty(max(wsb // 4, 1), device=DEV)
                 rc = fn(variant, ptr(x), cin, ptr(wt), 27, flip, cout, 128, ptr(loc["lidx"]), ptr(loc["u_start"]),
-                        ptr(loc["u_rows"]), ptr(loc["perm"]), V, ptr(out), ptr(ws), wsb, _lib.stream())
+                        ptr(loc["u_rows"]), ptr(loc["perm"]), ptr(loc["wave_off"]), V, ptr(out), ptr(ws), wsb,
+                        _lib.stream())
                 if rc:
                     raise RuntimeError(lib.msp_last_error().decode())
                 return out
             return f
-        for v in [int(t) for t in os.environ.get("EXP_VARIANTS", "20,21,10,11").split(",") if t]:
+        for v in [int(t) for t in os.environ.get("EXP_VARIANTS", "0,1").split(",") if t]:
             forms[f"x6s_v{v}"] = exp(v)
     if hasattr(ops, "conv_unit") and cout <= 64:
         forms["unit"] = lambda x, wt, flip: ops.conv_unit(x, wt, 27, flip, cout, rules, V)
@@ -131,15 +132,23 @@ def main():
                 wt, flip = w, 1
                 ref = torch.einsum("onc,odc->nd", g64, w.double().flip(0))
             scale = ref.abs().max().item()
-            res = []
-            for name, f in conv_forms(rules, V, cin, cout).items():
-                try:
-                    ms = timeit(lambda: f(x, wt, flip))
-                    out = f(x, wt, flip)
-                    err = (out[:len(rows)].double() - ref).abs().max().item() / scale
-                    res.append(f"{name} {ms:6.3f}ms {flops / ms / 1e9:6.1f}TF {err:.0e}")
-                except Exception as e:  # a form that does not take this shape
-                    res.append(f"{name} n/a ({str(e)[:40]})")
+            res, best = [], {}
+            forms = conv_forms(rules, V, cin, cout)
+            for _ in range(2):  # two passes over the forms, the better of each form's medians (clock ramp)
+                for name, f in forms.items():
+                    try:
+                        ms = timeit(lambda: f(x, wt, flip))
+                        best[name] = min(best.get(name, ms), ms)
+                    except Exception as e:  # a form that does not take this shape
+                        best[name] = str(e)[:40]
+            for name, f in forms.items():
+                if isinstance(best[name], str):
+                    res.append(f"{name} n/a ({best[name]})")
+                    continue
+                ms = best[name]
+                out = f(x, wt, flip)
+                err = (out[:len(rows)].double() - ref).abs().max().item() / scale
+                res.append(f"{name} {ms:6.3f}ms {flops / ms / 1e9:6.1f}TF {err:.0e}")
             print(f"  {pas} {cin:3d}->{cout:3d}  " + "  ".join(res), flush=True)
         if "wgrad" in PASSES:
             for cin, cout in ((a, a), (2 * a, a), (a, 2 * a)):

@@ -1,4 +1,4 @@
-"""NetworkInNetwork GEMM shapes on msp_nin_gemm and of the headline UNet (x[V, 2a] @ W[2a, a] and
+"""NetworkInNetwork GEMM shapes of the headline UNet on msp_nin_gemm (split-bf16 MFMA) (x[V, 2a] @ W[2a, a] and
 the backward-data g[V, a] @ W^T) on hipBLASLt vs rocBLAS (torch's
 preferred_blas_library), HIP-event timed; HBM roofline = (V*(cin+cout))*4 B / 8 TB/s."""
 import torch
@@ -15,7 +15,7 @@ for lib in ("msp", "cublaslt", "cublas"):
         x = torch.randn(V, ci, device=dev); w = torch.randn(ci, co, device=dev)
         g = torch.randn(V, co, device=dev)
         wt = w.t().contiguous()
-        mm = (lambda a, b: ops.nin_gemm(a, b, force=True)) if lib == "msp" else (lambda a, b: a @ b)
+        mm = (lambda a, b: ops.nin_gemm(a, b)) if lib == "msp" else (lambda a, b: a @ b)
         for name, fn in (("fwd", lambda: mm(x, w)), ("bwd", lambda: mm(g, wt))):
             for _ in range(3): fn()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -3,7 +3,7 @@ whole synthetic scenes): the HIP path against the fp64 CPU oracle with shared Re
 (oracle/parity.py), at the sizes where the production kernel selections take over -- the dense row-group
 convolution (msp_conv_nbr, >= 1e5 rows and c_out >= 64: level 0's 32 -> 64 backward-data), the tile-local
 convolution (msp_conv_local, 64+ channels from 4096 rows: levels 1-4), the NetworkInNetwork kernel
-(msp_nin_gemm, >= 2^18 rows), the per-wave split-bf16 tile at level 0 (conv_x6r) and the chunk-local weight gradient
+(msp_nin_gemm), the per-wave split-bf16 tile at level 0 (conv_x6r) and the chunk-local weight gradient
 (msp_conv_wgrad_chunk, c_out >= 64) beside the pair-list one.  The test records which forms ran
 (through the same hook bench.py times them with) and requires each to have fired.
 
@@ -89,10 +89,10 @@ def _run(name, m, reps, residual, scenes, need):
 
 def test_headline_unet_full_size_parity():
     """configs[2] network (SparseConvUNet m=32, block_reps=2, residual) on two whole scenes at 2 cm:
-    level 0 >= 2^18 voxels (NIN kernel), level 1 >= 1e5 (dense row groups)."""
+    level 0 >= 2^18 voxels (fp32 NIN form, split form below), level 1 >= 1e5 (dense row groups)."""
     kinds = _run("SparseConvUNet", 32, 2, True, 2,
                  need=["subm_fwd/x6r", "subm_fwd/x6s", "subm_bwd_data/x6s", "subm_bwd_data/x6g", "subm_fwd/x6d",
-                       "nin_fwd/hip", "nin_bwd_data/hip", "wgrad/x6", "wgrad/x6c", "nin_wgrad/x6", "conv_fwd/x6d",
+                       "nin_fwd/f32", "nin_bwd_data/f32", "nin_fwd/x6", "nin_bwd_data/x6", "wgrad/x6", "wgrad/x6c", "nin_wgrad/x6", "conv_fwd/x6d",
                        "deconv_fwd/f32"])
     assert kinds["subm_fwd/x6s"] >= 4
 

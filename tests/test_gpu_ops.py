@@ -198,7 +198,7 @@ def test_nin_join_add():
 
 @pytest.mark.parametrize("n,cin,cout", [(5000, 64, 32), (3001, 40, 24), (70000, 96, 48)])
 def test_nin_grads(n, cin, cout):
-    """NetworkInNetwork backward: dx on hipBLASLt, dW on msp_conv_wgrad with
+    """NetworkInNetwork backward: dx on msp_nin_gemm, dW on msp_conv_wgrad with
     identity pairs (any channel counts: padded to 16), against fp64 torch."""
     torch.manual_seed(n)
     coords, feats = _inputs(n, 30, n_feat=cin)
@@ -510,21 +510,37 @@ def test_residual_block_fused_matches_unfused(C, leak, nin):
                                    (30000, 64, 128), (20000, 96, 192)])
 def test_nin_gemm(M, K, N):
     """msp_nin_gemm (NetworkInNetwork forward / backward-data) against an fp64
-    product: fp32 products and accumulation, tolerance 1e-5 of max |ref|
-    (ragged last row group, 1-8 column tiles, several column chunks, the
-    headline UNet's forward and backward-data shapes)."""
+    product: below 2^18 rows split-bf16 MFMA (the x6 forms' bar, 1e-6 of max
+    |ref|), from 2^18 rows fp32 MFMA products and accumulation (1e-5); ragged
+    last row group, half-empty last k-slice, one- and two-tile column slices,
+    the headline UNet's forward and backward-data shapes."""
     from sparseconvnet import ops
     torch.manual_seed(M + K + N)
     a = torch.randn(M, K, device=DEV)
     b = torch.randn(K, N, device=DEV) / K ** 0.5
-    out = ops.nin_gemm(a, b, force=True)
-    close(out, a.double() @ b.double(), 1e-5, "nin_gemm")
+    out = ops.nin_gemm(a, b)
+    assert out.shape == (M, N)
+    if M:
+        ref = a.double() @ b.double()
+        tol = 1e-5 if M >= 1 << 18 else 1e-6
+        assert (out.double() - ref).abs().max().item() < tol * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("M,K,N", [(3001, 40, 24), (500, 8, 20)])
+def test_nin_gemm_padded(M, K, N):
+    """Channel counts off the 16-grid are zero-padded around msp_nin_gemm."""
+    from sparseconvnet import ops
+    torch.manual_seed(M)
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV)
+    ref = a.double() @ b.double()
+    assert (ops.nin_gemm(a, b).double() - ref).abs().max().item() < 1e-6 * ref.abs().max().item()
 
 
 def test_nin_layer_grad():
     """NetworkInNetwork fwd + bwd (dx via msp_nin_gemm on W^T, dW via msp_conv_wgrad) against fp64 torch."""
     torch.manual_seed(3)
-    coords, feats = _inputs(4000, 24, n_feat=64)  # below the preferred size: checks the routing too
+    coords, feats = _inputs(4000, 24, n_feat=64)
     g, _ = _pair(coords, feats)
     nin = scn.NetworkInNetwork(64, 32, False).to(DEV)
     x = g.features.detach().clone().requires_grad_(True)
@@ -586,6 +602,26 @@ def _check_local_rulebook(nbr, loc, n):
         absent = ent < 0
         assert bool((li[absent] == 0xFFFF).all())
         assert torch.equal(u[li[~absent]], ent[~absent])
+    wo = loc.get("wave_off")
+    if T == 128 and K <= 27:  # conv_x6s's offset lists: per half, every offset some row has, once, packed
+        wo = wo[:nt * 64].view(nt, 2, 4, 8).cpu().to(torch.int64)
+        has = torch.zeros(K, nt * T, dtype=torch.bool)
+        for t in range(nt):
+            rows = perm[t]
+            has[:, t * T:t * T + int((rows >= 0).sum())] = nb[:, rows[rows >= 0].long()] >= 0
+        has = has.view(K, nt, T // 16, 16).any(3)  # [K][tile][group]
+        for t in range(nt):
+            for h in range(2):
+                need = sorted(o for o in range(K) if bool(has[o, t, h::2].any()))
+                lists = wo[t, h]
+                got = []
+                for c in range(4):
+                    n = int((lists[c] != 0xFF).sum())
+                    assert bool((lists[c, :n] != 0xFF).all()) and bool((lists[c, n:] == 0xFF).all())
+                    got += lists[c, :n].tolist()
+                assert sorted(got) == need, (t, h)
+    else:
+        assert wo is None
 
 
 def test_tile_local_rulebook():
@@ -648,6 +684,10 @@ def test_conv_local_accuracy(cin, cout, flip):
     assert err < 1e-6, err
     yg = _gather_form(x, wt, flip, cout, rules, V)
     assert (y - yg).abs().max().item() / scale < 2e-6
+    # the same rulebook without the offset lists (offsets dealt round-robin to the waves)
+    loc = dict(rules.local(), wave_off=None)
+    y0 = ops.conv_local(x, wt, 27, flip, cout, type("R", (), {"local": lambda self, tile_rows=128: loc})(), V)
+    assert (y0.double() - ref).abs().max().item() / scale < 1e-6
 
 
 def test_conv_local_overflow_rows():
