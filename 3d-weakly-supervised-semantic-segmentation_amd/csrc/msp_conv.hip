@@ -105,6 +105,86 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   if (seg == 0 && e < cc) dw[(int64_t)o * cc + e] = ((part[0][el] + part[1][el]) + part[2][el]) + part[3][el];
 }
 
+// ---------------------------------------------------------------- narrow inputs
+// The first SubmanifoldConvolution of every encoder takes the 3 colour channels (models/SparseConvNet.py:62).
+// Padded to 16 channels it ran the per-wave MFMA tile at the cost of a 32-channel layer (0.3 ms at level 0 of
+// the headline batch, ~6 TF/s algorithmic) and its weight gradient the pair lists at 0.29 ms.  With CIN <= 4
+// the whole contraction is 27 CIN fmaf per output element: one thread per (row, output channel), the
+// neighbour indices and gathered inputs (broadcast over the COUT threads of a row) all in flight, weights in
+// LDS; exact fp32 products accumulated in offset-then-channel order.
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void conv_narrow_in_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                                                             int K, const int32_t* __restrict__ nbr, int64_t n,
+                                                             float* __restrict__ out) {
+  constexpr int RPB = 256 / COUT, KM = 27;
+  __shared__ float w_s[KM * CIN * COUT];
+  for (int i = threadIdx.x; i < K * CIN * COUT; i += 256) w_s[i] = wt[i];
+  __syncthreads();
+  const int c = threadIdx.x % COUT, rs = threadIdx.x / COUT;
+  for (int64_t row = (int64_t)blockIdx.x * RPB + rs; row < n; row += (int64_t)gridDim.x * RPB) {
+    int32_t nb[KM];
+#pragma unroll
+    for (int o = 0; o < KM; ++o) nb[o] = o < K ? nbr[o * n + row] : -1;
+    float xv[KM][CIN];
+#pragma unroll
+    for (int o = 0; o < KM; ++o)
+#pragma unroll
+      for (int k = 0; k < CIN; ++k) xv[o][k] = x[(int64_t)(nb[o] < 0 ? 0 : nb[o]) * CIN + k];
+    float acc = 0.f;
+#pragma unroll
+    for (int o = 0; o < KM; ++o)
+#pragma unroll
+      for (int k = 0; k < CIN; ++k)
+        if (nb[o] >= 0) acc = fmaf(xv[o][k], w_s[(o * CIN + k) * COUT + c], acc);
+    out[row * COUT + c] = acc;
+  }
+}
+
+// dW[o][k][c] = sum over rows i with a neighbour at offset o of x[nbr(i, o)][k] dy[i][c]: block = a contiguous
+// row range, thread = (row group g, output channel c) with the 27 CIN sums in registers; the row groups' sums
+// are added in group order in LDS and the block's partial goes to slab[block] (wgrad_reduce_kernel adds the
+// blocks in order: deterministic).
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void wgrad_narrow_in_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ dy, int K,
+                                                              const int32_t* __restrict__ nbr, int64_t n,
+                                                              int64_t n_parts, float* __restrict__ slab) {
+  constexpr int G = 256 / COUT, KM = 27;
+  __shared__ float red[KM * CIN * COUT];
+  const int c = threadIdx.x % COUT, g = threadIdx.x / COUT;
+  const int64_t r0 = n * blockIdx.x / n_parts, r1 = n * (blockIdx.x + 1) / n_parts;
+  float acc[KM][CIN];
+#pragma unroll
+  for (int o = 0; o < KM; ++o)
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) acc[o][k] = 0.f;
+  for (int64_t row = r0 + g; row < r1; row += G) {
+    const float d = dy[row * COUT + c];
+#pragma unroll
+    for (int o = 0; o < KM; ++o) {
+      const int32_t nb = o < K ? nbr[o * n + row] : -1;
+#pragma unroll
+      for (int k = 0; k < CIN; ++k) {
+        const float xv = x[(int64_t)(nb < 0 ? 0 : nb) * CIN + k];
+        if (nb >= 0) acc[o][k] = fmaf(xv, d, acc[o][k]);
+      }
+    }
+  }
+  for (int gg = 0; gg < G; ++gg) {
+    if (g == gg)
+#pragma unroll
+      for (int o = 0; o < KM; ++o)
+#pragma unroll
+        for (int k = 0; k < CIN; ++k) {
+          float& e = red[(o * CIN + k) * COUT + c];
+          e = gg == 0 ? acc[o][k] : e + acc[o][k];
+        }
+    __syncthreads();
+  }
+  float* sb = slab + (int64_t)blockIdx.x * K * CIN * COUT;
+  for (int i = threadIdx.x; i < K * CIN * COUT; i += 256) sb[i] = red[i];
+}
+
 inline int pick_tile(int n16) {
   if (n16 % 4 == 0) return 4;
   if (n16 % 3 == 0) return 3;
@@ -184,6 +264,57 @@ int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, 
   switch (NT) { LAUNCH(1) LAUNCH(2) LAUNCH(3) LAUNCH(4) }
 #undef LAUNCH
   return check_launch("msp_conv_pairs");
+}
+
+int msp_conv_narrow_in_ok(int K, int c_in, int c_out) {
+  return (K >= 1 && K <= 27 && c_in >= 1 && c_in <= 4 && (c_out == 16 || c_out == 32 || c_out == 64)) ? 1 : 0;
+}
+
+int msp_conv_narrow_in(const float* x, int c_in, const float* wt, int K, int c_out, const int32_t* nbr,
+                       int64_t n_rows, float* out, msp_stream_t stream) {
+  MSP_REQUIRE(msp_conv_narrow_in_ok(K, c_in, c_out), "msp_conv_narrow_in: needs K <= 27, c_in <= 4, c_out in "
+              "{16, 32, 64} (K=%d c_in=%d c_out=%d)", K, c_in, c_out);
+  MSP_REQUIRE(n_rows >= 0, "msp_conv_narrow_in: n_rows must be >= 0");
+  if (n_rows == 0) return MSP_OK;
+  MSP_REQUIRE(x && wt && nbr && out, "msp_conv_narrow_in: null pointer");
+  hipStream_t s = as_stream(stream);
+  const int64_t rpb = 256 / c_out;
+  int64_t grid = ceil_div(n_rows, rpb);
+  if (grid > 8192) grid = 8192;
+#define NL(CI, CO)                                                                                                   \
+  if (c_in == CI && c_out == CO) conv_narrow_in_kernel<CI, CO><<<(unsigned)grid, 256, 0, s>>>(x, wt, K, nbr, n_rows, out);
+  NL(1, 16) NL(1, 32) NL(1, 64) NL(2, 16) NL(2, 32) NL(2, 64) NL(3, 16) NL(3, 32) NL(3, 64) NL(4, 16) NL(4, 32)
+  NL(4, 64)
+#undef NL
+  return check_launch("msp_conv_narrow_in");
+}
+
+int64_t msp_conv_wgrad_narrow_parts(int64_t n_rows, int K, int c_in, int c_out) {
+  (void)K;
+  (void)c_in;
+  (void)c_out;
+  const int64_t p = ceil_div(n_rows > 0 ? n_rows : 1, 2048);
+  return p < 1 ? 1 : (p > 512 ? 512 : p);
+}
+
+int msp_conv_wgrad_narrow_in(const float* x, int c_in, const float* dy, int c_out, const int32_t* nbr, int K,
+                             int64_t n_rows, int64_t n_parts, float* slab, float* dw, msp_stream_t stream) {
+  MSP_REQUIRE(msp_conv_narrow_in_ok(K, c_in, c_out), "msp_conv_wgrad_narrow_in: needs K <= 27, c_in <= 4, c_out "
+              "in {16, 32, 64} (K=%d c_in=%d c_out=%d)", K, c_in, c_out);
+  MSP_REQUIRE(n_rows >= 0 && n_parts >= 1, "msp_conv_wgrad_narrow_in: n_rows=%lld n_parts=%lld",
+              (long long)n_rows, (long long)n_parts);
+  MSP_REQUIRE(x && dy && nbr && slab && dw, "msp_conv_wgrad_narrow_in: null pointer");
+  hipStream_t s = as_stream(stream);
+#define WL(CI, CO)                                                                                     \
+  if (c_in == CI && c_out == CO)                                                                       \
+    wgrad_narrow_in_kernel<CI, CO><<<(unsigned)n_parts, 256, 0, s>>>(x, dy, K, nbr, n_rows, n_parts, slab);
+  WL(1, 16) WL(1, 32) WL(1, 64) WL(2, 16) WL(2, 32) WL(2, 64) WL(3, 16) WL(3, 32) WL(3, 64) WL(4, 16) WL(4, 32)
+  WL(4, 64)
+#undef WL
+  const int64_t cc = (int64_t)c_in * c_out;
+  dim3 g2((unsigned)ceil_div(cc, 64), (unsigned)K);
+  wgrad_reduce_kernel<<<g2, 256, 0, s>>>(slab, n_parts, K, cc, dw);
+  return check_launch("msp_conv_wgrad_narrow_in");
 }
 
 int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out) {

@@ -57,6 +57,10 @@ PROTOTYPES = {
     "msp_conv_pairs": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
     "msp_wgrad_pieces": (I64, [I64, I, I, I]),
     "msp_conv_wgrad": (I, [P, I, P, I, P, P, P, I, I64, P, P, P]),
+    "msp_conv_narrow_in_ok": (I, [I, I, I]),
+    "msp_conv_narrow_in": (I, [P, I, P, I, I, P, I64, P, P]),
+    "msp_conv_wgrad_narrow_parts": (I64, [I64, I, I, I]),
+    "msp_conv_wgrad_narrow_in": (I, [P, I, P, I, P, I, I64, I64, P, P, P]),
     "msp_bn_partials": (I64, [I64, I]),
     "msp_bn_stats": (I, [P, I64, I, P, P]),
     "msp_bn_finalize": (I, [P, I64, I, D, D, I, P, P, P, P, P, P]),

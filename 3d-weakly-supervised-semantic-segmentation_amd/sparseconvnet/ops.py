@@ -8,6 +8,8 @@ are zero-padded to the MFMA chunk width here and sliced back.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -15,6 +17,12 @@ from . import _lib
 from ._lib import call, ptr
 
 _EMPTY = {}
+# diagnosis (bench.py per-kind breakdowns): recorded kinds carry the call's shape, "[c_in x c_out : rows]"
+_SHAPES = os.environ.get("MI3DSPARSE_KIND_SHAPES") == "1"
+
+
+def _shape(kind, c_in, c_out, n):
+    return f"{kind}[{c_in}x{c_out}:{n}]" if _SHAPES else kind
 
 
 def _stream(t):
@@ -108,7 +116,7 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
         # the contraction msp_conv_tile runs on 128-row tiles: bf16 MFMA over
         # exact three-piece operand splits (per-wave tiles for narrow outputs)
         form = int(_lib.query("msp_conv_tile_form", _lib.I64(n_rows), c_in, c_out, tr))
-        kind += {1: "/x6r", 2: "/x6d"}.get(form, "/f32")
+        kind = _shape(kind + {1: "/x6r", 2: "/x6d"}.get(form, "/f32"), c_in, c_out, n_rows)
         wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(n_rows), K, c_in, c_out, tr))
         ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
         # compulsory bytes: input rows, output rows, weights, rulebook (chunk
@@ -133,7 +141,7 @@ def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0)
     # compulsory bytes: input rows, output rows, weights, the tile-local rulebook
     nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
         4 * loc["total"] + 2 * K * loc["n_tiles"] * loc["tile_rows"] + 4 * loc["n_tiles"] * loc["tile_rows"]
-    _record(kind + "/x6s", flops, lambda: call(
+    _record(_shape(kind + "/x6s", c_in, c_out, n_rows), flops, lambda: call(
         "msp_conv_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
         ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), ptr(loc.get("wave_off")), n_rows, ptr(out),
         ptr(ws), wsb, _stream(x)),
@@ -196,7 +204,7 @@ def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
         flops = 2.0 * pairs.total * c_in * c_out
     # compulsory bytes: x and dy rows, the pair lists, dW
     nbytes = 4 * (x.size(0) * c_in + dy.size(0) * c_out + K * c_in * c_out) + 8 * pairs.total
-    _record(kind + "/x6", flops, lambda: call(
+    _record(_shape(kind + "/x6", c_in, c_out, dy.size(0)), flops, lambda: call(
         "msp_conv_wgrad", ptr(x), c_in, ptr(dy), c_out, ptr(pin), ptr(pout), ptr(pairs.off_start), K,
         n_pieces, ptr(slab), ptr(dw), _stream(x)), nbytes)
     return dw
@@ -222,7 +230,7 @@ def conv_wgrad_chunk(x, dy, rules, K, kind="wgrad", flops=None):
     # starts), the tiles' distinct-row lists, dW
     nbytes = 4 * (x.size(0) * c_in + n * c_out + K * c_in * c_out) + \
         tiles["n_chunks"] * (1 + 16 * 4) + 8 * tiles["tile_start"].numel() + 4 * idx["u_rows"].numel()
-    _record(kind + "/x6c", flops, lambda: call(
+    _record(_shape(kind + "/x6c", c_in, c_out, n), flops, lambda: call(
         "msp_conv_wgrad_chunk", ptr(x), c_in, ptr(dy), c_out, K, tiles["tile_rows"], ptr(tiles["tile_start"]),
         ptr(tiles["chunk_off"]), ptr(idx["chunk_lr"]), ptr(idx["u_start"]), ptr(idx["u_rows"]), n, ranges,
         ptr(slab), ptr(dw), _stream(x)), nbytes)
@@ -253,19 +261,33 @@ class SubmanifoldConvFunction(torch.autograd.Function):
     def forward(ctx, x, weight, rules):
         _check_feats(x)
         K, _, cin, cout = weight.shape
+        V = x.size(0)
+        nbr = getattr(rules, "nbr", None)
+        if nbr is not None and int(_lib.query("msp_conv_narrow_in_ok", K, cin, cout)):
+            # the colour input layer (c_in <= 4): straight from the neighbour map, no channel padding
+            xc, wc = x.contiguous(), weight.reshape(K, cin, cout).contiguous()
+            out = torch.empty((max(V, 1), cout), dtype=torch.float32, device=x.device)
+            if V:
+                nbytes = 4 * (V * cin + V * cout + K * cin * cout + K * V)
+                _record(_shape("subm_fwd/f32n", cin, cout, V), 2.0 * rules.n_rules * cin * cout, lambda: call(
+                    "msp_conv_narrow_in", ptr(xc), cin, ptr(wc), K, cout, ptr(nbr), V, ptr(out), _stream(x)), nbytes)
+            ctx.save_for_backward(xc, wc)
+            ctx.rules, ctx.dims, ctx.narrow = rules, (cin, cout), True
+            return out[:V]
         cin_p, cout_p = _pad16(cin), _pad16(cout)
         xp = _pad_cols(x.contiguous(), cin_p)
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
-        V = x.size(0)
         # flip bit 1: the weights in their own [K][c_in][c_out] layout (no transposed copy)
         out = conv_tile(xp, wp, K, 2, cout_p, rules, V, "subm_fwd",
                         2.0 * rules.n_rules * cin * cout)
         ctx.save_for_backward(xp, wp)
-        ctx.rules, ctx.dims = rules, (cin, cout)
+        ctx.rules, ctx.dims, ctx.narrow = rules, (cin, cout), False
         return out if cout_p == cout else out[:, :cout].contiguous()
 
     @staticmethod
     def backward(ctx, gout):
+        if ctx.narrow:
+            return SubmanifoldConvFunction._backward_narrow(ctx, gout)
         xp, wp = ctx.saved_tensors
         rules, (cin, cout) = ctx.rules, ctx.dims
         K, cin_p, cout_p = wp.shape
@@ -288,6 +310,30 @@ class SubmanifoldConvFunction(torch.autograd.Function):
             dx = dxp if cin_p == cin else dxp[:, :cin]
         if join is not None:
             join()
+        return dx, dw, None
+
+    @staticmethod
+    def _backward_narrow(ctx, gout):
+        x, w = ctx.saved_tensors
+        rules, (cin, cout) = ctx.rules, ctx.dims
+        K, V = w.size(0), x.size(0)
+        g = gout.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            parts = int(_lib.query("msp_conv_wgrad_narrow_parts", _lib.I64(V), K, cin, cout))
+            slab = torch.empty((parts, K, cin, cout), dtype=torch.float32, device=x.device)
+            dw = torch.empty((K, cin, cout), dtype=torch.float32, device=x.device)
+            nbytes = 4 * (V * cin + V * cout + K * cin * cout + K * V)
+            _record(_shape("wgrad/f32n", cin, cout, V), 2.0 * rules.n_rules * cin * cout, lambda: call(
+                "msp_conv_wgrad_narrow_in", ptr(x), cin, ptr(g), cout, ptr(rules.nbr), K, V, parts, ptr(slab),
+                ptr(dw), _stream(x)), nbytes)
+            dw = dw.reshape(K, 1, cin, cout)
+        if ctx.needs_input_grad[0]:  # (the input layer's features rarely need a gradient): padded tile path
+            cin_p, cout_p = _pad16(cin), _pad16(cout)
+            wp = _pad_weight(w, cin_p, cout_p)
+            dxp = conv_tile(_pad_cols(g, cout_p), wp, K, 1, cin_p, rules, V, "subm_bwd_data",
+                            2.0 * rules.n_rules * cin * cout)
+            dx = dxp[:, :cin]
         return dx, dw, None
 
 
@@ -462,7 +508,7 @@ def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, tra
              ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
         call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
     # compulsory bytes: statistics pass (read x) unless a join produced them, apply (read x, write y)
-    _record("bn_fwd/hbm", 0, run, 4 * V * C * (3 if (partial is None and train) else 2))
+    _record(_shape("bn_fwd/hbm", C, C, V), 0, run, 4 * V * C * (3 if (partial is None and train) else 2))
     return y, stats
 
 
@@ -483,7 +529,7 @@ def _bn_bwd(x, weight, stats, cfg, gy, addend):
              ptr(weight) if has_w else None, leak, train, ptr(addend) if addend is not None else None, ptr(dx),
              ptr(dw), ptr(db), s)
     # compulsory bytes: statistics pass (read x, dy), apply (read x, dy [, shortcut grad], write dx)
-    _record("bn_bwd/hbm", 0, run, 4 * V * C * (5 + (addend is not None)))
+    _record(_shape("bn_bwd/hbm", C, C, V), 0, run, 4 * V * C * (5 + (addend is not None)))
     return dx, (dw if has_w else None), (db if has_b else None)
 
 
@@ -549,7 +595,7 @@ class ResidualJoinFunction(torch.autograd.Function):
         V, C = a.shape
         out = torch.empty_like(a)
         partial = _bn_partial_buf(V, C, a.device)
-        _record("bn_join/hbm", 0, lambda: call("msp_add_bn_stats", ptr(a), ptr(b), V, C, ptr(out), ptr(partial),
+        _record(_shape("bn_join/hbm", C, C, V), 0, lambda: call("msp_add_bn_stats", ptr(a), ptr(b), V, C, ptr(out), ptr(partial),
                                                 _stream(a)), 12 * V * C)
         ctx.mark_non_differentiable(partial)
         ctx.set_materialize_grads(False)  # no zero-filled fp64 "gradient" of the partials per join

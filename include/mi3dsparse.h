@@ -264,6 +264,20 @@ int64_t msp_wgrad_pieces(int64_t total_pairs, int K, int c_in, int c_out);
 int msp_conv_wgrad(const float* x, int c_in, const float* dy, int c_out, const int32_t* pair_in,
                    const int32_t* pair_out, const int64_t* off_start, int K, int64_t n_pieces, float* slab,
                    float* dw, msp_stream_t stream);
+/* Submanifold convolution of a narrow input (the first layer's colour channels, models/SparseConvNet.py:62:
+ * SubmanifoldConvolution(3, m, 3, False)) straight from the neighbour map nbr[K][n_rows] (int32, -1 absent):
+ * out[i][c] = sum_o sum_k x[nbr[o][i]][k] wt[o][k][c], x [n][c_in] and wt [K][c_in][c_out] unpadded (the
+ * module's layout), fp32 fmaf per term, offsets then channels in order.  msp_conv_wgrad_narrow_in: dw[o][k][c] =
+ * sum over rows i with a neighbour at offset o of x[nbr[o][i]][k] dy[i][c]; n_parts blocks each write a partial
+ * to slab[n_parts][K][c_in][c_out], added in part order into dw (msp_conv_wgrad_narrow_parts: the count the
+ * library is tuned for).  Shapes: msp_conv_narrow_in_ok (K <= 27, c_in <= 4, c_out in {16, 32, 64}).  Replaces
+ * the padded 16-channel path of msp_conv_tile / msp_conv_wgrad for that layer. */
+int msp_conv_narrow_in_ok(int K, int c_in, int c_out);
+int msp_conv_narrow_in(const float* x, int c_in, const float* wt, int K, int c_out, const int32_t* nbr,
+                       int64_t n_rows, float* out, msp_stream_t stream);
+int64_t msp_conv_wgrad_narrow_parts(int64_t n_rows, int K, int c_in, int c_out);
+int msp_conv_wgrad_narrow_in(const float* x, int c_in, const float* dy, int c_out, const int32_t* nbr, int K,
+                             int64_t n_rows, int64_t n_parts, float* slab, float* dw, msp_stream_t stream);
 
 /* ---------------- batch norm + (leaky) ReLU (replaces SCN BatchNormalization
  * with leakiness; scn.BatchNormReLU / BatchNormLeakyReLU).

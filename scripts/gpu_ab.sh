@@ -1,0 +1,24 @@
+#!/bin/bash
+# Interleaved end-to-end A/B on one box: bench.py on the product library (A) and on lib/libmi3dsparse_exp.so
+# (B, scripts/build_exp.sh with EXP_FLAGS), ROUNDS times each, alternating; one JSON line per run in
+# gpurun_out/ab_$TAG.log (prefixed A / B).
+set -o pipefail
+TAG=${TAG:-ab}
+ROUNDS=${ROUNDS:-2}
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+EXP=$GRAFT_REPO_ROOT/3d-weakly-supervised-semantic-segmentation_amd/lib/libmi3dsparse_exp.so
+: > gpurun_out/ab_$TAG.log
+for i in $(seq 1 $ROUNDS); do
+  for v in A B; do
+    if [ $v = B ]; then export MI3DSPARSE_LIB=$EXP; else unset MI3DSPARSE_LIB; fi
+    timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 15 --warmup 5} > gpurun_out/ab_${TAG}_$v$i.log 2>&1 || exit $?
+    echo "$v $(grep '^{"metric"' gpurun_out/ab_${TAG}_$v$i.log)" >> gpurun_out/ab_$TAG.log
+    python - "$v" gpurun_out/ab_${TAG}_$v$i.log <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[2]) if l.startswith('{"metric"')][-1])
+fams = {k: round(v["ms"] / 5, 2) for k, v in d.get("roofline_families", {}).items() if isinstance(v, dict)}
+print(sys.argv[1], round(d["ms_per_step"], 2), round(d["ms_per_step_median"], 2), fams, flush=True)
+PY
+  done
+done

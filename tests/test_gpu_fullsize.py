@@ -35,6 +35,7 @@ class _Kinds:
         self.kinds = {}
 
     def run(self, kind, flops, fn, nbytes=0):
+        kind = kind.split("[")[0]  # without the shape tag of MI3DSPARSE_KIND_SHAPES=1
         self.kinds[kind] = self.kinds.get(kind, 0) + 1
         return fn()
 
@@ -93,10 +94,11 @@ def test_headline_unet_full_size_parity():
     kinds = _run("SparseConvUNet", 32, 2, True, 2,
                  need=["subm_fwd/x6r", "subm_fwd/x6s", "subm_bwd_data/x6s", "subm_bwd_data/x6g", "subm_fwd/x6d",
                        "nin_fwd/f32", "nin_bwd_data/f32", "nin_fwd/x6", "nin_bwd_data/x6", "wgrad/x6", "wgrad/x6c", "nin_wgrad/x6", "conv_fwd/x6d",
-                       "deconv_fwd/f32"])
+                       "deconv_fwd/f32", "subm_fwd/f32n", "wgrad/f32n"])
     assert kinds["subm_fwd/x6s"] >= 4
 
 
 def test_c2_unet_full_size_parity():
     """configs[1] network (SparseConvUNet m=16, block_reps=1, VGG blocks) on two whole scenes at 2 cm."""
-    _run("SparseConvUNet", 16, 1, False, 2, need=["subm_fwd/x6r", "subm_bwd_data/x6r", "wgrad/x6"])
+    _run("SparseConvUNet", 16, 1, False, 2, need=["subm_fwd/x6r", "subm_bwd_data/x6r", "wgrad/x6", "subm_fwd/f32n",
+                                                  "wgrad/f32n"])

@@ -95,7 +95,7 @@ def test_levels_match_oracle():
         size //= 2
 
 
-@pytest.mark.parametrize("cin,cout", [(3, 16), (16, 16), (32, 32), (64, 32), (48, 96), (32, 224)])
+@pytest.mark.parametrize("cin,cout", [(3, 16), (3, 32), (1, 64), (4, 32), (16, 16), (32, 32), (64, 32), (48, 96), (32, 224)])
 def test_subm_conv(cin, cout):
     torch.manual_seed(cin * 1000 + cout)
     coords, feats = _inputs(4000, 28, n_feat=cin)
