@@ -108,76 +108,137 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // ---------------------------------------------------------------- narrow inputs
 // The first SubmanifoldConvolution of every encoder takes the 3 colour channels (models/SparseConvNet.py:62).
 // Padded to 16 channels it ran the per-wave MFMA tile at the cost of a 32-channel layer (0.3 ms at level 0 of
-// the headline batch, ~6 TF/s algorithmic) and its weight gradient the pair lists at 0.29 ms.  With CIN <= 4
-// the whole contraction is 27 CIN fmaf per output element: one thread per (row, output channel), the
-// neighbour indices and gathered inputs (broadcast over the COUT threads of a row) all in flight, weights in
-// LDS; exact fp32 products accumulated in offset-then-channel order.
+// the headline batch, ~6 TF/s algorithmic) and its weight gradient the pair lists at 0.29 ms.
+//
+// Forward: one lane per output row.  The lane gathers its 27 neighbour indices (coalesced over the wave's 64
+// rows) and their CIN-channel input rows (one dwordx3 per neighbour for CIN = 3), and accumulates all COUT
+// outputs in registers from weights held in SGPRs (uniform scalar loads: every lane needs the same weight),
+// so the contraction is 27 CIN COUT v_fma_f32 with a scalar operand per row and nothing else; exact fp32
+// products, offsets then channels in order.
+template <int CIN>
+struct RowIn {
+  float v[CIN];
+};
+
 template <int CIN, int COUT>
 __global__ __launch_bounds__(256) void conv_narrow_in_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                                                              int K, const int32_t* __restrict__ nbr, int64_t n,
                                                              float* __restrict__ out) {
-  constexpr int RPB = 256 / COUT, KM = 27;
-  __shared__ float w_s[KM * CIN * COUT];
-  for (int i = threadIdx.x; i < K * CIN * COUT; i += 256) w_s[i] = wt[i];
-  __syncthreads();
-  const int c = threadIdx.x % COUT, rs = threadIdx.x / COUT;
-  for (int64_t row = (int64_t)blockIdx.x * RPB + rs; row < n; row += (int64_t)gridDim.x * RPB) {
-    int32_t nb[KM];
+  const RowIn<CIN>* xr = reinterpret_cast<const RowIn<CIN>*>(x);
+  auto ld = [&](int32_t i) {  // the neighbour's input row (zero where absent)
+    RowIn<CIN> v = xr[i < 0 ? 0 : i];
 #pragma unroll
-    for (int o = 0; o < KM; ++o) nb[o] = o < K ? nbr[o * n + row] : -1;
-    float xv[KM][CIN];
+    for (int k = 0; k < CIN; ++k) v.v[k] = i < 0 ? 0.f : v.v[k];
+    return v;
+  };
+  for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < n; row += (int64_t)gridDim.x * 256) {
+    float acc[COUT];
 #pragma unroll
-    for (int o = 0; o < KM; ++o)
-#pragma unroll
-      for (int k = 0; k < CIN; ++k) xv[o][k] = x[(int64_t)(nb[o] < 0 ? 0 : nb[o]) * CIN + k];
-    float acc = 0.f;
-#pragma unroll
-    for (int o = 0; o < KM; ++o)
+    for (int c = 0; c < COUT; ++c) acc[c] = 0.f;
+    // offsets in a rolled loop (the weights of one offset, CIN COUT of them, are its scalar operands): indices
+    // two offsets ahead, input rows one ahead
+    int32_t i1 = K > 1 ? nbr[n + row] : -1;
+    RowIn<CIN> v0 = ld(nbr[row]);
+    for (int o = 0; o < K; ++o) {
+      const int32_t i2 = o + 2 < K ? nbr[(o + 2) * n + row] : -1;
+      const RowIn<CIN> v1 = ld(i1);
+      const float* w = wt + o * CIN * COUT;
 #pragma unroll
       for (int k = 0; k < CIN; ++k)
-        if (nb[o] >= 0) acc = fmaf(xv[o][k], w_s[(o * CIN + k) * COUT + c], acc);
-    out[row * COUT + c] = acc;
+#pragma unroll
+        for (int c = 0; c < COUT; ++c) acc[c] = fmaf(v0.v[k], w[k * COUT + c], acc[c]);
+      v0 = v1;
+      i1 = i2;
+    }
+    floatx4* dst = reinterpret_cast<floatx4*>(out + row * COUT);
+#pragma unroll
+    for (int c = 0; c < COUT / 4; ++c) dst[c] = floatx4{acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]};
   }
 }
 
-// dW[o][k][c] = sum over rows i with a neighbour at offset o of x[nbr(i, o)][k] dy[i][c]: block = a contiguous
-// row range, thread = (row group g, output channel c) with the 27 CIN sums in registers; the row groups' sums
-// are added in group order in LDS and the block's partial goes to slab[block] (wgrad_reduce_kernel adds the
-// blocks in order: deterministic).
+// Weight gradient: dW^T[c][(o, k)] = sum over rows i of dy[i][c] X[i][(o, k)], X[i][(o, k)] = x[nbr(o, i)][k]
+// (0 where absent) -- a dense [COUT x rows] x [rows x 27 CIN] product with the rows as the contraction, on
+// v_mfma_f32_16x16x4_f32 (k = 4 rows).  Per 16-row batch a wave gathers X into its LDS tile (4 lanes per row,
+// 7 offsets each; columns past 27 CIN stay zero), its dy fragments for the batch's 4 k-steps are loaded from
+// global memory alongside (16 lanes read 64 contiguous bytes of one row); the block's 4 waves take batches
+// round-robin over a contiguous row range and their tiles are added in wave order into the block's slab
+// (wgrad_reduce_kernel adds the blocks in order: deterministic).
 template <int CIN, int COUT>
 __global__ __launch_bounds__(256) void wgrad_narrow_in_kernel(const float* __restrict__ x,
                                                               const float* __restrict__ dy, int K,
                                                               const int32_t* __restrict__ nbr, int64_t n,
                                                               int64_t n_parts, float* __restrict__ slab) {
-  constexpr int G = 256 / COUT, KM = 27;
-  __shared__ float red[KM * CIN * COUT];
-  const int c = threadIdx.x % COUT, g = threadIdx.x / COUT;
+  constexpr int KM = 27, KC = KM * CIN, NU = (KC + 15) / 16, NCOL = 16 * NU, MT = COUT / 16, BR = 16;
+  constexpr int OQ = (KM + 3) / 4;  // offsets per gathering lane
+  __shared__ float xl[4][BR][NCOL + 1];  // +1: the rows a ds_write_b32 spans land on distinct banks
+  __shared__ float red[KC * COUT];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const RowIn<CIN>* xr = reinterpret_cast<const RowIn<CIN>*>(x);
+  for (int i = lane; i < BR * (NCOL + 1); i += 64) (&xl[wave][0][0])[i] = 0.f;
   const int64_t r0 = n * blockIdx.x / n_parts, r1 = n * (blockIdx.x + 1) / n_parts;
-  float acc[KM][CIN];
+  floatx4 acc[MT][NU];
 #pragma unroll
-  for (int o = 0; o < KM; ++o)
+  for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int k = 0; k < CIN; ++k) acc[o][k] = 0.f;
-  for (int64_t row = r0 + g; row < r1; row += G) {
-    const float d = dy[row * COUT + c];
+    for (int u = 0; u < NU; ++u) acc[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int gr = lane & 15, oq = lane >> 4;  // gather: row of the batch, offset quarter
+  for (int64_t b0 = r0 + (int64_t)BR * wave; b0 < r1; b0 += 4 * BR) {
+    const int64_t grow = b0 + gr;
+    int32_t nb[OQ];
 #pragma unroll
-    for (int o = 0; o < KM; ++o) {
-      const int32_t nb = o < K ? nbr[o * n + row] : -1;
-#pragma unroll
-      for (int k = 0; k < CIN; ++k) {
-        const float xv = x[(int64_t)(nb < 0 ? 0 : nb) * CIN + k];
-        if (nb >= 0) acc[o][k] = fmaf(xv, d, acc[o][k]);
-      }
+    for (int j = 0; j < OQ; ++j) {
+      const int o = oq * OQ + j;
+      nb[j] = (o < K && o < KM && grow < r1) ? nbr[o * n + grow] : -1;
     }
+    float a[BR / 4][MT];  // dy fragments of the batch's k-steps, in flight with the gather
+#pragma unroll
+    for (int j = 0; j < BR / 4; ++j) {
+      const int64_t row = b0 + 4 * j + q;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) a[j][t] = row < r1 ? dy[row * COUT + 16 * t + r] : 0.f;
+    }
+    RowIn<CIN> v[OQ];
+#pragma unroll
+    for (int j = 0; j < OQ; ++j) v[j] = xr[nb[j] < 0 ? 0 : nb[j]];
+#pragma unroll
+    for (int j = 0; j < OQ; ++j) {
+      const int o = oq * OQ + j;
+      if (o < KM)
+#pragma unroll
+        for (int k = 0; k < CIN; ++k) xl[wave][gr][o * CIN + k] = nb[j] < 0 ? 0.f : v[j].v[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < BR / 4; ++j) {
+      float bv[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) bv[u] = xl[wave][4 * j + q][16 * u + r];
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][t], bv[u], acc[t][u], 0, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the tile's reads are done before the next batch's gather overwrites it
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  for (int gg = 0; gg < G; ++gg) {
-    if (g == gg)
+  // lane (r, q) register jj of tile (t, u): dW[(o, k) = 16 u + r][c = 16 t + 4 q + jj]; waves added in order
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w)
 #pragma unroll
-      for (int o = 0; o < KM; ++o)
+      for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int k = 0; k < CIN; ++k) {
-          float& e = red[(o * CIN + k) * COUT + c];
-          e = gg == 0 ? acc[o][k] : e + acc[o][k];
+        for (int u = 0; u < NU; ++u) {
+          const int ok = 16 * u + r;
+          if (ok < KC)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              float& e = red[ok * COUT + 16 * t + 4 * q + jj];
+              e = w == 0 ? acc[t][u][jj] : e + acc[t][u][jj];
+            }
         }
     __syncthreads();
   }
@@ -278,8 +339,7 @@ int msp_conv_narrow_in(const float* x, int c_in, const float* wt, int K, int c_o
   if (n_rows == 0) return MSP_OK;
   MSP_REQUIRE(x && wt && nbr && out, "msp_conv_narrow_in: null pointer");
   hipStream_t s = as_stream(stream);
-  const int64_t rpb = 256 / c_out;
-  int64_t grid = ceil_div(n_rows, rpb);
+  int64_t grid = ceil_div(n_rows, 256);
   if (grid > 8192) grid = 8192;
 #define NL(CI, CO)                                                                                                   \
   if (c_in == CI && c_out == CO) conv_narrow_in_kernel<CI, CO><<<(unsigned)grid, 256, 0, s>>>(x, wt, K, nbr, n_rows, out);
@@ -293,8 +353,9 @@ int64_t msp_conv_wgrad_narrow_parts(int64_t n_rows, int K, int c_in, int c_out) 
   (void)K;
   (void)c_in;
   (void)c_out;
-  const int64_t p = ceil_div(n_rows > 0 ? n_rows : 1, 2048);
-  return p < 1 ? 1 : (p > 512 ? 512 : p);
+  // blocks of at least 4 batches of 16 rows per wave, at most 1024 (4 per CU: 36 KiB of LDS each)
+  const int64_t p = ceil_div(n_rows > 0 ? n_rows : 1, 256);
+  return p < 1 ? 1 : (p > 1024 ? 1024 : p);
 }
 
 int msp_conv_wgrad_narrow_in(const float* x, int c_in, const float* dy, int c_out, const int32_t* nbr, int K,

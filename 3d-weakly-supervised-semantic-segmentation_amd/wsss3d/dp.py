@@ -140,6 +140,14 @@ class GradSync:
         self._pending = None
         self._next = 0
         self._hooks = []
+        if self.overlap and self._side is not None:
+            # the process group's communicator exists before any step is captured: created lazily by a first
+            # collective inside a capture, its set-up events were recorded on the capturing stream and the
+            # watchdog thread's query of them failed (hipErrorCapturedEvent) on a one-rank RCCL group, where no
+            # broadcast above ran first
+            warm = torch.zeros(1, device=device, dtype=torch.float32)
+            dist.all_reduce(warm)
+            torch.cuda.synchronize(device)
         if self.overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))

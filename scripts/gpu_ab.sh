@@ -1,7 +1,8 @@
 #!/bin/bash
 # Interleaved end-to-end A/B on one box: bench.py on the product library (A) and on lib/libmi3dsparse_exp.so
 # (B, scripts/build_exp.sh with EXP_FLAGS), ROUNDS times each, alternating; one JSON line per run in
-# gpurun_out/ab_$TAG.log (prefixed A / B).
+# gpurun_out/ab_$TAG.log (prefixed A / B).  B_ENV="VAR=value ..." sets environment variables for the B runs
+# only; B_LIB=0 keeps B on the product library (an environment-only A/B).
 set -o pipefail
 TAG=${TAG:-ab}
 ROUNDS=${ROUNDS:-2}
@@ -11,8 +12,11 @@ EXP=$GRAFT_REPO_ROOT/3d-weakly-supervised-semantic-segmentation_amd/lib/libmi3ds
 : > gpurun_out/ab_$TAG.log
 for i in $(seq 1 $ROUNDS); do
   for v in A B; do
-    if [ $v = B ]; then export MI3DSPARSE_LIB=$EXP; else unset MI3DSPARSE_LIB; fi
-    timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 15 --warmup 5} > gpurun_out/ab_${TAG}_$v$i.log 2>&1 || exit $?
+    unset MI3DSPARSE_LIB
+    [ $v = B ] && [ "${B_LIB:-1}" = 1 ] && export MI3DSPARSE_LIB=$EXP
+    envs=""
+    [ $v = B ] && envs="${B_ENV:-}"
+    env $envs timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 15 --warmup 5} > gpurun_out/ab_${TAG}_$v$i.log 2>&1 || exit $?
     echo "$v $(grep '^{"metric"' gpurun_out/ab_${TAG}_$v$i.log)" >> gpurun_out/ab_$TAG.log
     python - "$v" gpurun_out/ab_${TAG}_$v$i.log <<'PY'
 import json, sys
