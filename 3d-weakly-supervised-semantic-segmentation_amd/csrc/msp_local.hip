@@ -144,6 +144,20 @@ __global__ __launch_bounds__(kLT) void local_count_kernel(const int32_t* __restr
 // union), so the union sizes are its work: on the headline batch this fills 0.66 / 0.69 / 0.68 of those rows at
 // levels 1-3 against 0.61 / 0.66 / 0.66 for rows sorted by mask (scripts/tile_fill.py).  Rows past nv (the
 // padding of the last tile) come last.  ord[i] = tile row at position i; gmask[g] = group g's offset union.
+// Wave-wide minimum of x (every lane gets it): DPP shifts inside each 16-lane row, then the four row minima by
+// readlane -- no LDS round trips (a __shfl_xor ladder is six dependent ds_bpermute, and group_rows below runs
+// one reduction per row of a tile, 128 in sequence).
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+  constexpr int kId = -1;  // 0xFFFFFFFF: what a lane shifted in from outside its row contributes
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)x, 0x111, 0xF, 0xF, false));  // row_shr:1
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)x, 0x112, 0xF, 0xF, false));  // row_shr:2
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)x, 0x114, 0xF, 0xF, false));  // row_shr:4
+  x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)x, 0x118, 0xF, 0xF, false));  // row_shr:8
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)x, 15), b = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)x, 47), d = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  return min(min(a, b), min(c, d));
+}
+
 template <int T>
 __device__ void group_rows(const uint32_t* __restrict__ msk, int nv, uint8_t* __restrict__ ord,
                            uint32_t* __restrict__ gmask) {
@@ -169,11 +183,7 @@ __device__ void group_rows(const uint32_t* __restrict__ msk, int nv, uint8_t* __
       const uint32_t key = ((uint32_t)score << 8) | (uint32_t)(lane + 64 * j);
       best = fr[j] && key < best ? key : best;
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)best, off);
-      best = o < best ? o : best;
-    }
+    best = wave_min_u32(best);
     const int p = (int)(best & 0xFF);
 #pragma unroll
     for (int j = 0; j < RPL; ++j)

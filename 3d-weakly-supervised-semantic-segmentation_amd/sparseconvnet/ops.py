@@ -19,8 +19,6 @@ from ._lib import call, ptr
 _EMPTY = {}
 # diagnosis (bench.py per-kind breakdowns): recorded kinds carry the call's shape, "[c_in x c_out : rows]"
 _SHAPES = os.environ.get("MI3DSPARSE_KIND_SHAPES") == "1"
-# experiment knob (scripts/gpu_ab.sh B_ENV): pair-list weight-gradient pieces x this factor
-_PIECES_MUL = max(1, int(os.environ.get("MI3DSPARSE_WGRAD_PIECES_MUL", "1")))
 
 
 def _shape(kind, c_in, c_out, n):
@@ -200,7 +198,7 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None, kind="wgrad"):
 def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
     c_in, c_out = x.size(1), dy.size(1)
     dw = torch.empty((K, c_in, c_out), dtype=torch.float32, device=x.device)
-    n_pieces = int(_lib.query("msp_wgrad_pieces", _lib.I64(pairs.total), K, c_in, c_out)) * _PIECES_MUL
+    n_pieces = int(_lib.query("msp_wgrad_pieces", _lib.I64(pairs.total), K, c_in, c_out))
     slab = torch.empty((n_pieces, K, c_in, c_out), dtype=torch.float32, device=x.device)
     if flops is None:
         flops = 2.0 * pairs.total * c_in * c_out

@@ -21,7 +21,7 @@ for st in ${STEPS//,/ }; do
     bench)
       timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$TAG.log 2>&1; rc=$?; tail -3 gpurun_out/bench_$TAG.log | cut -c1-3000 ;;
     prof)
-      TAG=$TAG STEPS=5 bash scripts/gpu_profile_r02.sh > gpurun_out/profsum_$TAG.log 2>&1; rc=$?; tail -40 gpurun_out/profsum_$TAG.log ;;
+      TAG=$TAG bash scripts/gpu_profile_r03.sh > gpurun_out/profsum_$TAG.log 2>&1; rc=$?; tail -40 gpurun_out/profsum_$TAG.log ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== step $st rc=$rc"

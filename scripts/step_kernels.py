@@ -6,8 +6,19 @@ import collections
 import csv
 import sys
 
+def short(name):
+    """Kernel name without its argument list; torch's elementwise kernels keep the functor they run."""
+    base = name.split("(")[0]
+    if base.startswith("void at::native::"):
+        for key in ("FusedAdam", "CatArray", "direct_copy", "FillFunctor", "CUDAFunctor_add", "MulFunctor",
+                    "BinaryFunctor", "reduce_kernel", "index", "sum", "neg"):
+            if key in name:
+                return "at::native::" + key
+    return base[:90]
+
+
 rows = list(csv.DictReader(open(sys.argv[1])))
-iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][:70]) for r in rows)
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
 marks = [v[0] for v in iv if v[2].startswith("msp::scene_final_kernel")]
 first = int(sys.argv[2]) if len(sys.argv) > 2 else max(1, len(marks) // 4)
 last = int(sys.argv[3]) if len(sys.argv) > 3 else len(marks) - 2
