@@ -287,7 +287,7 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
               "msp_conv_tile: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= 128, "msp_conv_tile: K must be in [1, 128] (got %d)", K);
   MSP_REQUIRE(tile_rows == 128, "msp_conv_tile: tile_rows must be 128 (got %d)", tile_rows);
-  MSP_REQUIRE(flip >= 0 && flip <= 3, "msp_conv_tile: flip must be 0..3 (got %d)", flip);
+  MSP_REQUIRE(flip >= 0 && flip <= 7, "msp_conv_tile: flip must be 0..7 (got %d)", flip);
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);

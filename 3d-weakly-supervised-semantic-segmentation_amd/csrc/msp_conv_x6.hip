@@ -46,30 +46,7 @@ namespace msp {
 // wlay 1: wt given as [K][c_in][c_out] (the module's own layout; no transposed copy).
 __global__ __launch_bounds__(256) void split_weights_kernel(const float* __restrict__ wt, int K, int c_out, int c_in,
                                                             int NC, int KS, u32x4* __restrict__ img, int wlay = 0) {
-  const int K8 = KS / 8, WU = 3 * K8 * NC;
-  const int n_y = c_out / NC, nks = (c_in + KS - 1) / KS;
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (int64_t)K * n_y * nks * WU) return;
-  const int u = (int)(g % WU);
-  const int64_t rest = g / WU;
-  const int ks = (int)(rest % nks);
-  const int64_t r2 = rest / nks;
-  const int cy = (int)(r2 % n_y);
-  const int64_t o = r2 / n_y;
-  const int p = u / (K8 * NC), rem = u % (K8 * NC), k8 = rem / NC, n = rem % NC;
-  const int k = ks * KS + 8 * k8;
-  u32x4 pc[3] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
-  if (k < c_in) {  // c_in % 16 == 0: a unit is all data or all padding
-    if (wlay) {
-      const float* src = wt + (o * c_in + k) * c_out + cy * NC + n;
-      split8(floatx4{src[0], src[c_out], src[2 * c_out], src[3 * c_out]},
-             floatx4{src[4 * c_out], src[5 * c_out], src[6 * c_out], src[7 * c_out]}, pc);
-    } else {
-      const floatx4* src = reinterpret_cast<const floatx4*>(wt + ((o * c_out) + cy * NC + n) * c_in + k);
-      split8(src[0], src[1], pc);
-    }
-  }
-  img[g] = p == 0 ? pc[0] : (p == 1 ? pc[1] : pc[2]);
+  split_weights_unit(wt, K, c_out, c_in, NC, KS, img, wlay, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
 // D-deep pipelined form.  A step is one (offset, KS-deep k-slice); with the
@@ -564,8 +541,9 @@ int launch_x6r(const float* x, int c_in, const float* wt, int K, int flip, int c
   const int64_t n_tiles = ceil_div(n_rows, 128);
   u32x4* wimg = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)K * c_out * NKK * 32 * 6 / 16;
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg,
-                                                                       (flip >> 1) & 1);
+  if (!(flip & 4))  // bit 2: ws already holds this image (msp_split_weight_images)
+    split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg,
+                                                                         (flip >> 1) & 1);
   flip &= 1;
   const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
 #define LR(N, C)                                                                                               \
@@ -799,8 +777,9 @@ int launch_x6g(const float* x, int c_in, const float* wt, int K, int flip, int c
   const int nks = (c_in + 31) / 32;
   u32x4* wimg = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)K * c_out * nks * 32 * 6 / 16;
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * nt, 32, wimg,
-                                                                       (flip >> 1) & 1);
+  if (!(flip & 4))  // bit 2: ws already holds this image (msp_split_weight_images)
+    split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * nt, 32, wimg,
+                                                                         (flip >> 1) & 1);
   flip &= 1;
   const unsigned grid = (unsigned)(ceil_div(n_rows, (int64_t)kWaves * 16) * n_y);
 #define LL(N)                                                                                                 \
@@ -1080,8 +1059,9 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
   const int64_t n_tiles = ceil_div(n_rows, 128);
   u32x4* wsp = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)x6_weight_bytes(K, c_in, c_out) / 16;
-  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * p.nt, 32, wsp,
-                                                                       (flip >> 1) & 1);
+  if (!(flip & 4))  // bit 2: ws already holds this image (msp_split_weight_images)
+    split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * p.nt, 32, wsp,
+                                                                         (flip >> 1) & 1);
   flip &= 1;
   float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + round256(x6_weight_bytes(K, c_in, c_out)));
   float* dst = p.split > 1 ? part : out;
@@ -1132,6 +1112,7 @@ int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_nbr: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= 128, "msp_conv_nbr: K must be in [1, 128] (got %d)", K);
+  MSP_REQUIRE(flip >= 0 && flip <= 7, "msp_conv_nbr: flip must be 0..7 (got %d)", flip);
   MSP_REQUIRE(n_rows >= 0, "msp_conv_nbr: n_rows must be >= 0");
   if (n_rows == 0) return MSP_OK;
   MSP_REQUIRE(x && wt && nbr && out, "msp_conv_nbr: null pointer");

@@ -303,35 +303,26 @@ __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restri
 __global__ __launch_bounds__(256) void split_weights_lane_kernel(const float* __restrict__ wt, int K, int c_out,
                                                                  int c_in, int NT, u32x4* __restrict__ img,
                                                                  int wlay) {
-  const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (o, cy, ks, t, lane)
-  if (g >= (int64_t)K * n_y * nks * NT * 64) return;
-  const int lane = (int)(g & 63), r = lane & 15, q = lane >> 4;
-  int64_t rest = g >> 6;
-  const int t = (int)(rest % NT);
-  rest /= NT;
-  const int ks = (int)(rest % nks);
-  rest /= nks;
-  const int cy = (int)(rest % n_y);
-  const int64_t o = rest / n_y;
-  const int oc = 16 * (cy * NT + t) + r, k = 32 * ks + 8 * q;
-  floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-  if (k < c_in) {  // c_in % 16 == 0: an octet is all data or all padding
-    if (wlay) {
-      const float* src = wt + (o * c_in + k) * c_out + oc;
-      a = floatx4{src[0], src[c_out], src[2 * c_out], src[3 * c_out]};
-      b = floatx4{src[4 * c_out], src[5 * c_out], src[6 * c_out], src[7 * c_out]};
-    } else {
-      const floatx4* src = reinterpret_cast<const floatx4*>(wt + (o * c_out + oc) * c_in + k);
-      a = src[0];
-      b = src[1];
-    }
+  split_weights_lane_unit(wt, K, c_out, c_in, NT, img, wlay, (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
+
+// Every image of a step in one launch (msp_split_weight_images): thread g finds its image by a binary search in
+// the units' prefix sums and runs that image's unit.
+__global__ __launch_bounds__(256) void split_images_kernel(const msp_weight_image* __restrict__ d, int n,
+                                                           const int64_t* __restrict__ start, int64_t total) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= total) return;
+  int lo = 0, hi = n;  // start[lo] <= g < start[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (start[mid] <= g) lo = mid;
+    else hi = mid;
   }
-  u32x4* dst = img + ((g >> 6) * 3) * 64 + lane;
-  u32x4 pc[3];
-  split8(a, b, pc);
-#pragma unroll
-  for (int p = 0; p < 3; ++p) dst[p * 64] = pc[p];
+  const msp_weight_image e = d[lo];
+  const int64_t u = g - start[lo];
+  u32x4* img = static_cast<u32x4*>(e.img);
+  if (e.kind == 2) split_weights_lane_unit(e.wt, e.K, e.c_out, e.c_in, e.p, img, e.wlay, u);
+  else split_weights_unit(e.wt, e.K, e.c_out, e.c_in, e.p, 32, img, e.wlay, u);
 }
 
 // ---------------------------------------------------------------- convolution
@@ -984,6 +975,53 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
   return check_launch("msp_conv_wgrad_chunk");
 }
 
+// The image a convolution entry point splits its weights into for one call (msp_weight_image, the header).
+int msp_conv_weight_image(int entry, int64_t n_rows, int K, int c_in, int c_out, int flip, msp_weight_image* d) {
+  MSP_REQUIRE(d && K >= 1 && c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
+              "msp_conv_weight_image: bad shape (K=%d c_in=%d c_out=%d)", K, c_in, c_out);
+  d->K = K;
+  d->c_in = c_in;
+  d->c_out = c_out;
+  d->wlay = (flip >> 1) & 1;
+  const int nks = (c_in + 31) / 32;
+  if (entry == 1) {  // msp_conv_local: lane-ordered image
+    d->kind = 2;
+    d->p = local_nt(c_out);
+    d->units = (int64_t)K * (c_out / (16 * d->p)) * nks * d->p * 64;
+    d->bytes = (int64_t)msp_conv_local_workspace_size(K, c_in, c_out);
+    return MSP_OK;
+  }
+  d->kind = 1;
+  d->units = (int64_t)K * c_out * nks * 12;
+  if (entry == 0) {  // msp_conv_tile, 128-row tiles
+    if (c_out <= 32 && c_in <= 64) {
+      d->p = 16 * (c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1);
+    } else {
+      d->p = 16 * plan_x6(n_rows, c_out).nt;
+    }
+    d->bytes = (int64_t)msp_conv_tile_workspace_size(n_rows, K, c_in, c_out, 128);
+    return MSP_OK;
+  }
+  if (entry == 2) {  // msp_conv_nbr
+    const int n16 = c_out / 16;
+    d->p = 16 * (n16 % 4 == 0 ? 4 : (n16 % 3 == 0 ? 3 : (n16 % 2 == 0 ? 2 : 1)));
+    d->bytes = (int64_t)msp_conv_nbr_workspace_size(K, c_in, c_out);
+    return MSP_OK;
+  }
+  set_error("msp_conv_weight_image: entry must be 0 (tile), 1 (local) or 2 (nbr), got %d", entry);
+  return MSP_EINVAL;
+}
+
+int msp_split_weight_images(const msp_weight_image* descs, int n, const int64_t* unit_start, int64_t total_units,
+                            msp_stream_t stream) {
+  MSP_REQUIRE(n >= 0 && total_units >= 0, "msp_split_weight_images: n=%d total=%lld", n, (long long)total_units);
+  if (n == 0 || total_units == 0) return MSP_OK;
+  MSP_REQUIRE(descs && unit_start, "msp_split_weight_images: null pointer");
+  split_images_kernel<<<(unsigned)ceil_div(total_units, 256), 256, 0, as_stream(stream)>>>(descs, n, unit_start,
+                                                                                             total_units);
+  return check_launch("msp_split_weight_images");
+}
+
 // Measured against the gather forms on the headline batch's rulebooks (profiles/r02/kbench_local_r02_levels.log):
 // ahead from 64 channels on both sides and 4096 rows up (levels 1-4 of m = 32: 0-34 % less time), behind on the
 // 32-channel level 0 and on the few-tile levels 5-6 (grids of 16 / 4 tiles).
@@ -1003,7 +1041,7 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
               "msp_conv_local: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= kKMax, "msp_conv_local: K must be in [1, %d] (got %d)", kKMax, K);
   MSP_REQUIRE(tile_rows == 128, "msp_conv_local: tile_rows must be 128 (got %d)", tile_rows);
-  MSP_REQUIRE(flip >= 0 && flip <= 3, "msp_conv_local: flip must be 0..3 (got %d)", flip);
+  MSP_REQUIRE(flip >= 0 && flip <= 7, "msp_conv_local: flip must be 0..7 (got %d)", flip);
   const size_t need = msp_conv_local_workspace_size(K, c_in, c_out);
   MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_local: workspace too small (%zu < %zu)", ws_bytes, need);
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
@@ -1013,8 +1051,9 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
   const int n_y = c_out / (16 * NT), nks = (c_in + 31) / 32;
   u32x4* img = static_cast<u32x4*>(ws);
   const int64_t lanes = (int64_t)K * n_y * nks * NT * 64;
-  split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
-                                                                           (flip >> 1) & 1);
+  if (!(flip & 4))  // bit 2: ws already holds this image (msp_split_weight_images)
+    split_weights_lane_kernel<<<(unsigned)ceil_div(lanes, 256), 256, 0, s>>>(wt, K, c_out, c_in, NT, img,
+                                                                             (flip >> 1) & 1);
   const int64_t n_pad = n_tiles * tile_rows;
   const unsigned grid = (unsigned)(n_tiles * n_y);
   if (NT == 2)

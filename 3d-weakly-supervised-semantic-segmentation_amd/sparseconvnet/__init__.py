@@ -14,6 +14,7 @@ from .modules import (AddTable, BatchNormalization, BatchNormLeakyReLU, BatchNor
 from .networkArchitectures import FullyConvolutionalNet, FullyConvolutionalNetEncoder, UNet
 from .utils import checkpoint_restore, checkpoint_save, is_power2
 from . import _lib
+from . import weight_images
 
 # SCN's global work counters (train.py:50-51,86-87): multiply-adds of every
 # convolution (rules * nIn * nOut) and output elements of every convolution.
@@ -26,4 +27,5 @@ __all__ = [
     "BatchNormLeakyReLU", "Sequential", "ConcatTable", "AddTable", "JoinTable", "Identity", "SparseToDense",
     "UNet", "FullyConvolutionalNet", "FullyConvolutionalNetEncoder", "checkpoint_save", "checkpoint_restore",
     "is_power2", "forward_pass_multiplyAdd_count", "forward_pass_hidden_states", "prefetch_metadata",
+    "weight_images",
 ]

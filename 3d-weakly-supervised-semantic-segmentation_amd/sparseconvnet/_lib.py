@@ -17,6 +17,13 @@ LIB_PATH = os.environ.get("MI3DSPARSE_LIB", os.path.join(PKG_ROOT, "lib", "libmi
 
 P, I, I64, F, D, SZ = c_void_p, c_int, c_int64, c_float, c_double, c_size_t
 
+
+class WeightImage(ctypes.Structure):
+    """msp_weight_image (include/mi3dsparse.h)."""
+    _fields_ = [("wt", c_void_p), ("img", c_void_p), ("units", c_int64), ("bytes", c_int64), ("kind", ctypes.c_int32),
+                ("K", ctypes.c_int32), ("c_in", ctypes.c_int32), ("c_out", ctypes.c_int32), ("p", ctypes.c_int32),
+                ("wlay", ctypes.c_int32)]
+
 # name -> (restype, argtypes); mirrors include/mi3dsparse.h one to one
 PROTOTYPES = {
     "msp_abi_version": (I, []),
@@ -57,6 +64,8 @@ PROTOTYPES = {
     "msp_conv_pairs": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
     "msp_wgrad_pieces": (I64, [I64, I, I, I]),
     "msp_conv_wgrad": (I, [P, I, P, I, P, P, P, I, I64, P, P, P]),
+    "msp_conv_weight_image": (I, [I, I64, I, I, I, I, P]),
+    "msp_split_weight_images": (I, [P, I, P, I64, P]),
     "msp_conv_narrow_in_ok": (I, [I, I, I]),
     "msp_conv_narrow_in": (I, [P, I, P, I, I, P, I64, P, P]),
     "msp_conv_wgrad_narrow_parts": (I64, [I64, I, I, I]),

@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import weight_images as _wimg
 from ._lib import call, ptr
 
 _EMPTY = {}
@@ -49,6 +50,18 @@ def _pad_weight(w, cin_p, cout_p):
     if cin == cin_p and cout == cout_p:
         return w.contiguous()
     return F.pad(w, (0, cout_p - cout, 0, cin_p - cin))
+
+
+def _workspace(entry, wt, n_rows, K, c_in, c_out, flip, wsb, device):
+    """(workspace tensor, its bytes, flip) for a convolution call: the step's prepared weight image when
+    sparseconvnet.weight_images is on and holds a fresh one (flip bit 2: the split is skipped), else a new
+    workspace the call splits its weights into."""
+    wi = _wimg.active()
+    if wi is not None:
+        img = wi.lookup(entry, wt, n_rows, K, c_in, c_out, flip)
+        if img is not None:
+            return img, img.numel(), flip | 4
+    return torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=device), wsb, flip
 
 
 def _record(kind, flops, fn, nbytes=0):
@@ -118,7 +131,7 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
         form = int(_lib.query("msp_conv_tile_form", _lib.I64(n_rows), c_in, c_out, tr))
         kind = _shape(kind + {1: "/x6r", 2: "/x6d"}.get(form, "/f32"), c_in, c_out, n_rows)
         wsb = int(_lib.query("msp_conv_tile_workspace_size", _lib.I64(n_rows), K, c_in, c_out, tr))
-        ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
+        ws, wsb, flip = _workspace(0, wt, n_rows, K, c_in, c_out, int(flip), wsb, x.device)
         # compulsory bytes: input rows, output rows, weights, rulebook (chunk
         # offsets, 16 x (int32 src + uint16 row) per chunk, tile starts)
         nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
@@ -137,7 +150,7 @@ def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0)
     loc = rules.local()
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
     wsb = int(_lib.query("msp_conv_local_workspace_size", K, c_in, c_out))
-    ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
+    ws, wsb, flip = _workspace(1, wt, n_rows, K, c_in, c_out, int(flip), wsb, x.device)
     # compulsory bytes: input rows, output rows, weights, the tile-local rulebook
     nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
         4 * loc["total"] + 2 * K * loc["n_tiles"] * loc["tile_rows"] + 4 * loc["n_tiles"] * loc["tile_rows"]
@@ -244,7 +257,7 @@ def conv_nbr(x, wt, K, flip, c_out, nbr, n_rows, kind="conv_nbr", flops=0, perm=
     c_in = x.size(1)
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
     wsb = int(_lib.query("msp_conv_nbr_workspace_size", K, c_in, c_out))
-    ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=x.device)
+    ws, wsb, flip = _workspace(2, wt, n_rows, K, c_in, c_out, int(flip), wsb, x.device)
     # compulsory bytes: input rows, output rows, weights, the neighbour map (+ row order)
     nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out + K * n_rows + (n_rows if perm is not None else 0))
     _record(kind + "/x6g", flops, lambda: call(

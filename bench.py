@@ -148,7 +148,7 @@ class KernelRecorder:
 def pmc_traffic():
     """HBM bytes per conv-family call measured with rocprofv3 PMC counters on this workload
     (scripts/pmc_traffic.sh; committed under profiles/, newest round first), or None."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         if os.path.isfile(path):
             break
@@ -297,6 +297,9 @@ def main():
                          "prefetched, replayed on the compute stream while the next step is prefetched and "
                          "captured; N ranks: forward + backward captured, the gradient all-reduce and Adam eager after each "
                          "replay) -- removes the per-kernel launch gaps; default 1")
+    ap.add_argument("--weight-images", type=int, default=1, choices=[0, 1],
+                    help="1: split every convolution's weight image of a step in one launch at its start "
+                         "(sparseconvnet.weight_images); 0: each call splits its own")
     ap.add_argument("--balance", choices=["none", "lpt"], default="none",
                     help="scene assignment over ranks: none = every rank draws its own scenes (weak scaling, the "
                          "default); lpt = all ranks' scenes drawn from one pool and assigned by point count, "
@@ -400,6 +403,9 @@ def main():
     gsync = dp.GradSync(model, dev, overlap=overlap) if graph_dp else None
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
                                                            {"fused": True, "capturable": use_graph}))
+    # every convolution's split-bf16 weight image of a step in one launch at its start (sparseconvnet.weight_images;
+    # the optimizer's steps invalidate them)
+    wimg = scn.weight_images.enable(model, dev, optimizer=opt) if args.weight_images else None
     cls_loss, _ = LOSS_REGISTRY.get("Classification")
     con_loss, _ = LOSS_REGISTRY.get("TextContrastive")
 
@@ -418,6 +424,8 @@ def main():
     def step(i):
         x, y, _, text = batches[i % len(batches)]
         h0 = time.perf_counter()
+        if wimg is not None:
+            wimg.prepare()
         opt.zero_grad(set_to_none=gsync is None)
         logits, meta = model((x, text), istrain=True)
         h1 = time.perf_counter()
@@ -455,6 +463,8 @@ def main():
 
     def body(i):  # one training step without its prefetch (what a graph captures; N ranks: up to backward)
         x, y, _, text = batches[i % len(batches)]
+        if wimg is not None:
+            wimg.prepare()
         opt.zero_grad(set_to_none=gsync is None)
         logits, meta = model((x, text), istrain=True)
         loss = cls_loss(logits, y)
@@ -473,6 +483,8 @@ def main():
         """Graph of step i, whose metadata is the pending prefetch; returns (graph, metadata it reads, the
         metadata's build event).  Nothing executes here: the kernels run at replay."""
         t = time.perf_counter()
+        if wimg is not None:
+            wimg.build()  # eagerly: images and descriptor table for what the last step added
         ev = scn_meta.prefetch_event(dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(cap_stream):
@@ -671,6 +683,9 @@ def main():
                            f"on the compute stream (capture host time {1e3 * statistics.median(capture_s):.1f} ms "
                            "median, overlapped with the previous step's replay)") if use_graph and capture_s else
                 "eager kernel launches",
+                "weight_images": (f"{len(wimg.entries)} split-bf16 weight images of the convolutions prepared in one "
+                                  "launch at the start of each step (sparseconvnet.weight_images)") if wimg else
+                "each convolution call splits its own weight image",
                 "active_voxels_per_step_rank0": batches[0][2],
                 "levels": stats,
                 "fwd_multiply_adds": macs,

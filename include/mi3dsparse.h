@@ -205,6 +205,27 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
  * msp_wgrad_chunk_preferred: the shapes the library takes it for).
  * Blocks run n_ranges contiguous tile ranges (msp_wgrad_chunk_ranges) per slice; slab holds n_ranges x K x
  * c_in x c_out floats of partial sums, added in range order into dw. */
+/* Per-step split-weight images (round 3).  msp_conv_tile, msp_conv_local and msp_conv_nbr split their fp32
+ * weights into an exact bf16-piece image in the workspace on every call; flip bit 2 (value 4) tells them the
+ * workspace ALREADY holds that image (they skip the split).  msp_conv_weight_image describes the image a call with
+ * these arguments makes (entry 0: msp_conv_tile with tile_rows 128, 1: msp_conv_local, 2: msp_conv_nbr) -- every
+ * field but wt and img, which the caller fills; bytes = the workspace size the call needs.  A training step can
+ * then split every layer's images in ONE launch: msp_split_weight_images over a device array of n descriptors and
+ * their units' exclusive prefix sums unit_start[0..n] (total_units = unit_start[n]), after the weights last
+ * changed and before the convolutions that use them. */
+typedef struct {
+  const float* wt; /* weights as the convolution is called with them */
+  void* img;       /* caller-owned buffer of >= bytes */
+  int64_t units;   /* work items of the image */
+  int64_t bytes;   /* workspace bytes the call needs (image first) */
+  int32_t kind;    /* 1: per-step slices (msp_conv_tile / msp_conv_nbr), 2: lane-ordered (msp_conv_local) */
+  int32_t K, c_in, c_out;
+  int32_t p;    /* kind 1: columns per slice; kind 2: 16-column tiles per block */
+  int32_t wlay; /* 1: wt is [K][c_in][c_out], 0: [K][c_out][c_in] (flip bit 1) */
+} msp_weight_image;
+int msp_conv_weight_image(int entry, int64_t n_rows, int K, int c_in, int c_out, int flip, msp_weight_image* d);
+int msp_split_weight_images(const msp_weight_image* descs, int n, const int64_t* unit_start, int64_t total_units,
+                            msp_stream_t stream);
 int64_t msp_wgrad_chunk_cap(void);
 int msp_wgrad_chunk_ok(int64_t n_rows, int K, int c_in, int c_out);
 int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out);

@@ -2,7 +2,8 @@
 # Interleaved end-to-end A/B on one box: bench.py on the product library (A) and on lib/libmi3dsparse_exp.so
 # (B, scripts/build_exp.sh with EXP_FLAGS), ROUNDS times each, alternating; one JSON line per run in
 # gpurun_out/ab_$TAG.log (prefixed A / B).  B_ENV="VAR=value ..." sets environment variables for the B runs
-# only; B_LIB=0 keeps B on the product library (an environment-only A/B).
+# only; B_LIB=0 keeps B on the product library (an environment-only A/B); B_ARGS: extra bench.py arguments
+# for the B runs.
 set -o pipefail
 TAG=${TAG:-ab}
 ROUNDS=${ROUNDS:-2}
@@ -15,8 +16,9 @@ for i in $(seq 1 $ROUNDS); do
     unset MI3DSPARSE_LIB
     [ $v = B ] && [ "${B_LIB:-1}" = 1 ] && export MI3DSPARSE_LIB=$EXP
     envs=""
-    [ $v = B ] && envs="${B_ENV:-}"
-    env $envs timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 15 --warmup 5} > gpurun_out/ab_${TAG}_$v$i.log 2>&1 || exit $?
+    extra=""
+    [ $v = B ] && envs="${B_ENV:-}" && extra="${B_ARGS:-}"
+    env $envs timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 15 --warmup 5} $extra > gpurun_out/ab_${TAG}_$v$i.log 2>&1 || exit $?
     echo "$v $(grep '^{"metric"' gpurun_out/ab_${TAG}_$v$i.log)" >> gpurun_out/ab_$TAG.log
     python - "$v" gpurun_out/ab_${TAG}_$v$i.log <<'PY'
 import json, sys
