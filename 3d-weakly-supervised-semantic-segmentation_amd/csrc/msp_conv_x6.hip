@@ -375,13 +375,14 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
 // weight sets in registers: the current run's and the next run's, loaded at
 // the current run's first chunk (uniform branches; the chunk values keep
 // their D-deep pipeline across runs).
-template <int NT, int NKK, int D, int NW>
+// TR: output rows per wave tile (128, or 64: half the LDS accumulator tile per wave, so twice the blocks per CU).
+template <int NT, int NKK, int D, int NW, int TR = 128>
 __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
     int64_t n_tiles, int n_y, float* __restrict__ out) {
-  constexpr int NC = 16 * NT, TR = 128;
+  constexpr int NC = 16 * NT;
   constexpr int WU = 3 * 4 * NC;  // 16-byte units of one (offset, k-slice) image
   __shared__ floatx4 lds4[kWaves][TR * NC / 4];
   __shared__ int runs_s[kWaves][128];
@@ -560,6 +561,39 @@ int launch_x6r(const float* x, int c_in, const float* wt, int K, int flip, int c
 
 
 size_t x6p_ws_bytes(int K, int c_in, int c_out) { return (size_t)K * c_out * ((c_in + 31) / 32) * 32 * 6; }
+
+#ifdef MSP_EXPERIMENTS
+// Per-wave form with the tile height and pipeline depth as parameters (scripts/kbench.py, experiments build):
+// variant = 10 * D + (tile_rows == 64); the rulebook must have tile_rows-row tiles.
+int launch_x6r_exp(int variant, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+                   int tile_rows, const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                   const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, hipStream_t s) {
+  const int NT = c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1;
+  const int NKK = (c_in + 31) / 32;
+  const int n_y = c_out / (16 * NT);
+  const int64_t n_tiles = ceil_div(n_rows, tile_rows);
+  u32x4* wimg = static_cast<u32x4*>(ws);
+  const int64_t units = (int64_t)K * c_out * NKK * 32 * 6 / 16;
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, wimg,
+                                                                       (flip >> 1) & 1);
+  flip &= 1;
+  const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
+  const int D = variant / 10, T = variant % 10 == 1 ? 64 : 128;
+  if (T != tile_rows) return MSP_EINVAL;
+#define LE(N, C, DD, TT)                                                                                        \
+  if (NT == N && NKK == C && D == DD && T == TT) {                                                             \
+    conv_x6r_kernel<N, C, DD, 2, TT><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,      \
+                                                               chunk_off, chunk_src, chunk_row, n_rows,        \
+                                                               n_tiles, n_y, out);                             \
+    return MSP_OK;                                                                                             \
+  }
+  LE(2, 1, 3, 128) LE(2, 1, 3, 64) LE(2, 1, 2, 128) LE(2, 1, 2, 64)
+  LE(2, 2, 3, 128) LE(2, 2, 3, 64) LE(2, 2, 2, 64)
+#undef LE
+  set_error("launch_x6r_exp: no variant %d for c_in=%d c_out=%d", variant, c_in, c_out);
+  return MSP_EINVAL;
+}
+#endif
 
 // ---------------------------------------------------------------- dense row groups
 // Submanifold convolutions on large levels, straight from the neighbour map
@@ -1121,5 +1155,19 @@ int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int
   const int rc = launch_x6g(x, c_in, wt, K, flip, c_out, nbr, perm, n_rows, out, ws, as_stream(stream));
   return rc ? rc : check_launch("msp_conv_nbr");
 }
+
+#ifdef MSP_EXPERIMENTS
+int msp_exp_conv_x6r(int variant, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
+                     int tile_rows, const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                     const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                     msp_stream_t stream) {
+  MSP_REQUIRE(c_out <= 32 && c_in <= 64 && c_in % 16 == 0 && c_out % 16 == 0, "msp_exp_conv_x6r: shape");
+  MSP_REQUIRE(ws && ws_bytes >= x6p_ws_bytes(K, c_in, c_out), "msp_exp_conv_x6r: workspace");
+  if (n_rows <= 0) return MSP_OK;
+  const int rc = launch_x6r_exp(variant, x, c_in, wt, K, flip, c_out, tile_rows, tile_start, chunk_off, chunk_src,
+                                chunk_row, n_rows, out, ws, as_stream(stream));
+  return rc ? rc : check_launch("msp_exp_conv_x6r");
+}
+#endif
 
 }  // extern "C"

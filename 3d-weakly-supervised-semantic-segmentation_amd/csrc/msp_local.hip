@@ -952,11 +952,12 @@ int msp_wgrad_chunk_ok(int64_t n_rows, int K, int c_in, int c_out) {
 }
 
 // Measured against the pair lists on the headline batch's rulebooks (scripts/kbench.py, profiles/r03/kbench_r03*.log):
-// ahead for 64+ output channels at every level (level 1 64 -> 64 0.62 vs 0.64 ms, level 4 160 -> 160 0.082 vs
-// 0.107, level 5 192 -> 192 0.041 vs 0.052, level 6 224 -> 224 0.027 vs 0.036); behind at level 0's 32 output
-// channels (32 -> 32 0.36 vs 0.34 ms), which stay on the pair lists.
+// ahead for 64+ output channels at every level (level 1 64 -> 64 0.53 vs 0.58 ms, level 4 160 -> 160 0.082 vs
+// 0.107, level 5 192 -> 192 0.041 vs 0.052, level 6 224 -> 224 0.027 vs 0.036) and, since the products accumulate
+// straight into the tile sums, at level 0's 32 -> 32 (0.327 vs 0.347 ms); behind at 64 -> 32 (0.538 vs 0.522),
+// which stays on the pair lists (profiles/r03/kbench_r03y_level0.log).
 int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out) {
-  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && c_out >= 64 ? 1 : 0;
+  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && (c_out >= 64 || c_in <= c_out) ? 1 : 0;
 }
 
 int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out) {
@@ -1055,8 +1056,10 @@ int msp_split_weight_images(const msp_weight_image* descs, int n, const int64_t*
 // Measured against the gather forms on the headline batch's rulebooks (profiles/r02/kbench_local_r02_levels.log):
 // ahead from 64 channels on both sides and 4096 rows up (levels 1-4 of m = 32: 0-34 % less time), behind on the
 // 32-channel level 0 and on the few-tile levels 5-6 (grids of 16 / 4 tiles).
+// From 64 output channels (and 32+ input channels: the level-0 backward-data 32 -> 64, 0.685 vs 0.711 ms on the
+// dense row groups, profiles/r03/kbench_r03y_level0.log); narrower outputs stay on the per-wave tiles.
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {
-  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 64 && c_out >= 64 && n_rows >= 4096) ? 1 : 0;
+  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 32 && c_out >= 64 && n_rows >= 4096) ? 1 : 0;
 }
 
 size_t msp_conv_local_workspace_size(int K, int c_in, int c_out) {

@@ -85,6 +85,29 @@ def conv_forms(rules, V, cin, cout):
             return f
         for v in [int(t) for t in os.environ.get("EXP_VARIANTS", "0,1").split(",") if t]:
             forms[f"x6s_v{v}"] = exp(v)
+    if hasattr(lib, "msp_exp_conv_x6r") and cout <= 32 and cin <= 64:  # experiments build: per-wave tile variants
+        import ctypes
+        fx = lib.msp_exp_conv_x6r
+        P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        fx.restype = I
+        fx.argtypes = [I, P, I, P, I, I, I, I, P, P, P, P, I64, P, P, ctypes.c_size_t, P]
+
+        def x6r(variant):
+            tr = 64 if variant % 10 == 1 else 128
+
+            def f(x, wt, flip):
+                tl = rules.tiles_for(tr)
+                out = torch.empty(V, cout, device=DEV)
+                wsb = 27 * cout * ((cin + 31) // 32) * 32 * 6
+                ws = torch.empty(max(wsb // 4, 1), device=DEV)
+                rc = fx(variant, ptr(x), cin, ptr(wt), 27, flip, cout, tr, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
+                        ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), ptr(ws), wsb, _lib.stream())
+                if rc:
+                    raise RuntimeError(lib.msp_last_error().decode())
+                return out
+            return f
+        for v in [int(t) for t in os.environ.get("X6R_VARIANTS", "30,31,20,21").split(",") if t]:
+            forms[f"x6r_v{v}"] = x6r(v)
     if hasattr(ops, "conv_unit") and cout <= 64:
         forms["unit"] = lambda x, wt, flip: ops.conv_unit(x, wt, 27, flip, cout, rules, V)
     if FORMS:
