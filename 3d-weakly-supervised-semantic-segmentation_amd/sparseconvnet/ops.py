@@ -175,22 +175,24 @@ def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out, kind="pairs", flops=0):
 
 
 _WGRAD_SIDE = {}
-# True: weight gradients on a side stream beside the backward-data (bench.py --concurrent-wgrad).
-# Off by default: it saved 0.3 ms of 66.9 per step, inside the box-to-box spread, and the
+# True: every weight gradient on a side stream beside the backward-data (bench.py --concurrent-wgrad).
+# Off by default: it saved 0.3 ms of 66.9 per step (round 2, eager), inside the box-to-box spread, and the
 # co-running kernels stretch each other's event-timed durations (the conv roofline reads low).
 WGRAD_CONCURRENT = False
+# Levels below this many rows run their weight gradient beside the backward-data (bench.py --wgrad-side-rows).
+# Off: although neither fills the chip below ~10^4 rows, the graph-captured step measured 54.6-54.8 ms with it
+# at 2^14 rows and 54.6 at 2^16, against 54.2 without (profiles/r03/args_r03_wgrad_side.log).
+WGRAD_SIDE_ROWS = 0
 
 
-def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None, kind="wgrad"):
-    """conv_wgrad on a side stream, ordered after the work already queued on
-    the current stream, so it runs concurrently with the backward-data
-    launched next on the current stream (both are latency-bound gathers at
-    2-3 waves per SIMD; co-running fills the chip).  Returns (dw, join):
-    join() makes the current stream wait for it -- call it before the
-    backward returns, so everything after this autograd node is ordered
-    after the weight gradient as well."""
-    if not WGRAD_CONCURRENT:
-        return conv_wgrad(x, dy, pairs, pin, pout, K, kind, flops=flops), lambda: None
+def _on_side(x, rows, fn):
+    """fn() on a side stream ordered after the work already queued on the current stream, so it runs
+    concurrently with what is launched next on the current stream, when WGRAD_CONCURRENT or the level has
+    fewer than WGRAD_SIDE_ROWS rows; else on the current stream.  Returns (result, join): join() makes the
+    current stream wait for it -- call it before the backward returns, so everything after this autograd node
+    is ordered after it as well."""
+    if not (WGRAD_CONCURRENT or rows < WGRAD_SIDE_ROWS) or not x.is_cuda:
+        return fn(), lambda: None
     dev = x.device
     cur = torch.cuda.current_stream(dev)
     side = _WGRAD_SIDE.get(dev.index)
@@ -198,14 +200,21 @@ def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None, kind="wgrad"):
         side = _WGRAD_SIDE[dev.index] = torch.cuda.Stream(dev)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
-        dw = conv_wgrad(x, dy, pairs, pin, pout, K, kind, flops=flops)
+        out = fn()
         ev = torch.cuda.Event()
         ev.record(side)
 
     def join():
         cur.wait_event(ev)
-        dw.record_stream(cur)
-    return dw, join
+        if out is not None:
+            out.record_stream(cur)
+    return out, join
+
+
+def conv_wgrad_async(x, dy, pairs, pin, pout, K, flops=None, kind="wgrad"):
+    """conv_wgrad beside the backward-data launched next on the current stream (_on_side: both are
+    latency-bound gathers at 2-3 waves per SIMD; co-running fills the chip).  Returns (dw, join)."""
+    return _on_side(x, dy.size(0), lambda: conv_wgrad(x, dy, pairs, pin, pout, K, kind, flops=flops))
 
 
 def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
@@ -312,9 +321,10 @@ class SubmanifoldConvFunction(torch.autograd.Function):
             V = xp.size(0)
             dwp = None
             rules.note_use("wgrad", cin_p, cout_p)
-            if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)):
-                dwp = conv_wgrad_chunk(xp, g, rules, K, flops=2.0 * p.total * cin * cout)
-            if dwp is None:  # pair lists (beside the backward-data when WGRAD_CONCURRENT)
+            if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)) and \
+                    rules.wgrad_index() is not None:
+                dwp, join = _on_side(xp, V, lambda: conv_wgrad_chunk(xp, g, rules, K, flops=2.0 * p.total * cin * cout))
+            if dwp is None:  # pair lists (beside the backward-data on small levels or when WGRAD_CONCURRENT)
                 dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:

@@ -286,7 +286,10 @@ def main():
                          "and the step-level compulsory bytes); 0 = none")
     ap.add_argument("--foreach-adam", action="store_true", help="torch's foreach Adam instead of the fused one")
     ap.add_argument("--concurrent-wgrad", action="store_true",
-                    help="weight gradients on a side stream beside the backward-data (sparseconvnet.ops)")
+                    help="every weight gradient on a side stream beside the backward-data (sparseconvnet.ops)")
+    ap.add_argument("--wgrad-side-rows", type=int, default=None,
+                    help="levels below this many rows run the weight gradient beside the backward-data "
+                         "(sparseconvnet.ops.WGRAD_SIDE_ROWS; 0 = never)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="build each batch's metadata inside its own forward (no side-stream input pipelining)")
     ap.add_argument("--prefetch-at", choices=["end", "fwd"], default="end",
@@ -346,6 +349,8 @@ def main():
     _lib.load()
     from sparseconvnet import ops as scn_ops
     scn_ops.WGRAD_CONCURRENT = bool(args.concurrent_wgrad)
+    if args.wgrad_side_rows is not None:
+        scn_ops.WGRAD_SIDE_ROWS = args.wgrad_side_rows
     # two distinct batches per rank, alternated step to step
     if args.balance == "lpt" and world > 1:
         host_batches = [balanced_batch(args, rank, world, k) for k in range(2)]
