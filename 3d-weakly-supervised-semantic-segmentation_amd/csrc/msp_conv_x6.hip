@@ -1049,6 +1049,9 @@ int launch_wgrad_x6(const float* x, int c_in, const float* dy, int c_out, const 
 // divides) with double-buffered weights.  Small grids split each tile's
 // offsets over up to 8 blocks (partials reduced in split order).  Pipeline
 // depth 2 (3 and 4 measured no faster).
+// Offset split on small grids: aim at 1024 blocks, at most 8 splits; at most 8 tiles (the deepest level, a few
+// hundred rows) 2048 blocks and 16 splits (level 6 224 -> 224 0.038 vs 0.042 ms, 448 -> 224 0.055 vs 0.066; the
+// wider split lost at level 5's 16 tiles, 0.059 vs 0.048: profiles/r03/kbench_r03_split.log).
 PlanX6 plan_x6(int64_t n_rows, int c_out) {
   const int n16 = c_out / 16;
   const int64_t n_tiles = ceil_div(n_rows, 128);
@@ -1066,9 +1069,10 @@ PlanX6 plan_x6(int64_t n_rows, int c_out) {
   }
   p.n_y = n16 / p.nt;
   const int64_t blocks = n_tiles * p.n_y;
-  if (blocks < 1024) {
-    const int64_t sp = (1024 + blocks - 1) / blocks;
-    p.split = (int)(sp > 8 ? 8 : sp);
+  const int64_t target = n_tiles <= 8 ? 2048 : 1024, cap = n_tiles <= 8 ? 16 : 8;
+  if (blocks < target) {
+    const int64_t sp = (target + blocks - 1) / blocks;
+    p.split = (int)(sp > cap ? cap : sp);
   }
   return p;
 }

@@ -1057,9 +1057,12 @@ int msp_split_weight_images(const msp_weight_image* descs, int n, const int64_t*
 // ahead from 64 channels on both sides and 4096 rows up (levels 1-4 of m = 32: 0-34 % less time), behind on the
 // 32-channel level 0 and on the few-tile levels 5-6 (grids of 16 / 4 tiles).
 // From 64 output channels (and 32+ input channels: the level-0 backward-data 32 -> 64, 0.685 vs 0.711 ms on the
-// dense row groups, profiles/r03/kbench_r03y_level0.log); narrower outputs stay on the per-wave tiles.
+// dense row groups, profiles/r03/kbench_r03y_level0.log) and 4096 rows; from 1024 rows when the output is at least
+// twice the input (level 5's backward-data 192 -> 384: 0.063 vs 0.086 ms on the shared tiles,
+// profiles/r03/kbench_r03_split.log).  Narrower outputs stay on the per-wave tiles.
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {
-  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 32 && c_out >= 64 && n_rows >= 4096) ? 1 : 0;
+  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 32 && c_out >= 64 &&
+          (n_rows >= 4096 || (n_rows >= 1024 && c_out >= 2 * c_in))) ? 1 : 0;
 }
 
 size_t msp_conv_local_workspace_size(int K, int c_in, int c_out) {
