@@ -568,14 +568,37 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
   }
 }
 
-// dW[e] = sum over ranges in order of slab[range][e]
+// dW[e] = sum of slab[range][e] over the ranges: 16 consecutive runs of ranges, each added in range order by one
+// thread (eight loads in flight), then the 16 run sums in run order (deterministic).  Block = 16 float4 elements x
+// 16 runs: the slab (256 ranges x K c_in c_out floats, 28 MB at every shape) is read with 16x the loads in flight
+// of one thread per element walking all ranges (a latency-bound 17 us per call, 0.8 ms per step).
+constexpr int kRRuns = 16;
 __global__ __launch_bounds__(256) void wgrad_ranges_reduce_kernel(const floatx4* __restrict__ slab, int n_ranges,
                                                                   int64_t n4, floatx4* __restrict__ dw) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n4) return;
-  floatx4 s = slab[i];
-  for (int k = 1; k < n_ranges; ++k) s += slab[(int64_t)k * n4 + i];
-  dw[i] = s;
+  __shared__ floatx4 part[kRRuns][16];
+  const int el = threadIdx.x & 15, run = threadIdx.x >> 4;
+  const int64_t i = (int64_t)blockIdx.x * 16 + el;
+  const int k0 = n_ranges * run / kRRuns, k1 = n_ranges * (run + 1) / kRRuns;
+  floatx4 s = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    int k = k0;
+    for (; k + 8 <= k1; k += 8) {
+      floatx4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(int64_t)(k + u) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < k1; ++k) s += slab[(int64_t)k * n4 + i];
+  }
+  part[run][el] = s;
+  __syncthreads();
+  if (run == 0 && i < n4) {
+    floatx4 t = part[0][el];
+#pragma unroll
+    for (int r = 1; r < kRRuns; ++r) t += part[r][el];
+    dw[i] = t;
+  }
 }
 
 // ---------------------------------------------------------------- chunk-local weight gradient
@@ -953,11 +976,16 @@ int msp_wgrad_chunk_ok(int64_t n_rows, int K, int c_in, int c_out) {
 
 // Measured against the pair lists on the headline batch's rulebooks (scripts/kbench.py, profiles/r03/kbench_r03*.log):
 // ahead for 64+ output channels at every level (level 1 64 -> 64 0.53 vs 0.58 ms, level 4 160 -> 160 0.082 vs
-// 0.107, level 5 192 -> 192 0.041 vs 0.052, level 6 224 -> 224 0.027 vs 0.036) and, since the products accumulate
-// straight into the tile sums, at level 0's 32 -> 32 (0.327 vs 0.347 ms); behind at 64 -> 32 (0.538 vs 0.522),
-// which stays on the pair lists (profiles/r03/kbench_r03y_level0.log).
+// 0.107, level 5 192 -> 192 0.041 vs 0.052, level 6 224 -> 224 0.027 vs 0.036).  Level 0's 32 -> 32 is ahead too
+// in isolation since the products accumulate straight into the tile sums (0.327 vs 0.347 ms,
+// profiles/r03/kbench_r03y_level0.log) but needs level 0's tile-local rulebook (see msp_conv_local_preferred):
+// 32 output channels stay on the pair lists.
+#ifndef MSP_CHUNK_NARROW  // experiments build: -DMSP_CHUNK_NARROW=1 takes c_in <= c_out = 32 too
+#define MSP_CHUNK_NARROW 0
+#endif
 int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out) {
-  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && (c_out >= 64 || c_in <= c_out) ? 1 : 0;
+  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && (c_out >= 64 || (MSP_CHUNK_NARROW && c_in <= c_out)) ? 1
+                                                                                                             : 0;
 }
 
 int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out) {
@@ -1000,7 +1028,7 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
                                                                     chunk_lr, u_start, u_rows, n_rows, n_tiles,
                                                                     (int)n_ranges, slab);
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
-  wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
+  wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 16), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
                                                                          (int)n_ranges, n4,
                                                                          reinterpret_cast<floatx4*>(dw));
   return check_launch("msp_conv_wgrad_chunk");
@@ -1056,12 +1084,16 @@ int msp_split_weight_images(const msp_weight_image* descs, int n, const int64_t*
 // Measured against the gather forms on the headline batch's rulebooks (profiles/r02/kbench_local_r02_levels.log):
 // ahead from 64 channels on both sides and 4096 rows up (levels 1-4 of m = 32: 0-34 % less time), behind on the
 // 32-channel level 0 and on the few-tile levels 5-6 (grids of 16 / 4 tiles).
-// From 64 output channels (and 32+ input channels: the level-0 backward-data 32 -> 64, 0.685 vs 0.711 ms on the
-// dense row groups, profiles/r03/kbench_r03y_level0.log) and 4096 rows; from 1024 rows when the output is at least
-// twice the input (level 5's backward-data 192 -> 384: 0.063 vs 0.086 ms on the shared tiles,
-// profiles/r03/kbench_r03_split.log).  Narrower outputs stay on the per-wave tiles.
+// From 64 channels on both sides and 4096 rows; from 1024 rows when the output is at least twice the input (level
+// 5's backward-data 192 -> 384: 0.063 vs 0.086 ms on the shared tiles, profiles/r03/kbench_r03_split.log).  Level
+// 0's 32 -> 64 backward-data is faster here in isolation (0.685 vs 0.711 ms, profiles/r03/kbench_r03y_level0.log),
+// but it needs level 0's tile-local rulebook, whose side-stream build cost more than that: 57.1 vs 56.7 ms/step
+// with MSP_LOCAL_MIN_CIN 32 and MSP_CHUNK_NARROW 1 (profiles/r03/ab_r03_level0_local.log).
+#ifndef MSP_LOCAL_MIN_CIN  // experiments build: -DMSP_LOCAL_MIN_CIN=32 takes level 0's 32 -> 64
+#define MSP_LOCAL_MIN_CIN 64
+#endif
 int msp_conv_local_preferred(int64_t n_rows, int c_in, int c_out) {
-  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= 32 && c_out >= 64 &&
+  return (c_in % 16 == 0 && c_out % 16 == 0 && c_in >= MSP_LOCAL_MIN_CIN && c_out >= 64 &&
           (n_rows >= 4096 || (n_rows >= 1024 && c_out >= 2 * c_in))) ? 1 : 0;
 }
 
@@ -1158,7 +1190,7 @@ int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, 
     return MSP_EINVAL;
   }
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
-  wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 256), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
+  wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 16), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
                                                                          (int)n_ranges, n4,
                                                                          reinterpret_cast<floatx4*>(dw));
   return check_launch("msp_exp_wgrad_chunk");

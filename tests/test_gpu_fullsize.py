@@ -1,10 +1,10 @@
 """Full-size parity of the benchmarked networks (BASELINE.json configs[1] and configs[2] shapes at 2 cm,
 whole synthetic scenes): the HIP path against the fp64 CPU oracle with shared ReLU decisions
-(oracle/parity.py), at the sizes where the production kernel selections take over -- the tile-local
-convolution (msp_conv_local, 64+ output channels from 4096 rows: levels 1-4 and level 0's 32 -> 64
-backward-data), the NetworkInNetwork kernel (msp_nin_gemm), the per-wave split-bf16 tile at level 0
-(conv_x6r) and the chunk-local weight gradient (msp_conv_wgrad_chunk: c_out >= 64, and level 0's 32 x 32)
-beside the pair-list one (level 0's 64 x 32).  The test records which forms ran
+(oracle/parity.py), at the sizes where the production kernel selections take over -- the dense row-group
+convolution (msp_conv_nbr, >= 1e5 rows and c_out >= 64: level 0's 32 -> 64 backward-data), the tile-local
+convolution (msp_conv_local, 64+ channels from 4096 rows: levels 1-4), the NetworkInNetwork kernel
+(msp_nin_gemm), the per-wave split-bf16 tile at level 0 (conv_x6r) and the chunk-local weight gradient
+(msp_conv_wgrad_chunk, c_out >= 64) beside the pair-list one.  The test records which forms ran
 (through the same hook bench.py times them with) and requires each to have fired.
 
 Bars (tests/test_gpu_encoders.py explains them): per-point and scene features within 1e-4 of
@@ -96,7 +96,7 @@ def test_headline_unet_full_size_parity():
     """configs[2] network (SparseConvUNet m=32, block_reps=2, residual) on two whole scenes at 2 cm:
     level 0 >= 2^18 voxels (fp32 NIN form, split form below), level 1 >= 1e5 (dense row groups)."""
     kinds = _run("SparseConvUNet", 32, 2, True, 2,
-                 need=["subm_fwd/x6r", "subm_fwd/x6s", "subm_bwd_data/x6s", "subm_fwd/x6d",
+                 need=["subm_fwd/x6r", "subm_fwd/x6s", "subm_bwd_data/x6s", "subm_bwd_data/x6g", "subm_fwd/x6d",
                        "nin_fwd/f32", "nin_bwd_data/f32", "nin_fwd/x6", "nin_bwd_data/x6", "wgrad/x6", "wgrad/x6c", "nin_wgrad/x6", "conv_fwd/x6d",
                        "deconv_fwd/f32", "subm_fwd/f32n", "wgrad/f32n"])
     assert kinds["subm_fwd/x6s"] >= 4
