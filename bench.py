@@ -287,6 +287,8 @@ def main():
     ap.add_argument("--foreach-adam", action="store_true", help="torch's foreach Adam instead of the fused one")
     ap.add_argument("--concurrent-wgrad", action="store_true",
                     help="every weight gradient on a side stream beside the backward-data (sparseconvnet.ops)")
+    ap.add_argument("--compute-priority", type=int, choices=[0, 1], default=0,
+                    help="1: run the step on a high-priority stream (the metadata prefetch keeps the default one)")
     ap.add_argument("--wgrad-side-rows", type=int, default=None,
                     help="levels below this many rows run the weight gradient beside the backward-data "
                          "(sparseconvnet.ops.WGRAD_SIDE_ROWS; 0 = never)")
@@ -340,6 +342,11 @@ def main():
     if rank == 0 and world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
               file=sys.stderr)
+
+    if args.compute_priority:
+        # the step's kernels on a high-priority stream: the metadata prefetch (side stream, default priority)
+        # gets the CUs the step leaves idle instead of competing for them
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
 
     import sparseconvnet as scn
     from sparseconvnet import _lib
