@@ -25,6 +25,8 @@ from __future__ import annotations
 
 import os
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -147,7 +149,7 @@ class GradSync:
             # broadcast above ran first
             warm = torch.zeros(1, device=device, dtype=torch.float32)
             dist.all_reduce(warm)
-            torch.cuda.synchronize(device)
+            settle(device)
         if self.overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -210,6 +212,18 @@ class GradSync:
             dist.all_reduce(self.flat)
         if self.world > 1:
             self.flat.mul_(1.0 / self.world)
+
+
+def settle(device=None):
+    """Call after an eager collective and before a graph capture that issues collectives.  ProcessGroupNCCL's
+    watchdog thread polls the events of every eager collective until it has seen it complete (one pass per
+    ~100 ms); a poll that lands while the communicator's stream is capturing fails with hipErrorCapturedEvent and
+    the watchdog terminates the process (seen intermittently right after the communicator warm-up).  Waiting for
+    the device and a few of its passes lets it retire the eager work first."""
+    if not (dist.is_initialized() and dist.get_backend() == "nccl"):
+        return
+    torch.cuda.synchronize(device)
+    time.sleep(0.35)
 
 
 def max_over_ranks(x: float) -> float:

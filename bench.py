@@ -543,6 +543,8 @@ def main():
         entry = capture(0)
     if world > 1:
         dist.barrier()
+        if graph_dp:
+            dp.settle(dev)  # the barrier's work retired by the watchdog before the loop captures collectives
     torch.cuda.synchronize()
     rec.active = True
     # step boundaries on the compute stream: device time per step (median reported beside the mean)
