@@ -378,30 +378,45 @@ def test_conv_nbr_accuracy(cin, cout, flip):
 
 
 def test_subm_conv_large_level_uses_nbr_form():
-    """A level above the dense-form threshold (>= 10^5 rows) runs the module
-    forward and backward-data through msp_conv_nbr; both match an fp64
-    evaluation from the neighbour map (1e-5 of scale), and the weight gradient
-    matches too."""
+    """A level above the dense-form threshold (>= 10^5 rows) with 32 -> 64 channels (level 0's decoder shape,
+    below the tile-local form's 64 input channels) runs the module forward through msp_conv_nbr (the recorded
+    kind says so) and the backward-data 64 -> 32 through the per-wave tiles; output, input gradient and weight
+    gradient match an fp64 evaluation from the neighbour map (1e-5 of scale)."""
     from sparseconvnet import _lib
     b = make_batch(1, 50, seed=5)
     coords = torch.from_numpy(b["coords"]).to(DEV)
     feats = torch.from_numpy(b["feats"]).to(DEV)
     t = scn.InputLayer(3, 4096, mode=4)([coords, feats])
     V = t.features.size(0)
-    assert V >= 100000 and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(V), 64, 64))
+    assert V >= 100000 and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(V), 32, 64))
+    assert not int(_lib.query("msp_conv_local_preferred", _lib.I64(V), 32, 64))
     torch.manual_seed(3)
-    x = torch.randn(V, 64, device=DEV, requires_grad=True)
+    x = torch.randn(V, 32, device=DEV, requires_grad=True)
     t.features = x
-    conv = scn.SubmanifoldConvolution(3, 64, 64, 3, False).to(DEV)
-    y = conv(t).features
-    gy = torch.randn_like(y)
-    y.backward(gy)
+
+    class Kinds:
+        def __init__(self):
+            self.kinds = set()
+
+        def run(self, kind, flops, fn, nbytes=0):
+            self.kinds.add(kind.split("[")[0])
+            return fn()
+    rec = Kinds()
+    conv = scn.SubmanifoldConvolution(3, 32, 64, 3, False).to(DEV)
+    _lib.set_recorder(rec)
+    try:
+        y = conv(t).features
+        gy = torch.randn_like(y)
+        y.backward(gy)
+    finally:
+        _lib.set_recorder(None)
+    assert "subm_fwd/x6g" in rec.kinds, rec.kinds
     nb = t.metadata.level(4096).subm_rules(3).nbr.long()
-    w = conv.weight.detach().double().reshape(27, 64, 64)  # [K][c_in][c_out]
-    x64 = torch.cat([x.detach().double(), torch.zeros(1, 64, dtype=torch.float64, device=DEV)])
+    w = conv.weight.detach().double().reshape(27, 32, 64)  # [K][c_in][c_out]
+    x64 = torch.cat([x.detach().double(), torch.zeros(1, 32, dtype=torch.float64, device=DEV)])
     ref = torch.zeros(V, 64, dtype=torch.float64, device=DEV)
-    dx = torch.zeros(V + 1, 64, dtype=torch.float64, device=DEV)
-    dw = torch.zeros(27, 64, 64, dtype=torch.float64, device=DEV)
+    dx = torch.zeros(V + 1, 32, dtype=torch.float64, device=DEV)
+    dw = torch.zeros(27, 32, 64, dtype=torch.float64, device=DEV)
     g64 = gy.double()
     for o in range(27):
         src = torch.where(nb[o] >= 0, nb[o], V)
@@ -409,8 +424,8 @@ def test_subm_conv_large_level_uses_nbr_form():
         dx.index_add_(0, src, g64 @ w[o].t())
         dw[o] = x64[src].t() @ g64
     close(y, ref, 1e-5, "nbr fwd")
-    close(x.grad, dx[:V], 1e-5, "nbr bwd-data")
-    close(conv.weight.grad.reshape(27, 64, 64), dw, 1e-5, "nbr dW")
+    close(x.grad, dx[:V], 1e-5, "bwd-data")
+    close(conv.weight.grad.reshape(27, 32, 64), dw, 1e-5, "dW")
 
 
 @pytest.mark.parametrize("cin,cout,nbr_form", [(32, 32, False), (64, 32, False), (64, 64, False), (96, 192, False),
