@@ -689,7 +689,10 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
 
 // AC as conv_x6s: 1 (the product form) accumulates the six piece products straight into the running tile sums,
 // 0 sums each step in a zeroed accumulator first (12-16 % slower, profiles/r03/kbexp_r03x_accumulate.log).
-template <int NW, int AC = 1>
+// PW 1 (the product form): the next k-step's rule words are read from LDS at the start of the current one (within
+// an offset), so a k-step no longer opens with an LDS read -> address -> transposing-read chain: 1-6 % faster at
+// levels 0-3 (profiles/r03/kbexp_r03pw.log); PW 0 reads them at the k-step's start.
+template <int NW, int AC = 1, int PW = 1>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -806,25 +809,39 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
 
   // ---- one 32-rule step over the two chunks cA, cA + 1 (the second only if hasB): the B fragments (dy) of
   // both 16-column halves, then per 16-row half of x its A fragments and 12 MFMAs (36 fragment registers live)
-  auto rows_of = [&](int cA, bool hasB, int (&xr)[2], int (&dr)[2]) {
+  auto words_of = [&](int cA, uint32_t (&wd)[2]) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int kp = 8 * g + 4 * h + qq, cs = kp >> 4;
-      uint32_t w = ent[(cA + cs) * 16 + (kp & 15)];
+      wd[h] = ent[(cA + cs) * 16 + (kp & 15)];
+    }
+  };
+  auto rows_from = [&](const uint32_t (&wd)[2], bool hasB, int (&xr)[2], int (&dr)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kp = 8 * g + 4 * h + qq, cs = kp >> 4;
+      uint32_t w = wd[h];
       if (cs == 1 && !hasB) w = (uint32_t)kWCap | ((uint32_t)kWTile << 16);
       const int ls = (int)(w & 0xFFFFu);
       xr[h] = ls < kWCap ? ls : kWCap;
       dr[h] = (int)(w >> 16);
     }
   };
+  auto rows_of = [&](int cA, bool hasB, int (&xr)[2], int (&dr)[2]) {
+    uint32_t wd[2];
+    words_of(cA, wd);
+    rows_from(wd, hasB, xr, dr);
+  };
   auto frag = [&](const uint16_t* img, const int (&rr)[2], int v) {
     const uint2 lo = tr_read(img + wimg_off(rr[0], v));
     const uint2 hi = tr_read(img + wimg_off(rr[1], v));
     return u32x4{lo.x, lo.y, hi.x, hi.y};
   };
+  uint32_t wcur[2] = {0u, 0u}, wnxt[2] = {0u, 0u};  // PW: this and the next k-step's rule words
   auto kstep = [&](int cA, bool hasB, floatx4 (&ac)[2][2]) {
     int xr[2], dr[2];
-    rows_of(cA, hasB, xr, dr);
+    if constexpr (PW) rows_from(wcur, hasB, xr, dr);
+    else rows_of(cA, hasB, xr, dr);
     u32x4 fb[2][3], fa[3];
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
@@ -880,6 +897,15 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       for (int a = 0; a < NOW; ++a) {  // constant slot index: acc[a] stays in registers
         for (int c = first[a]; c < endc[a]; c += 2, ++s) {
           if (s == s_vals && more) issue_vals(t + 1);
+          if constexpr (PW) {
+            if (c == first[a]) {
+              words_of(c, wcur);
+            } else {
+              wcur[0] = wnxt[0];
+              wcur[1] = wnxt[1];
+            }
+            if (c + 2 < endc[a]) words_of(c + 2, wnxt);
+          }
           kstep(c, c + 1 < endc[a], acc[a]);
         }
       }
@@ -1179,11 +1205,14 @@ int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, 
   const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
   const unsigned grid = (unsigned)(n_ranges * slices);
   if (variant == 0)
-    wgrad_x6c_kernel<8, 0><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
+    wgrad_x6c_kernel<8, 0, 0><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
                                                 u_rows, n_rows, n_tiles, (int)n_ranges, slab);
   else if (variant == 1)
-    wgrad_x6c_kernel<8, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
+    wgrad_x6c_kernel<8, 1, 0><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
                                                 u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  else if (variant == 3)
+    wgrad_x6c_kernel<8, 1, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
+                                                   u_rows, n_rows, n_tiles, (int)n_ranges, slab);
 
   else {
     set_error("msp_exp_wgrad_chunk: no variant %d", variant);
