@@ -52,11 +52,14 @@ struct BnStats {
 // MODE 2: residual join fused with the statistics of its output: x = a,
 // dy = b, sum = a + b is written to sum_out and reduced as in MODE 0 (same
 // partition and order as msp_bn_stats on the sum: identical partials).
+// MODE 3: channel join (SCN JoinTable) fused with the statistics of its
+// output: x = a [V][ca], dy = b [V][C - ca], the row [a | b] is written to
+// sum_out [V][C] and reduced as in MODE 0 (identical partials again).
 template <int MODE>
 __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                         int64_t V, int C, const float* __restrict__ stats,
                                                         float leak, double* __restrict__ partial,
-                                                        float* __restrict__ sum_out = nullptr) {
+                                                        float* __restrict__ sum_out = nullptr, int ca = 0) {
   __shared__ double red[kT][8];
   const int64_t P = gridDim.x;
   const int64_t per = (V + P - 1) / P;
@@ -104,7 +107,34 @@ __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict_
       s4[e] = sm;
       return sm;
     };
+    // MODE 3: the column's source (a or b) is fixed per thread
+    const int ca4 = ca >> 2, cb4 = C4 - ca4;
+    const bool from_a = c4 < ca4;
+    const float4* src4 = from_a ? x4 : g4;
+    const int sc4 = from_a ? ca4 : cb4, soff = from_a ? c4 : c4 - ca4;
+    auto cat = [&](int64_t v) {
+      const float4 e = src4[v * sc4 + soff];
+      s4[v * C4 + c4] = e;
+      return e;
+    };
     int64_t v = v0 + ro;
+    if (MODE == 3) {
+      for (; v + 3 * R < v1; v += 4 * R) {
+        float4 e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = src4[(v + u * R) * sc4 + soff];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s4[(v + u * R) * C4 + c4] = e[u];
+          term(e[u], e[u]);
+        }
+      }
+      for (; v < v1; v += R) {
+        const float4 e = cat(v);
+        term(e, e);
+      }
+    }
+    if (MODE != 3) {
     for (; v + 3 * R < v1; v += 4 * R) {
       float4 xa[4], ga[4];
 #pragma unroll
@@ -129,6 +159,7 @@ __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict_
       } else {
         term(x4[v * C4 + c4], MODE == 1 ? g4[v * C4 + c4] : x4[v * C4 + c4]);
       }
+    }
     }
   }
 #pragma unroll
@@ -401,6 +432,49 @@ inline unsigned rows_grid(int64_t V, int C) {
   return (unsigned)(g < 1 ? 1 : g);
 }
 
+// [a | b] rows (JoinTable) and the inverse split of a gradient (its backward), element per thread
+__global__ __launch_bounds__(kT) void join_cols_kernel(const float* __restrict__ a, int ca,
+                                                       const float* __restrict__ b, int cb, int64_t V,
+                                                       float* __restrict__ out) {
+  const int C = ca + cb;
+  const int64_t n = V * C, stride = (int64_t)gridDim.x * kT;
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
+    const int64_t v = i / C;
+    const int c = (int)(i - v * C);
+    out[i] = c < ca ? a[v * ca + c] : b[v * cb + (c - ca)];
+  }
+}
+
+__global__ __launch_bounds__(kT) void split_cols_kernel(const float* __restrict__ in, int64_t V, int ca, int cb,
+                                                        float* __restrict__ a, float* __restrict__ b) {
+  const int C = ca + cb;
+  const int64_t n = V * C, stride = (int64_t)gridDim.x * kT;
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
+    const int64_t v = i / C;
+    const int c = (int)(i - v * C);
+    if (c < ca) {
+      if (a) a[v * ca + c] = in[i];
+    } else if (b) {
+      b[v * cb + (c - ca)] = in[i];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kT) void split_cols4_kernel(const float4* __restrict__ in, int64_t V, int ca4, int cb4,
+                                                         float4* __restrict__ a, float4* __restrict__ b) {
+  const int C4 = ca4 + cb4;
+  const int64_t n = V * C4, stride = (int64_t)gridDim.x * kT;
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
+    const int64_t v = i / C4;
+    const int c = (int)(i - v * C4);
+    if (c < ca4) {
+      if (a) a[v * ca4 + c] = in[i];
+    } else if (b) {
+      b[v * cb4 + (c - ca4)] = in[i];
+    }
+  }
+}
+
 __global__ __launch_bounds__(kT) void add_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
                                                  float* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * kT;
@@ -490,6 +564,39 @@ int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const do
                      msp_stream_t stream) {
   return msp_bn_bwd_apply_add(x, dy, V, C, partial, stats, weight, leak, train, nullptr, dx, dweight, dbias,
                               stream);
+}
+
+int msp_join_cols(const float* a, int ca, const float* b, int cb, int64_t V, float* out, double* partial,
+                  msp_stream_t stream) {
+  const int C = ca + cb;
+  MSP_REQUIRE(ca > 0 && cb > 0 && C <= 4096 && V >= 0, "msp_join_cols: bad shape (ca=%d cb=%d)", ca, cb);
+  MSP_REQUIRE((out != a && out != b) || V == 0, "msp_join_cols: out must not alias an input");
+  hipStream_t s = as_stream(stream);
+  if (partial && ca % 4 == 0 && cb % 4 == 0 && C <= 4 * kT && aligned16(a) && aligned16(b) && aligned16(out)) {
+    bn_reduce4_kernel<3><<<(unsigned)bn_parts(V, C), kT, 0, s>>>(a, b, V, C, nullptr, 0.f, partial, out, ca);
+    return check_launch("msp_join_cols");
+  }
+  if (V > 0) join_cols_kernel<<<ew_grid(V * C), kT, 0, s>>>(a, ca, b, cb, V, out);
+  if (partial) {
+    if (C % 4 == 0 && C <= 4 * kT && aligned16(out))
+      bn_reduce4_kernel<0><<<(unsigned)bn_parts(V, C), kT, 0, s>>>(out, nullptr, V, C, nullptr, 0.f, partial);
+    else
+      bn_reduce_kernel<0><<<(unsigned)bn_parts(V, C), kT, 0, s>>>(out, nullptr, V, C, nullptr, 0.f, partial);
+  }
+  return check_launch("msp_join_cols");
+}
+
+int msp_split_cols(const float* in, int64_t V, int ca, int cb, float* a, float* b, msp_stream_t stream) {
+  MSP_REQUIRE(ca > 0 && cb > 0 && V >= 0, "msp_split_cols: bad shape (ca=%d cb=%d)", ca, cb);
+  if (V == 0 || (!a && !b)) return MSP_OK;
+  hipStream_t s = as_stream(stream);
+  const int C = ca + cb;
+  if (ca % 4 == 0 && cb % 4 == 0 && aligned16(in) && (!a || aligned16(a)) && (!b || aligned16(b)))
+    split_cols4_kernel<<<ew_grid(V * (C / 4)), kT, 0, s>>>(reinterpret_cast<const float4*>(in), V, ca / 4, cb / 4,
+                                                            reinterpret_cast<float4*>(a), reinterpret_cast<float4*>(b));
+  else
+    split_cols_kernel<<<ew_grid(V * C), kT, 0, s>>>(in, V, ca, cb, a, b);
+  return check_launch("msp_split_cols");
 }
 
 int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,

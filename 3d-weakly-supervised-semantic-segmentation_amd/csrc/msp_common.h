@@ -44,6 +44,16 @@ inline int check_launch(const char* what) {
 
 inline hipStream_t as_stream(msp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---- per-device caches (the library's only process-wide state; include/mi3dsparse.h) -----------------------
+// Both are indexed by the current device and held in atomics: several host threads and several devices may call
+// the library concurrently.  device_cu_count(): the current device's CU count, read once per device.
+// raise_lds_limit(): hipFuncSetAttribute(MaxDynamicSharedMemorySize) for kernel `slot` (a small integer per
+// kernel, < 64) on the current device, once per (device, slot); the attribute is idempotent, so two threads
+// racing to set it are harmless.
+int device_cu_count();
+int raise_lds_limit(const void* fn, int bytes, int slot, const char* what);
+enum LdsSlot { kLdsNinF32 = 0, kLdsNinX6 = 8 };  // + template variant (NTT 1..8 / NT 1..2)
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ---- Morton (Z-order) keys -------------------------------------------------

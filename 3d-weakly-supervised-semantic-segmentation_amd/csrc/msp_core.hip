@@ -2,11 +2,36 @@
 // compaction in the library (voxel dedup, rulebooks, pair lists) is built on.
 #include "msp_common.h"
 
+#include <atomic>
 #include <cstring>
 
 namespace msp {
 
 static thread_local char g_err[512] = "";
+
+constexpr int kMaxDevices = 64;
+static std::atomic<int> g_cus[kMaxDevices];
+static std::atomic<unsigned long long> g_lds_raised[kMaxDevices];
+
+int device_cu_count() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+  int n = g_cus[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  g_cus[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
+
+int raise_lds_limit(const void* fn, int bytes, int slot, const char* what) {
+  int dev = 0;
+  MSP_HIP(hipGetDevice(&dev), what);
+  const unsigned long long bit = 1ull << (slot & 63);
+  if (dev >= 0 && dev < kMaxDevices && (g_lds_raised[dev].load(std::memory_order_acquire) & bit)) return MSP_OK;
+  MSP_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes), what);
+  if (dev >= 0 && dev < kMaxDevices) g_lds_raised[dev].fetch_or(bit, std::memory_order_acq_rel);
+  return MSP_OK;
+}
 
 void set_error(const char* fmt, ...) {
   va_list ap;

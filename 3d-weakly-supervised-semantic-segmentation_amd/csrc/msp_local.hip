@@ -932,16 +932,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
 
 inline int local_nt(int c_out) { return (c_out / 16) % 2 == 0 ? 2 : 1; }
 
-inline int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
+inline int cu_count() { return device_cu_count(); }
 
 }  // namespace msp
 

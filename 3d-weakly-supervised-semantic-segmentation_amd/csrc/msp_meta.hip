@@ -7,8 +7,6 @@
 // per call.  Here everything stays in HBM.
 #include "msp_common.h"
 
-#include <rocprim/device/device_radix_sort.hpp>
-
 namespace msp {
 
 constexpr int kThreads = 256;
@@ -416,25 +414,6 @@ int msp_batch_starts(const int64_t* coords, int64_t n, int64_t row_stride, int64
   return check_launch("msp_batch_starts");
 }
 
-size_t msp_sort_workspace_size(int64_t n, int end_bit) {
-  size_t bytes = 0;
-  (void)rocprim::radix_sort_pairs((void*)nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                            (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0u, (unsigned)end_bit);
-  return bytes;
-}
-
-int msp_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* vals_in, int32_t* vals_out,
-                   int64_t n, int end_bit, void* ws, size_t ws_bytes, msp_stream_t stream) {
-  MSP_REQUIRE(end_bit > 0 && end_bit <= 64, "msp_sort_pairs: bad end_bit %d", end_bit);
-  if (n == 0) return MSP_OK;
-  size_t need = msp_sort_workspace_size(n, end_bit);
-  MSP_REQUIRE(ws_bytes >= need, "msp_sort_pairs: workspace too small (%zu < %zu)", ws_bytes, need);
-  MSP_HIP(rocprim::radix_sort_pairs(ws, need, keys_in, keys_out, vals_in, vals_out, (size_t)n, 0u,
-                                    (unsigned)end_bit, as_stream(stream)),
-          "msp_sort_pairs");
-  return MSP_OK;
-}
-
 // ---------------------------------------------------------------- dense row order
 // Row order for the dense row-group convolution (msp_conv_nbr): inside each
 // window of 2^lw consecutive rows (spatially compact in key order), rows are
@@ -494,9 +473,8 @@ int msp_dense_order(const int32_t* nbr, int K, int64_t n, int log2_window, int32
   const int end_bit = dense_order_bits(n, K, log2_window);
   const unsigned nb = (unsigned)ceil_div(n, 256);
   dense_keys_kernel<<<nb, 256, 0, s>>>(nbr, K, n, log2_window, k_in, v_in);
-  size_t sbytes = msp_sort_workspace_size(n, end_bit);
-  MSP_HIP(rocprim::radix_sort_pairs(sws, sbytes, k_in, k_out, v_in, perm, (size_t)n, 0u, (unsigned)end_bit, s),
-          "msp_dense_order");
+  const int rc = msp_sort_pairs(k_in, k_out, v_in, perm, n, end_bit, sws, msp_sort_workspace_size(n, end_bit), stream);
+  if (rc) return rc;
   permute_map_kernel<<<nb, 256, 0, s>>>(nbr, K, n, perm, nbr_perm);
   return check_launch("msp_dense_order");
 }

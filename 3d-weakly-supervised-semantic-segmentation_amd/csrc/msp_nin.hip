@@ -234,13 +234,10 @@ int nin_ntt(int K, int N) {  // largest column-tile count <= 8 dividing N / 16 w
 
 template <int NTT>
 int launch_f32(const float* A, int64_t M, int K, const float* B, int N, float* C, hipStream_t s) {
-  static bool attr_set = false;  // dynamic LDS above the 64 KiB default
-  if (!attr_set) {
-    MSP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&nin_f32_kernel<NTT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kF32Lds),
-            "msp_nin_gemm: LDS attribute");
-    attr_set = true;
-  }
+  // dynamic LDS above the 64 KiB default, once per device
+  int rc = raise_lds_limit(reinterpret_cast<const void*>(&nin_f32_kernel<NTT>), (int)kF32Lds, kLdsNinF32 + NTT - 1,
+                           "msp_nin_gemm: LDS attribute");
+  if (rc) return rc;
   const size_t lds = nin_lds(K, NTT);
   const int n_chunks = N / (16 * NTT);
   const int64_t groups = (M + 15) / 16;
@@ -261,13 +258,9 @@ inline int nin_nt(int K, int N) {  // two 16-column tiles per slice unless N is 
 
 template <int NT>
 int launch_nin(const float* A, int64_t M, int K, const u32x4* img, int N, float* C, hipStream_t s) {
-  static bool attr_set = false;  // dynamic LDS above the 64 KiB default
-  if (!attr_set) {
-    MSP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&nin_x6_kernel<NT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNinLds),
-            "msp_nin_gemm: LDS attribute");
-    attr_set = true;
-  }
+  int rc = raise_lds_limit(reinterpret_cast<const void*>(&nin_x6_kernel<NT>), (int)kNinLds, kLdsNinX6 + NT - 1,
+                           "msp_nin_gemm: LDS attribute");
+  if (rc) return rc;
   const int n_y = N / (16 * NT), nks = (K + 31) / 32;
   const size_t lds = (size_t)nks * NT * 3 * 1024;
   const int64_t groups = (M + 31) / 32;

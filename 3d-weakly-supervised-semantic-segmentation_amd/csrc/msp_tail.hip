@@ -130,6 +130,68 @@ __global__ __launch_bounds__(kTT) void scene_mean_bwd_kernel(const float* __rest
 
 inline int64_t n_pieces_bound(int64_t V, int B) { return (V + kPiece - 1) / kPiece + B; }
 
+// ---------------------------------------------------------------- eval tail
+// Per-point logits of the head's Linear (models/MultiLabelContrastive.py:43-45, 84-101; train.py:106):
+// the Linear commutes with the OutputLayer's gather, so it runs on the level-0 voxel rows ((V, C) -> (V, ld)
+// on msp_nin_gemm) and each point gathers C_out columns of its voxel's row plus the bias.  Thread per output
+// element: the (N, C_out) writes are coalesced, the gathered rows hit L2 (points of a voxel are adjacent).
+__global__ __launch_bounds__(kTT) void point_rows_bias_kernel(const float* __restrict__ in, int64_t ld, int C,
+                                                              const float* __restrict__ bias,
+                                                              const int32_t* __restrict__ p2v, int64_t n,
+                                                              float* __restrict__ out) {
+  const int64_t total = n * C;
+  for (int64_t e = (int64_t)blockIdx.x * kTT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kTT) {
+    const int64_t p = e / C;
+    const int c = (int)(e - p * C);
+    const float v = in[(int64_t)p2v[p] * ld + c];
+    out[e] = bias ? v + bias[c] : v;
+  }
+}
+
+// index_add_ along rows (train.py:107 `store.index_add_(0, point_ids, predictions)`), deterministic and
+// bit-equal to the serial CPU loop (for i in order: store[ids[i]] += src[i]): the (id, i) pairs are
+// radix sorted stably by id, so each id's rows form one run in ascending i; the thread at a run's first
+// position adds the run's rows into the stored value in that order.  Ids outside [0, n_store) carry the key
+// n_store and are skipped (the caller validates them).
+__global__ __launch_bounds__(kTT) void index_keys_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t n_store,
+                                                         uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * kTT + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = ids[i];
+  keys[i] = (id >= 0 && id < n_store) ? (uint64_t)id : (uint64_t)n_store;
+  vals[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(kTT) void index_add_runs_kernel(float* __restrict__ store, int64_t n_store, int C,
+                                                             const uint64_t* __restrict__ keys,
+                                                             const int32_t* __restrict__ vals, int64_t n,
+                                                             const float* __restrict__ src) {
+  const int64_t total = n * C;
+  for (int64_t e = (int64_t)blockIdx.x * kTT + threadIdx.x; e < total; e += (int64_t)gridDim.x * kTT) {
+    const int64_t j = e / C;
+    const int c = (int)(e - j * C);
+    const uint64_t k = keys[j];
+    if (k >= (uint64_t)n_store || (j > 0 && keys[j - 1] == k)) continue;
+    float s = store[(int64_t)k * C + c];
+    for (int64_t q = j; q < n && keys[q] == k; ++q) s += src[(int64_t)vals[q] * C + c];
+    store[(int64_t)k * C + c] = s;
+  }
+}
+
+inline unsigned tail_grid(int64_t total) {
+  int64_t g = ceil_div(total > 0 ? total : 1, kTT);
+  if (g > 65535 * 16) g = 65535 * 16;
+  return (unsigned)g;
+}
+
+inline int id_bits(int64_t n_store) {
+  int b = 1;
+  while (b < 63 && (n_store >> b) != 0) ++b;
+  return b;
+}
+
+inline size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
 }  // namespace msp
 
 using namespace msp;
@@ -164,6 +226,43 @@ int msp_scene_mean_bwd(const float* dout, int C, const uint64_t* keys, int64_t V
   if (g > 65535 * 16) g = 65535 * 16;
   scene_mean_bwd_kernel<<<(unsigned)g, kTT, 0, as_stream(stream)>>>(dout, C, keys, V, shift, vstart, npts, dfeats);
   return check_launch("msp_scene_mean_bwd");
+}
+
+int msp_point_rows_bias(const float* in, int64_t ld, int C, const float* bias, const int32_t* p2v, int64_t n_points,
+                        float* out, msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && ld >= C && n_points >= 0, "msp_point_rows_bias: bad arguments (C=%d ld=%lld)", C,
+              (long long)ld);
+  if (n_points == 0) return MSP_OK;
+  MSP_REQUIRE(in && p2v && out, "msp_point_rows_bias: NULL pointer");
+  point_rows_bias_kernel<<<tail_grid(n_points * C), kTT, 0, as_stream(stream)>>>(in, ld, C, bias, p2v, n_points,
+                                                                                 out);
+  return check_launch("msp_point_rows_bias");
+}
+
+size_t msp_index_add_workspace_size(int64_t n, int64_t n_store) {
+  if (n <= 0) return 0;
+  return 2 * al256((size_t)n * 8) + 2 * al256((size_t)n * 4) + al256(msp_sort_workspace_size(n, id_bits(n_store)));
+}
+
+int msp_index_add_rows(float* store, int64_t n_store, int C, const int64_t* ids, const float* src, int64_t n,
+                       void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && n >= 0 && n_store >= 0 && n < (1ll << 31), "msp_index_add_rows: bad arguments");
+  if (n == 0 || n_store == 0) return MSP_OK;
+  const size_t need = msp_index_add_workspace_size(n, n_store);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_index_add_rows: workspace too small (%zu < %zu)", ws_bytes, need);
+  hipStream_t s = as_stream(stream);
+  char* w = static_cast<char*>(ws);
+  uint64_t* k_in = reinterpret_cast<uint64_t*>(w);
+  uint64_t* k_out = reinterpret_cast<uint64_t*>(w + al256((size_t)n * 8));
+  int32_t* v_in = reinterpret_cast<int32_t*>(w + 2 * al256((size_t)n * 8));
+  int32_t* v_out = reinterpret_cast<int32_t*>(w + 2 * al256((size_t)n * 8) + al256((size_t)n * 4));
+  void* sws = w + 2 * al256((size_t)n * 8) + 2 * al256((size_t)n * 4);
+  const int bits = id_bits(n_store);
+  index_keys_kernel<<<(unsigned)ceil_div(n, kTT), kTT, 0, s>>>(ids, n, n_store, k_in, v_in);
+  int rc = msp_sort_pairs(k_in, k_out, v_in, v_out, n, bits, sws, msp_sort_workspace_size(n, bits), stream);
+  if (rc) return rc;
+  index_add_runs_kernel<<<tail_grid(n * C), kTT, 0, s>>>(store, n_store, C, k_out, v_out, n, src);
+  return check_launch("msp_index_add_rows");
 }
 
 }  // extern "C"

@@ -78,6 +78,8 @@ PROTOTYPES = {
     "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),
+    "msp_join_cols": (I, [P, I, P, I, I64, P, P, P]),
+    "msp_split_cols": (I, [P, I64, I, I, P, P, P]),
     "msp_nin_gemm_ok": (I, [I64, I, I]),
     "msp_nin_gemm_form": (I, [I64, I, I]),
     "msp_nin_gemm_workspace_size": (SZ, [I, I]),
@@ -93,6 +95,9 @@ PROTOTYPES = {
     "msp_scene_mean_workspace_size": (SZ, [I64, I, I]),
     "msp_scene_mean_fwd": (I, [P, I, P, I64, I, P, I, P, P, P, P, SZ, P]),
     "msp_scene_mean_bwd": (I, [P, I, P, I64, I, P, P, P, P]),
+    "msp_point_rows_bias": (I, [P, I64, I, P, P, I64, P, P]),
+    "msp_index_add_workspace_size": (SZ, [I64, I64]),
+    "msp_index_add_rows": (I, [P, I64, I, P, P, I64, P, SZ, P]),
     "msp_merge_workspace_size": (SZ, [I, I64]),
     "msp_merge": (I, [P, P, P, P, I, I64, I, D, P, P, P, P, P, P, I, P, P, P, P, I64, P, P, P, SZ, P]),
 }

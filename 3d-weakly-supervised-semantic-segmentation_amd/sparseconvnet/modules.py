@@ -329,9 +329,22 @@ class AddTable(nn.Module):
 
 
 class JoinTable(nn.Module):
+    """Channel concatenation in branch order on msp_join_cols; in training mode it also
+    leaves the batch-statistic partials of its output for the BatchNormalization it feeds (the UNet decoder
+    block, the FCN's final BN), like the residual join.  More than two inputs are joined left to right."""
+
     def forward(self, input):
-        return SparseConvNetTensor(torch.cat([t.features for t in input], 1), input[0].metadata,
-                                   input[0].spatial_size)
+        f = input[0].features
+        partial = None
+        if not f.is_cuda:  # the product has no CPU path: fail in the library binding, as every op does
+            ops._check_feats(f)
+        for k, t in enumerate(input[1:]):
+            last = k == len(input) - 2
+            f, partial = ops.JoinFunction.apply(f, t.features, bool(FUSE_RESIDUAL and self.training and last))
+        out = SparseConvNetTensor(f, input[0].metadata, input[0].spatial_size)
+        if partial is not None:
+            out._bn_partial = (f, partial)
+        return out
 
 
 class Identity(nn.Module):

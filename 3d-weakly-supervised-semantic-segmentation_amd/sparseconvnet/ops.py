@@ -458,9 +458,20 @@ class _IdentityPairs:
         self.pair = ar[:max(n, 1)]
 
 
-def nin_gemm(a, b, kind="nin"):
+NIN_MAX_K = 1024  # msp_nin_gemm_ok: the split image of B's K rows must fit the kernel's LDS budget
+
+
+def _aligned16(t):
+    """t itself when its data is 16-byte aligned (msp_nin_gemm's float4 loads), else an aligned copy."""
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def nin_gemm(a, b, kind="nin", keep_pad=False):
     """a[M][K] @ b[K][N] on msp_nin_gemm (HBM-bound tall-skinny product: fp32 MFMA from 2^18 rows, split-bf16
-    MFMA below); channel counts that are not multiples of 16 are zero-padded around the call."""
+    MFMA below); channel counts that are not multiples of 16 are zero-padded around the call (keep_pad: the
+    [M][pad16(N)] result is returned as is, its last columns zero).  Any nIn works (SCN's NetworkInNetwork takes
+    any): K beyond the kernel's 1024 is contracted in 1024-deep slices whose products are added in slice order;
+    operands that are not 16-byte aligned (a view with an odd storage offset) are copied first."""
     M, K = a.shape
     N = b.size(1)
     Kp, Np = _pad16(K), _pad16(N)
@@ -468,16 +479,23 @@ def nin_gemm(a, b, kind="nin"):
         a, b = _pad_cols(a.contiguous(), Kp), torch.cat([b, b.new_zeros(Kp - K, N)])
     if Np != N:
         b = _pad_cols(b, Np)
-    a, b = a.contiguous(), b.contiguous()
+    a, b = _aligned16(a.contiguous()), _aligned16(b.contiguous())
     flops, nbytes = 2.0 * M * K * N, 4 * (M * K + M * N + K * N)
-    out = torch.empty((max(M, 1), Np), dtype=torch.float32, device=a.device)
-    wsb = int(_lib.query("msp_nin_gemm_workspace_size", Kp, Np))
-    ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=a.device)
-    form = "/f32" if int(_lib.query("msp_nin_gemm_form", _lib.I64(M), Kp, Np)) == 1 else "/x6"
-    _record(kind + form, flops, lambda: call("msp_nin_gemm", ptr(a), M, Kp, ptr(b), Np, ptr(out), ptr(ws), wsb,
-                                             _stream(a)), nbytes)
+    out = None
+    for k0 in range(0, Kp, NIN_MAX_K):
+        k1 = min(Kp, k0 + NIN_MAX_K)
+        ak = a if (k0 == 0 and k1 == Kp) else a[:, k0:k1].contiguous()
+        bk = b if (k0 == 0 and k1 == Kp) else b[k0:k1].contiguous()
+        kk = k1 - k0
+        part = torch.empty((max(M, 1), Np), dtype=torch.float32, device=a.device)
+        wsb = int(_lib.query("msp_nin_gemm_workspace_size", kk, Np))
+        ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32, device=a.device)
+        form = "/f32" if int(_lib.query("msp_nin_gemm_form", _lib.I64(M), kk, Np)) == 1 else "/x6"
+        _record(kind + form, flops * kk / Kp, lambda: call("msp_nin_gemm", ptr(ak), M, kk, ptr(bk), Np, ptr(part),
+                                                           ptr(ws), wsb, _stream(a)), nbytes * kk // Kp)
+        out = part if out is None else out.add_(part)
     out = out[:M]
-    return out if Np == N else out[:, :N].contiguous()
+    return out if (Np == N or keep_pad) else out[:, :N].contiguous()
 
 
 class NetworkInNetworkFunction(torch.autograd.Function):
@@ -629,6 +647,44 @@ class ResidualJoinFunction(torch.autograd.Function):
         return g, g
 
 
+class JoinFunction(torch.autograd.Function):
+    """[a | b] along channels (SCN JoinTable of the UNet / FCN skip joins: identity branch first, §8(a) a12) on
+    msp_join_cols, with the batch-statistic partials of the result when `stats` (the BatchNormalization the
+    join feeds then skips its own pass over it, as after a residual join); backward splits the gradient in one
+    pass (msp_split_cols).  Returns (joined, partials or None)."""
+
+    @staticmethod
+    def forward(ctx, a, b, stats):
+        _check_feats(a)
+        _check_feats(b)
+        a, b = a.contiguous(), b.contiguous()
+        V, ca = a.shape
+        cb = b.size(1)
+        C = ca + cb
+        out = torch.empty((V, C), dtype=torch.float32, device=a.device)
+        partial = _bn_partial_buf(V, C, a.device) if stats else None
+        _record(_shape("bn_join/hbm", C, C, V), 0, lambda: call(
+            "msp_join_cols", ptr(a), ca, ptr(b), cb, V, ptr(out), ptr(partial), _stream(a)), 8 * V * C)
+        ctx.dims = (ca, cb)
+        ctx.set_materialize_grads(False)
+        if partial is not None:
+            ctx.mark_non_differentiable(partial)
+        return out, partial
+
+    @staticmethod
+    def backward(ctx, g, _gp):
+        if g is None:
+            return None, None, None
+        ca, cb = ctx.dims
+        g = g.contiguous()
+        V = g.size(0)
+        ga = torch.empty((V, ca), dtype=torch.float32, device=g.device) if ctx.needs_input_grad[0] else None
+        gb = torch.empty((V, cb), dtype=torch.float32, device=g.device) if ctx.needs_input_grad[1] else None
+        if ga is not None or gb is not None:
+            call("msp_split_cols", ptr(g), V, ca, cb, ptr(ga), ptr(gb), _stream(g))
+        return ga, gb, None
+
+
 # ------------------------------------------------------------------ input / output / pooling
 class InputLayerFunction(torch.autograd.Function):
     """mode 3 (sum) / 4 (mean) point -> voxel reduction (§8(a) a4)."""
@@ -723,6 +779,79 @@ class SceneMeanFunction(torch.autograd.Function):
         call("msp_scene_mean_bwd", ptr(g), C, ptr(ctx.level.keys), ctx.V, ctx.shift, ptr(ctx.rules.vstart),
              ptr(npts), ptr(dx), _stream(g))
         return dx[:ctx.V], None, None, None
+
+
+class PointLogitsFunction(torch.autograd.Function):
+    """Per-point logits of the head's Linear without the (N, C) per-point features (the
+    eval half; models/MultiLabelContrastive.py:43-45 `self.linear(self.pc_encoder(x))`, :84-101, train.py:106):
+    logits[p] = W x[v(p)] + b.  The Linear commutes with the OutputLayer's gather, so it runs on the level-0
+    voxel rows ((V, C) @ W^T on msp_nin_gemm) and each point gathers its voxel's n_out columns plus the bias
+    (msp_point_rows_bias).  Backward: the points' gradients summed per voxel (msp_output_bwd, fixed order),
+    dW from those sums (msp_conv_wgrad, identity pairs), dx = g_v W (msp_nin_gemm), db = column sums."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, rules):
+        _check_feats(x)
+        x = x.contiguous()
+        V, C = x.shape
+        n_out = weight.size(0)
+        if weight.size(1) != C:
+            raise ValueError(f"PointLogits: Linear({weight.size(1)}, {n_out}) on {C} channels")
+        vl = nin_gemm(x, weight.t(), kind="logits_fwd", keep_pad=True)  # (V, pad16(n_out))
+        out = torch.empty((max(rules.n_points, 1), n_out), dtype=torch.float32, device=x.device)
+        if rules.n_points:
+            call("msp_point_rows_bias", ptr(vl), vl.size(1), n_out, ptr(bias.contiguous()) if bias is not None
+                 else None, ptr(rules.p2v), rules.n_points, ptr(out), _stream(x))
+        ctx.save_for_backward(x, weight)
+        ctx.rules, ctx.has_bias = rules, bias is not None
+        return out[:rules.n_points]
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        rules = ctx.rules
+        V, C = x.shape
+        n_out = weight.size(0)
+        g = g.contiguous()
+        gv = torch.empty((max(V, 1), n_out), dtype=torch.float32, device=g.device)
+        if V:
+            call("msp_output_bwd", ptr(g), n_out, ptr(rules.perm), ptr(rules.vstart), V, ptr(gv), _stream(g))
+        gv = gv[:V]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = nin_gemm(gv, weight, kind="logits_bwd_data")
+        if ctx.needs_input_grad[1]:
+            cin_p, cout_p = _pad16(C), _pad16(n_out)
+            p = _IdentityPairs(V, x.device)
+            dw = conv_wgrad(_pad_cols(x, cin_p), _pad_cols(gv, cout_p), p, p.pair, p.pair, 1, "logits_wgrad",
+                            2.0 * V * C * n_out)[0, :C, :n_out].t()
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = gv.sum(0)
+        return dx, dw, db, None
+
+
+def index_add_rows(store, ids, src):
+    """store.index_add_(0, ids, src) on the device, bit-equal to the serial CPU loop for any ids
+    (msp_index_add_rows); ids outside [0, len(store)) raise IndexError like torch's (one host read)."""
+    _check_feats(store)
+    _check_feats(src)
+    if store.dim() != 2 or src.dim() != 2 or src.size(1) != store.size(1) or ids.numel() != src.size(0):
+        raise ValueError(f"index_add_rows: store {tuple(store.shape)}, ids {tuple(ids.shape)}, src {tuple(src.shape)}")
+    if not store.is_contiguous():
+        raise ValueError("index_add_rows: store must be contiguous (it is updated in place)")
+    n = ids.numel()
+    if n == 0:
+        return store
+    ids = ids.to(device=store.device, dtype=torch.int64).contiguous()
+    lo, hi = torch.aminmax(ids)
+    if int(lo) < 0 or int(hi) >= store.size(0):
+        raise IndexError(f"index_add_rows: index out of range [0, {store.size(0)}) (min {int(lo)}, max {int(hi)})")
+    src = src.contiguous()
+    wsb = int(_lib.query("msp_index_add_workspace_size", n, store.size(0)))
+    ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=store.device)
+    call("msp_index_add_rows", ptr(store), store.size(0), store.size(1), ptr(ids), ptr(src), n, ptr(ws), wsb,
+         _stream(store))
+    return store
 
 
 class UnPoolingFunction(torch.autograd.Function):

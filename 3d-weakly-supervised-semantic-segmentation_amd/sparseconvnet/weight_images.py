@@ -17,7 +17,10 @@ image descriptor is the recorded one; otherwise the call splits its own copy as 
 recorded for the next `build()`.  Changes are caught on the host, captures included: every optimizer step of the
 optimizer given to `enable` (a step post-hook) and any in-place change that bumps a parameter's version counter
 invalidate the images until the next `prepare()` -- torch's fused Adam does NOT bump version counters, hence the
-hook (`tests/test_gpu_weight_images.py::test_stale_image_is_not_used`).  Disabled (the default), nothing changes.
+hook (`tests/test_gpu_weight_images.py::test_stale_image_is_not_used`), which is why `enable` requires the
+optimizer (`invalidate()` is public for weights changed any other way, e.g. `p.data` assignments or a
+broadcast).  A parameter whose storage is replaced (`model.to()`, `p.data = ...`) drops its images at the next
+`build()` / `prepare()`: no split ever reads a freed weight buffer.  Disabled (the default), nothing changes.
 """
 from __future__ import annotations
 
@@ -33,8 +36,10 @@ _ACTIVE = None
 class WeightImages:
     def __init__(self, params, device):
         self.device = torch.device(device)
-        self.owners = {p.untyped_storage().data_ptr(): p for p in params}
-        self.entries = {}  # key -> [desc, owner, img tensor or None, version at the last prepare or None]
+        self.params = list(params)
+        self.owners = {p.untyped_storage().data_ptr(): p for p in self.params}
+        # key -> [desc, owner, img tensor or None, version at the last prepare or None, owner storage at record]
+        self.entries = {}
         self.dirty = False
         self.table = None  # (descs device tensor, starts device tensor, n, total units)
         self.hits = 0      # calls that found their image prepared
@@ -53,18 +58,31 @@ class WeightImages:
         e = self.entries.get(key)
         if e is None:
             d.wt = wt.data_ptr()
-            self.entries[key] = [d, owner, None, None]
+            self.entries[key] = [d, owner, None, None, owner.untyped_storage().data_ptr()]
             self.dirty = True
             return None
-        desc, _, img, version = e
+        desc, _, img, version, _ = e
         if not self.valid or img is None or version is None or version != wt._version or img.numel() < d.bytes:
             return None
         self.hits += 1
         return img
 
     # ------------------------------------------------------------------ per step
+    def _prune(self):
+        """Drop the images of parameters whose storage was replaced since they were recorded (their descriptors
+        point at the old, possibly freed, buffer) and re-key the owners on the current storages."""
+        stale = [k for k, e in self.entries.items() if e[1].untyped_storage().data_ptr() != e[4]]
+        if stale:
+            for k in stale:
+                del self.entries[k]
+            self.owners = {p.untyped_storage().data_ptr(): p for p in self.params}
+            self.dirty = True
+            self.table = None
+            self.valid = False
+
     def build(self):
         """Allocate the images new descriptors need and upload the descriptor table (not inside a capture)."""
+        self._prune()
         if not self.dirty or not self.entries:
             return
         if torch.cuda.is_current_stream_capturing():
@@ -86,6 +104,7 @@ class WeightImages:
 
     def prepare(self):
         """Split every recorded image in one launch on the current stream (capturable).  Returns whether it ran."""
+        self._prune()
         if self.dirty:
             self.build()
         if self.table is None or self.dirty:
@@ -103,14 +122,17 @@ class WeightImages:
 
 
 def enable(model, device=None, optimizer=None):
-    """Turn per-step images on for the parameters of `model` (returns the manager); `optimizer`: its steps
-    invalidate the images (pass the optimizer that updates these parameters)."""
+    """Turn per-step images on for the parameters of `model` (returns the manager).  `optimizer` (required): the
+    optimizer that updates these parameters -- its steps invalidate the images.  Fused / capturable optimizers
+    do not bump parameter version counters, so without the hook a stale image would go unnoticed."""
     global _ACTIVE
+    if optimizer is None or not hasattr(optimizer, "register_step_post_hook"):
+        raise ValueError("sparseconvnet.weight_images.enable: pass the optimizer that updates the model's parameters "
+                         "(its step post-hook invalidates the images)")
     params = list(model.parameters())
     dev = device if device is not None else (params[0].device if params else "cuda")
     _ACTIVE = WeightImages(params, dev)
-    if optimizer is not None:
-        optimizer.register_step_post_hook(_ACTIVE.invalidate)
+    optimizer.register_step_post_hook(_ACTIVE.invalidate)
     return _ACTIVE
 
 

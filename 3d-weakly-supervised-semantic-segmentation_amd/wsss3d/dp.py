@@ -25,8 +25,6 @@ from __future__ import annotations
 
 import os
 
-import time
-
 import torch
 import torch.distributed as dist
 
@@ -215,15 +213,28 @@ class GradSync:
 
 
 def settle(device=None):
-    """Call after an eager collective and before a graph capture that issues collectives.  ProcessGroupNCCL's
-    watchdog thread polls the events of every eager collective until it has seen it complete (one pass per
-    ~100 ms); a poll that lands while the communicator's stream is capturing fails with hipErrorCapturedEvent and
-    the watchdog terminates the process (seen intermittently right after the communicator warm-up).  Waiting for
-    the device and a few of its passes lets it retire the eager work first."""
+    """Call after the last eager collective and before a graph capture that issues collectives.
+
+    Mechanism of the abort this removes (round 3, intermittent in the one-rank RCCL bench test): every eager
+    collective's Work sits in ProcessGroupNCCL's watchdog list until the watchdog thread, on one of its passes
+    (one per ~100 ms), queries the Work's end event and sees it complete.  That event was recorded on the
+    communicator's stream.  A collective captured into a HIP graph makes the same stream join the capture
+    (it waits on the capturing stream), and a watchdog query of an event of a stream that is capturing returns
+    hipErrorCapturedEvent -- which the watchdog treats as fatal and terminates the process.  So the race is
+    between the watchdog's retirement of the LAST eager collective (the communicator warm-up, the barrier) and
+    the first capture.
+
+    The fix is structural: wait until the watchdog list is empty.  ProcessGroupNCCL::waitForPendingWorks
+    (`ProcessGroup._wait_for_pending_works`) returns once the watchdog has retired every enqueued Work -- it
+    checks the list under the same mutex the watchdog holds while it queries events, so when it returns no
+    query is in flight and none can start for Works issued before.  Captured collectives are never enqueued
+    to the watchdog (ProcessGroupNCCL skips the watchdog while the stream is capturing), so after this call
+    nothing the watchdog polls can meet a capture.  The device synchronisation first makes the eager
+    collectives complete, so the wait is one or two watchdog passes."""
     if not (dist.is_initialized() and dist.get_backend() == "nccl"):
         return
     torch.cuda.synchronize(device)
-    time.sleep(0.35)
+    dist.distributed_c10d._get_default_group()._wait_for_pending_works()
 
 
 def max_over_ranks(x: float) -> float:

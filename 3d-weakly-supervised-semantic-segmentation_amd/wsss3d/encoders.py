@@ -16,7 +16,7 @@ import torch
 from torch import nn
 
 import sparseconvnet as scn
-from sparseconvnet.ops import SceneMeanFunction
+from sparseconvnet.ops import PointLogitsFunction, SceneMeanFunction
 
 from .registry import MODEL_REGISTRY
 
@@ -49,17 +49,35 @@ class SparseConvBase_(nn.Module):
             raise AssertionError(f"encoder name {name!r} does not match class {type(self).__name__!r}")
         self.encoder = self.getEncoder(*args, **kwarg)
 
-    def forward(self, x, istrain=False):
+    @staticmethod
+    def _inputs(x):
         if not isinstance(x, dict):
             raise AssertionError(f"batch data type unsupported. Expected EasyDict, got {type(x)}. ")
         coords, feats = x["coords"], x["feature"]
         if coords.size(0) != feats.size(0):
             raise AssertionError(f"Coords and feats not aligned! coords's batchsize is {coords.size(0)} "
                                  f"while feats' is {feats.size(0)}. ")
+        return coords, feats
+
+    def forward(self, x, istrain=False):
+        coords, feats = self._inputs(x)
         if istrain and self._fusable():
             return self._encode_scene_means(coords, feats, x["batch_offsets"])
         out = self.encode([coords, feats])
         return self.postProcessing(out, x["batch_offsets"]) if istrain else out
+
+    def point_logits(self, x, linear: nn.Linear):
+        """`linear(self(x))` -- the per-point logits of the reference's eval call (train.py:106;
+        models/MultiLabelContrastive.py:43-45, 84-101) -- with the Linear applied to the level-0 voxel rows
+        before the OutputLayer's gather (ops.PointLogitsFunction): the (N, C)
+        per-point feature tensor (N x 896 floats for SparseConvFCNet m=32) is never formed.  Same values up to
+        fp32 rounding (the gather is a copy); encoders that override encode/postProcessing take the per-point
+        path."""
+        coords, feats = self._inputs(x)
+        if not self._fusable():
+            return linear(self.encode([coords, feats]))
+        t = self.encoder[:-1]([coords, feats])
+        return PointLogitsFunction.apply(t.features, linear.weight, linear.bias, t.metadata.input)
 
     # ---------------------------------------------------------------- fused tail
     def _fusable(self):

@@ -2,7 +2,9 @@
 `utils/loss.py:5-33`).
 
 The training call is `model((x, text), istrain=True)` (train.py:69) and the
-eval call `model(x)` -> per-point logits (N, 20) (train.py:106).  The text
+eval call `model(x)` -> per-point logits (N, 20) (train.py:106), computed with
+the Linear on the level-0 voxel rows (no (N, C) per-point features; the
+device accumulation of train.py:107 is wsss3d.evaluate).  The text
 model of MultiLabelContrastive is looked up in the registry: TextTransformer
 (wsss3d/text.py) is registered; CLIPTransformer needs pretrained CLIP weights
 that are not available offline.  Scene features in training come from the
@@ -17,6 +19,13 @@ from torch import nn
 from .encoders import segment_mean
 from .registry import LOSS_REGISTRY, MODEL_REGISTRY
 from .synthetic import NUM_CLASSES
+
+
+def point_logits(encoder, x, linear):
+    """linear(encoder(x)) as per-point logits (N, 20): through the encoder's fused voxel-level head
+    (SparseConvBase_.point_logits, no (N, C) feature tensor) when it has one."""
+    fn = getattr(encoder, "point_logits", None)
+    return fn(x, linear) if fn is not None else linear(encoder(x))
 
 
 def _encoder(pc_config):
@@ -35,10 +44,9 @@ class MultiLabel(nn.Module):
         self.linear = nn.Linear(width, NUM_CLASSES)
 
     def forward(self, x, istrain=False):
-        if istrain:
-            x = x[0]
-        logits = self.linear(self.pc_encoder(x, istrain))
-        return (logits, None) if istrain else logits
+        if not istrain:
+            return point_logits(self.pc_encoder, x, self.linear)
+        return self.linear(self.pc_encoder(x[0], True)), None
 
 
 @MODEL_REGISTRY.register()
@@ -53,9 +61,9 @@ class FullySupervised(nn.Module):
     def forward(self, x, istrain=False):
         if istrain:
             pc_input = x[0]
-            logits = self.linear(self.pc_encoder(pc_input))
+            logits = point_logits(self.pc_encoder, pc_input, self.linear)
             return segment_mean(logits, pc_input.batch_offsets), logits
-        return self.linear(self.pc_encoder(x))
+        return point_logits(self.pc_encoder, x, self.linear)
 
 
 @MODEL_REGISTRY.register()
@@ -74,7 +82,7 @@ class MultiLabelContrastive(nn.Module):
 
     def forward(self, x, istrain=False):
         if not istrain:
-            return self.linear(self.pc_encoder(x))
+            return point_logits(self.pc_encoder, x, self.linear)
         pc_input, (text, has_text) = x
         if has_text.size(0) > 0:
             bt, nt, length = text.size()

@@ -22,8 +22,10 @@
  *   - Return 0 on success, a negative MSP_E* code on failure; the message is
  *     thread-local and read with msp_last_error().
  *   - Stateless and reentrant: no entry point reads or writes process-global
- *     state (the only static is the cached CU count of the device); every
- *     exported symbol is declared here (tests/test_abi.py checks the .so's
+ *     state beyond two per-device caches -- each device's CU count and which
+ *     kernels have had their dynamic-LDS limit raised on it -- held in atomics
+ *     indexed by device id (safe from several threads and on several devices);
+ *     every exported symbol is declared here (tests/test_abi.py checks the .so's
  *     dynamic symbol table against this header).
  *   - Offset-major maps: a neighbour / child map with K filter offsets over n
  *     rows is stored [K][n] (entry -1 = absent).  Filter offsets follow SCN's
@@ -331,6 +333,14 @@ int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, cons
                          float* dx, float* dweight, float* dbias, msp_stream_t stream);
 int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,
                      msp_stream_t stream);
+/* Channel join (SCN JoinTable, the UNet / FCN skip joins: identity branch first, then the upsampled deeper
+ * level): out[v] = [a[v] | b[v]], a [V][ca], b [V][cb], out [V][ca + cb].  With partial
+ * non-NULL also the msp_bn_stats partials of out (identical to msp_bn_stats on it), for the BatchNormalization
+ * the join feeds.  msp_split_cols is its backward: in [V][ca + cb] -> a [V][ca], b [V][cb] (either may be
+ * NULL). */
+int msp_join_cols(const float* a, int ca, const float* b, int cb, int64_t V, float* out, double* partial,
+                  msp_stream_t stream);
+int msp_split_cols(const float* in, int64_t V, int ca, int cb, float* a, float* b, msp_stream_t stream);
 
 /* ---------------- NetworkInNetwork products (replaces SCN's NetworkInNetwork
  * forward / backward-data, scn.NetworkInNetwork in the UNet/FCN residual
@@ -385,6 +395,23 @@ int msp_scene_mean_fwd(const float* feats, int C, const uint64_t* keys, int64_t 
 /* dfeats[v] = (cnt_v / npts[b(v)]) * dout[b(v)] */
 int msp_scene_mean_bwd(const float* dout, int C, const uint64_t* keys, int64_t V, int shift, const int32_t* vstart,
                        const int64_t* npts, float* dfeats, msp_stream_t stream);
+
+/* ---------------- fused encoder tail (eval / per-point logits): the head's Linear
+ * (models/MultiLabelContrastive.py:43-45 `self.linear(self.pc_encoder(x))`, :84-101; train.py:106) commutes
+ * with the OutputLayer's gather, so the caller applies it to the level-0 voxel rows ((V, C) @ W^T on
+ * msp_nin_gemm -> in, row stride ld) and this gathers the C output columns per point plus the bias:
+ * out[p][c] = in[p2v[p] * ld + c] + bias[c] (bias may be NULL).  The (N, C_embed) per-point feature tensor
+ * is never formed. */
+int msp_point_rows_bias(const float* in, int64_t ld, int C, const float* bias, const int32_t* p2v, int64_t n_points,
+                        float* out, msp_stream_t stream);
+/* store[ids[i]][:] += src[i][:] for i = 0..n-1 (train.py:107 `store.index_add_(0, point_ids, predictions)`),
+ * bit-equal to the serial loop in i order for any ids (repeated ids included): pairs (id, i) are radix sorted
+ * stably by id and each id's run is added into the stored row in ascending i.  Ids outside [0, n_store) are
+ * skipped (the caller validates them).  store [n_store][C], src [n][C] float32; ids int64 (device).
+ * ws_bytes >= msp_index_add_workspace_size(n, n_store). */
+size_t msp_index_add_workspace_size(int64_t n, int64_t n_store);
+int msp_index_add_rows(float* store, int64_t n_store, int C, const int64_t* ids, const float* src, int64_t n,
+                       void* ws, size_t ws_bytes, msp_stream_t stream);
 
 /* ---------------- batch assembly on the device:
  * the per-point part of trainMerge (mode 0, dataset/data.py:135-238) and

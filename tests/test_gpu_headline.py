@@ -1,0 +1,165 @@
+"""Parity on the benchmarked batches themselves, with the north star's absolute bar on per-point LOGITS.
+
+* C3 (BASELINE.json configs[2], the headline): the exact batch and model bench.py times on rank 0 --
+  `make_batch(8, 50, seed=0)` (1.35e6 level-0 voxels), SparseConvUNet m=32 block_reps=2 residual under
+  `torch.manual_seed(0)`, MultiLabel head.
+* C5 (configs[4], per GPU): MultiLabelContrastive's point branch -- SparseConvFCNet m=32 block_reps=1 at
+  scale 20, 8 scenes (`make_batch(8, 20, seed=0)`, bench.py --preset c5's first batch) -- whose 896-wide
+  features are the case the fused eval head exists for.
+
+Each runs the reference's eval call `model(x)` (train.py:106; models/MultiLabelContrastive.py:43-45, 64-70)
+on the device -- the per-point logits through the fused voxel-level head (heads.point_logits) -- with
+train-mode BatchNorm (the batch statistics of all 8 scenes, as the timed training step normalises), under
+no_grad, and an INDEPENDENT fp64 oracle forward of the same weights (oracle/scn_oracle.py, its own ReLU
+decisions) followed by the head's Linear in fp64.  Bar: |logits - oracle| <= 1e-4 absolute, every point
+(BASELINE.json north star: "per-point logits within 1e-4 of reference").  The C3 test also prints the error
+of every BatchNorm-ReLU output through the network's depth (the per-layer error growth of the split-bf16
+convolutions, whose per-op accuracy bar is 3x a plain fp32 evaluation's error, tests/test_gpu_ops.py) and
+requires the production kernel forms to have run on this batch.  The C5 test requires the eval head to run
+without an (N, 896) allocation (peak device memory).  Parity is against the restated SCN semantics ("parity
+unpinned" against SCN itself).
+"""
+import pytest
+import torch
+
+import sparseconvnet as scn  # noqa: F401
+from sparseconvnet import _lib
+from oracle import scn_oracle as O
+from oracle.encoders import OracleEncoder
+from oracle.parity import raster_perm
+from wsss3d import EasyDict, MODEL_REGISTRY
+from wsss3d.synthetic import make_batch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+LOGIT_BAR = 1e-4  # absolute, per point and class (BASELINE.json north star)
+
+
+class _Kinds:
+    def __init__(self):
+        self.kinds = {}
+
+    def run(self, kind, flops, fn, nbytes=0):
+        kind = kind.split("[")[0]
+        self.kinds[kind] = self.kinds.get(kind, 0) + 1
+        return fn()
+
+
+def _oracle_twin(model, name, m, reps, residual):
+    ref = OracleEncoder(name, m=m, block_reps=reps, residual_blocks=residual).double()
+    ref.load_state_dict({k: v.double().cpu() for k, v in model.pc_encoder.state_dict().items()})
+    lin = torch.nn.Linear(model.linear.in_features, model.linear.out_features).double()
+    lin.load_state_dict({k: v.double().cpu() for k, v in model.linear.state_dict().items()})
+    return ref, lin
+
+
+def _layer_errors(model, ref, xg, xo):
+    """Device forward with every BatchNorm output captured, then the oracle forward comparing each BN output
+    as it is produced (rows matched by location).  Returns (device logits, oracle logits, table)."""
+    caps, hooks = {}, []
+    bn_dev = {n: mod for n, mod in model.pc_encoder.named_modules() if type(mod).__name__.startswith("BatchNorm")}
+    for n, mod in bn_dev.items():
+        hooks.append(mod.register_forward_hook(lambda md, i, o, n=n: caps.__setitem__(n, o)))
+    with torch.no_grad():
+        logits = model(xg)
+    for h in hooks:
+        h.remove()
+    perms, table = {}, []
+
+    def check(md, i, o, n):
+        d = caps[n]
+        size = int(d.spatial_size[0])
+        if size not in perms:
+            perms[size] = torch.from_numpy(raster_perm(d.metadata.locations(size).cpu().numpy(), size))
+        dv = d.features.detach().double().cpu()[perms[size]]
+        rv = o.features.detach()
+        table.append((n, size, rv.size(0), rv.size(1), (dv - rv).abs().max().item(), rv.abs().max().item()))
+
+    bn_ref = {n: mod for n, mod in ref.named_modules() if isinstance(mod, O.BatchNormalization)}
+    for n, mod in bn_ref.items():
+        hooks.append(mod.register_forward_hook(lambda md, i, o, n=n: check(md, i, o, n)))
+    with torch.no_grad():
+        feats_o = ref(xo)
+    for h in hooks:
+        h.remove()
+    del caps
+    return logits, feats_o, table
+
+
+def _inputs(b):
+    coords = torch.from_numpy(b["coords"])
+    feats = torch.from_numpy(b["feats"])
+    xg = EasyDict(coords=coords.to(DEV), feature=feats.to(DEV), batch_offsets=b["batch_offsets"])
+    xo = dict(coords=coords, feature=feats.double(), batch_offsets=b["batch_offsets"])
+    return xg, xo
+
+
+@pytest.mark.timeout(1100)
+def test_headline_batch_logits_parity():
+    """C3 exactly as bench.py times it (rank 0, first batch): per-point logits of the 8-scene batch within 1e-4
+    absolute of the fp64 oracle; per-layer error growth printed."""
+    torch.manual_seed(0)
+    pc = EasyDict(name="SparseConvUNet", m=32, dimension=3, full_scale=4096, block_reps=2, residual_blocks=True)
+    model = MODEL_REGISTRY.get("MultiLabel")[0](pc).to(DEV)
+    b = make_batch(8, 50, seed=0)
+    xg, xo = _inputs(b)
+    ref, lin = _oracle_twin(model, "SparseConvUNet", 32, 2, True)
+    rec = _Kinds()
+    _lib.set_recorder(rec)
+    try:
+        logits, feats_o, table = _layer_errors(model, ref, xg, xo)
+    finally:
+        _lib.set_recorder(None)
+    with torch.no_grad():
+        logits_o = lin(feats_o)
+    n = logits_o.size(0)
+    assert logits.shape == (n, 20) and n == len(b["coords"])
+    print(f"C3 headline batch: {n} points; BatchNorm-ReLU outputs through the depth (max abs err, max |oracle|, "
+          "ratio):")
+    for name, size, rows, c, err, mx in table:
+        print(f"  {name:<40s} size {size:5d} rows {rows:8d} C {c:4d}  err {err:.3e}  max {mx:.3e}  "
+              f"ratio {err / max(mx, 1e-30):.2e}")
+    worst_layer = max(t[4] / max(t[5], 1e-30) for t in table)
+    ferr = table[-1][4]
+    err = (logits.double().cpu() - logits_o).abs().max().item()
+    print(f"C3: final features max err {ferr:.3e}; per-point logits max err {err:.3e} (bar {LOGIT_BAR:g} absolute, "
+          f"max |logit| {logits_o.abs().max().item():.3e}); worst per-layer relative error {worst_layer:.2e}")
+    assert err <= LOGIT_BAR, f"C3 per-point logits: {err:.3e} > {LOGIT_BAR}"
+    need = ["subm_fwd/x6r", "subm_fwd/x6s", "subm_fwd/x6d", "subm_fwd/f32n", "nin_fwd/f32", "nin_fwd/x6",
+            "conv_fwd/x6d", "deconv_fwd/f32", "logits_fwd"]
+    got = {k.split("/")[0] if k.startswith("logits_fwd") else k for k in rec.kinds}
+    missing = [k for k in need if k not in got]
+    assert not missing, f"production forms that did not run: {missing} (ran: {sorted(rec.kinds)})"
+
+
+@pytest.mark.timeout(900)
+def test_c5_batch_logits_parity_without_per_point_features():
+    """C5's point branch at its full per-GPU batch (8 scenes at scale 20): per-point logits from the 896-wide
+    FCNet features within 1e-4 absolute of the fp64 oracle, and the fused eval head never allocates the
+    (N, 896) per-point feature tensor (peak device memory of the eval call stays below it)."""
+    torch.manual_seed(0)
+    pc = EasyDict(name="SparseConvFCNet", m=32, dimension=3, full_scale=4096, block_reps=1, residual_blocks=False)
+    tc = EasyDict(name="TextTransformer", context_length=120, width=512, layers=12, vocab_size=49408)
+    model = MODEL_REGISTRY.get("MultiLabelContrastive")[0](pc, tc).to(DEV)
+    b = make_batch(8, 20, seed=0)
+    xg, xo = _inputs(b)
+    n = len(b["coords"])
+    per_point_bytes = n * 896 * 4
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    with torch.no_grad():
+        logits = model(xg)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    print(f"C5 eval call: {n} points, peak device memory {peak / 2**20:.0f} MiB above the inputs; an (N, 896) "
+          f"feature tensor alone is {per_point_bytes / 2**20:.0f} MiB")
+    assert logits.shape == (n, 20)
+    assert peak < per_point_bytes, "the eval head allocated at least an (N, 896) tensor's worth of memory"
+    ref, lin = _oracle_twin(model, "SparseConvFCNet", 32, 1, False)
+    with torch.no_grad():
+        logits_o = lin(ref(xo))
+    err = (logits.double().cpu() - logits_o).abs().max().item()
+    print(f"C5: per-point logits max err {err:.3e} (bar {LOGIT_BAR:g} absolute, max |logit| "
+          f"{logits_o.abs().max().item():.3e})")
+    assert err <= LOGIT_BAR, f"C5 per-point logits: {err:.3e} > {LOGIT_BAR}"

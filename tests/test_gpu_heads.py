@@ -134,3 +134,79 @@ def test_text_block_fixture_on_device():
     with torch.no_grad():
         y = blk(x).transpose(0, 1).cpu()
     assert (y - torch.from_numpy(g["y"])).abs().max().item() < 1e-10
+
+
+@pytest.mark.parametrize("head", ["MultiLabel", "FullySupervised"])
+def test_fused_eval_logits_match_per_point_head(head):
+    """The fused eval head (heads.point_logits: Linear on the voxel rows, msp_point_rows_bias gather) against the
+    reference's composition linear(pc_encoder(x)) on the same device model (train.py:106,
+    models/MultiLabelContrastive.py:64-70, 96-99); FullySupervised's training outputs (scene-mean logits and
+    per-point logits, :84-94) and every parameter gradient through the fused head's backward against the same
+    composition.  Eval-mode BatchNorm (running statistics) for the eval call."""
+    torch.manual_seed(1)
+    b = make_batch(2, 20, seed=6, spacing=0.04)
+    pc = EasyDict(name="SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=1, residual_blocks=True)
+    model = MODEL_REGISTRY.get(head)[0](pc).to(DEV)
+    with torch.no_grad():
+        model.linear.bias.uniform_(-0.5, 0.5)
+    x = EasyDict(coords=torch.from_numpy(b["coords"]).to(DEV), feature=torch.from_numpy(b["feats"]).to(DEV),
+                 batch_offsets=b["batch_offsets"])
+    model.eval()
+    with torch.no_grad():
+        fused = model(x)
+        ref = model.linear(model.pc_encoder(x))
+    assert fused.shape == ref.shape == (len(b["coords"]), 20)
+    err = (fused - ref).abs().max().item()
+    assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
+    if head != "FullySupervised":
+        return
+    model.train()
+    y = torch.from_numpy(b["labels"]).to(DEV)
+    y[::7] = -100
+    up = torch.randn(2, 20, device=DEV)
+    grads = []
+    for fused_path in (True, False):
+        model.zero_grad(set_to_none=True)
+        if fused_path:
+            glob, logits = model((x, None), istrain=True)
+        else:
+            logits = model.linear(model.pc_encoder(x))
+            glob = segment_mean(logits, x.batch_offsets)
+        loss = LOSS_REGISTRY.get("Classification")[0](logits, y) + (glob * up).sum()
+        loss.backward()
+        grads.append(({k: p.grad.detach().clone() for k, p in model.named_parameters()}, glob.detach(),
+                      logits.detach()))
+    (gf, globf, lf), (gr, globr, lr) = grads
+    assert (globf - globr).abs().max().item() <= 1e-5 * max(1.0, globr.abs().max().item())
+    assert (lf - lr).abs().max().item() <= 1e-5 * max(1.0, lr.abs().max().item())
+    for k in gr:
+        scale = max(gr[k].abs().max().item(), 1e-12)
+        assert (gf[k] - gr[k]).abs().max().item() <= 1e-4 * scale + 1e-9, k
+
+
+def test_device_logit_store_matches_cpu_index_add():
+    """wsss3d.evaluate.PointLogitStore.add = train.py:107's `store.index_add_(0, point_ids, predictions.cpu())`
+    bit for bit, over two validation reps (every id once per rep, shuffled, as valMerge's point_ids) and over
+    a batch with repeated ids (the serial loop's order decides the rounding; the device sorts stably)."""
+    from wsss3d.evaluate import PointLogitStore
+    g = torch.Generator().manual_seed(3)
+    n = 50000
+    store_cpu = torch.zeros(n, 20)
+    dev = PointLogitStore(n, DEV)
+    for rep in range(2):
+        for part in torch.randperm(n, generator=g).chunk(3):
+            pred = torch.randn(len(part), 20, generator=g) * 10
+            store_cpu.index_add_(0, part, pred)
+            dev.add(part.to(DEV), pred.to(DEV))
+    assert torch.equal(dev.cpu(), store_cpu)
+    assert torch.equal(dev.argmax().cpu(), store_cpu.max(1)[1])
+    ids = torch.randint(0, 300, (40000,), generator=g)
+    src = torch.randn(40000, 20, generator=g) * torch.logspace(-3, 3, 40000)[:, None]
+    base = torch.randn(300, 20, generator=g)
+    want = base.clone().index_add_(0, ids, src)
+    got = base.to(DEV)
+    from sparseconvnet.ops import index_add_rows
+    index_add_rows(got, ids.to(DEV), src.to(DEV))
+    assert torch.equal(got.cpu(), want)
+    with pytest.raises(IndexError):
+        index_add_rows(got, torch.tensor([0, 300], device=DEV), src[:2].to(DEV))

@@ -196,6 +196,41 @@ def test_nin_join_add():
     torch.testing.assert_close(a.features, 2 * y.features)
 
 
+@pytest.mark.parametrize("ca,cb", [(32, 32), (64, 128), (16, 8), (6, 10)])
+def test_join_table(ca, cb):
+    """JoinTable on msp_join_cols: bit-equal to torch.cat in branch order, its backward bit-equal to the gradient's
+    column slices (msp_split_cols), and the batch-statistic partials it leaves in training mode give the following
+    BatchNormalization bit-identical outputs, gradients and running statistics to the BN's own statistics pass
+    (FUSE_RESIDUAL off)."""
+    from sparseconvnet import modules as M
+    coords, feats = _inputs(5000, 24, n_feat=ca)
+    torch.manual_seed(ca + cb)
+    outs = []
+    for fuse in (True, False):
+        M.FUSE_RESIDUAL = fuse
+        try:
+            t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+            a = t.features.detach().clone().requires_grad_(True)
+            b = torch.randn(a.size(0), cb, device=DEV, requires_grad=True)
+            ta = scn.SparseConvNetTensor(a, t.metadata, t.spatial_size)
+            tb = scn.SparseConvNetTensor(b, t.metadata, t.spatial_size)
+            j = scn.JoinTable().train()([ta, tb])
+            assert torch.equal(j.features, torch.cat([a, b], 1))
+            assert (getattr(j, "_bn_partial", None) is not None) == fuse
+            bn = scn.BatchNormReLU(ca + cb).to(DEV)
+            y = bn(j).features
+            g = torch.randn_like(y)
+            y.backward(g)
+            outs.append((y.detach(), a.grad, b.grad, bn.weight.grad, bn.running_mean.clone(), bn.running_var.clone()))
+        finally:
+            M.FUSE_RESIDUAL = True
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+    gj = torch.randn(a.size(0), ca + cb, device=DEV)
+    ga, gb = torch.autograd.grad(scn.JoinTable()([ta, tb]).features, (a, b), gj)
+    assert torch.equal(ga, gj[:, :ca]) and torch.equal(gb, gj[:, ca:])
+
+
 @pytest.mark.parametrize("n,cin,cout", [(5000, 64, 32), (3001, 40, 24), (70000, 96, 48)])
 def test_nin_grads(n, cin, cout):
     """NetworkInNetwork backward: dx on msp_nin_gemm, dW on msp_conv_wgrad with
@@ -333,9 +368,11 @@ def test_conv_tile_split_bf16_accuracy(cin, cout, flip):
                                            (96, 192, 0), (48, 64, 0), (64, 128, 1), (32, 32, 0), (16, 80, 1)])
 def test_conv_nbr_accuracy(cin, cout, flip):
     """msp_conv_nbr (dense row groups over the neighbour map, register
-    accumulators) against an fp64 evaluation of the same convolution: the
-    error bar of the split-bf16 tile form (at most 2x a plain fp32
-    evaluation's error, and below 1e-6 of the output scale), and agreement
+    accumulators) against an fp64 evaluation of the same convolution: at most
+    2x a plain fp32 evaluation's error and below 1e-6 of the output scale
+    (this form sums each step's six piece products in a zeroed accumulator;
+    the tile-local form, which chains them into the running sums, has the 3x
+    bar of test_conv_tile_split_bf16_accuracy), and agreement
     with msp_conv_tile; the mask-sorted row order
     (msp_dense_order) gives bitwise the same rows.  Includes c_in not a
     multiple of 32 (zero k-padding) and a last group of rows past the level."""
@@ -554,6 +591,24 @@ def test_nin_gemm_padded(M, K, N):
     b = torch.randn(K, N, device=DEV)
     ref = a.double() @ b.double()
     assert (ops.nin_gemm(a, b).double() - ref).abs().max().item() < 1e-6 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("M,K,N", [(5000, 1200, 64), (3000, 2048, 48), (300000, 1040, 32)])
+def test_nin_gemm_deep_k(M, K, N):
+    """nIn beyond the kernel's 1024-deep split image (SCN's NetworkInNetwork takes any nIn): 1024-deep slices
+    whose products are added in order, on both forms; and a misaligned operand view (odd storage offset)."""
+    from sparseconvnet import ops
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV) / K ** 0.5
+    ref = a.double() @ b.double()
+    tol = 2e-5 if M >= 1 << 18 else 2e-6
+    assert (ops.nin_gemm(a, b).double() - ref).abs().max().item() < tol * ref.abs().max().item()
+    buf = torch.randn(M * 64 + 1, device=DEV)
+    am = buf[1:].view(M, 64)  # 4-byte aligned only
+    bm = torch.randn(64, N, device=DEV)
+    ref = am.double() @ bm.double()
+    assert (ops.nin_gemm(am, bm).double() - ref).abs().max().item() < 1e-5 * ref.abs().max().item()
 
 
 def test_nin_layer_grad():
@@ -808,3 +863,31 @@ def test_conv_wgrad_chunk_over_cap_falls_back():
         ref[o] = x.detach().double()[nb[o][m]].t() @ dy.double()[m]
     dw = w.grad.reshape(K, 32, 64).double()
     assert (dw - ref).abs().max().item() / ref.abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("n,end_bit,span", [(1, 8, 256), (4095, 12, 3000), (4097, 39, 1 << 39), (300001, 39, 5000),
+                                            (1600000, 39, 1 << 39), (70000, 64, 0), (5000, 20, 7)])
+def test_sort_pairs_stable(n, end_bit, span):
+    """msp_sort_pairs (the library's own LSD radix sort: ballot-ranked scatter, msp_sort.hip) against numpy's
+    stable argsort on key bits [0, end_bit): ragged last tiles, one-digit and five-digit sorts, heavy duplicates
+    (stability decides the values' order), all-ones keys (the InputLayer's out-of-range sentinel) and a 64-bit
+    sort of full-range keys."""
+    import numpy as np
+    from sparseconvnet import _lib
+    from sparseconvnet._lib import ptr
+    rng = np.random.default_rng(n + end_bit)
+    if span:
+        keys = rng.integers(0, span, n, dtype=np.uint64)
+    else:
+        keys = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    keys[rng.random(n) < 0.01] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    masked = keys & np.uint64((1 << end_bit) - 1) if end_bit < 64 else keys
+    order = np.argsort(masked, kind="stable")
+    kin = torch.from_numpy(keys.view(np.int64)).to(DEV)
+    vin = torch.arange(n, dtype=torch.int32, device=DEV)
+    kout, vout = torch.empty_like(kin), torch.empty_like(vin)
+    wsb = int(_lib.query("msp_sort_workspace_size", n, end_bit))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+    _lib.call("msp_sort_pairs", ptr(kin), ptr(kout), ptr(vin), ptr(vout), n, end_bit, ptr(ws), wsb, _lib.stream())
+    assert np.array_equal(vout.cpu().numpy(), order.astype(np.int32))
+    assert np.array_equal(kout.cpu().numpy().view(np.uint64), keys[order])

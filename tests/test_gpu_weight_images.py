@@ -138,3 +138,37 @@ def test_weight_images_in_a_captured_step():
         _same(model, twin, opts)
     finally:
         scn.weight_images.disable()
+
+
+def test_replaced_storage_drops_its_images():
+    """A parameter whose storage is replaced after its images were recorded (`p.data = ...`) loses them at the next
+    prepare(): no split reads the old buffer, the convolutions split the new weights, and the results equal a
+    model that never had images."""
+    model, xs, ys = _model()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    images = scn.weight_images.enable(model, optimizer=opt)
+    try:
+        for k in range(2):
+            images.prepare()
+            opt.zero_grad(set_to_none=True)
+            logits, _ = model((xs[k % 2], None), istrain=True)
+            F.multilabel_soft_margin_loss(logits, ys[k % 2]).backward()
+            opt.step()
+        n0 = len(images.entries)
+        conv = next(m for m in model.modules() if isinstance(m, scn.SubmanifoldConvolution) and m.nIn == 32)
+        old_ptr = conv.weight.data_ptr()
+        conv.weight.data = conv.weight.data.clone() * 1.5   # new storage; the old one is freed
+        assert conv.weight.data_ptr() != old_ptr
+        images.prepare()
+        assert len(images.entries) < n0
+        assert all(e[0].wt != old_ptr for e in images.entries.values())
+        twin = copy.deepcopy(model)
+        scn.weight_images._ACTIVE = images
+        with torch.no_grad():
+            a, _ = model((xs[0], None), istrain=True)
+        scn.weight_images._ACTIVE = None
+        with torch.no_grad():
+            b, _ = twin((xs[0], None), istrain=True)
+        assert torch.equal(a, b)
+    finally:
+        scn.weight_images.disable()
