@@ -152,9 +152,20 @@ def call(name, *args):
             raise RuntimeError(f"{name}: device fault after this call: {e}") from e
 
 
+_QUERIES = {}
+
+
 def query(name, *args):
-    """Invoke a size/capacity query that returns a value."""
-    return getattr(load(), name)(*args)
+    """Invoke a size/capacity query that returns a value.  The queries are pure functions of their arguments
+    (the device's CU count aside), so results are memoised: a training step asks the same few hundred
+    questions every step, at a ctypes round trip each."""
+    key = (name,) + tuple(a.value if isinstance(a, ctypes._SimpleCData) else a for a in args)
+    r = _QUERIES.get(key)
+    if r is None:
+        if len(_QUERIES) > 1 << 16:
+            _QUERIES.clear()
+        r = _QUERIES[key] = getattr(load(), name)(*args)
+    return r
 
 
 # --------------------------------------------------------------- GPU event hooks

@@ -206,12 +206,14 @@ def test_join_table(ca, cb):
     coords, feats = _inputs(5000, 24, n_feat=ca)
     torch.manual_seed(ca + cb)
     outs = []
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    b0 = torch.randn(t.features.size(0), cb, device=DEV)
+    g = torch.randn(t.features.size(0), ca + cb, device=DEV)
     for fuse in (True, False):
         M.FUSE_RESIDUAL = fuse
         try:
-            t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
             a = t.features.detach().clone().requires_grad_(True)
-            b = torch.randn(a.size(0), cb, device=DEV, requires_grad=True)
+            b = b0.clone().requires_grad_(True)
             ta = scn.SparseConvNetTensor(a, t.metadata, t.spatial_size)
             tb = scn.SparseConvNetTensor(b, t.metadata, t.spatial_size)
             j = scn.JoinTable().train()([ta, tb])
@@ -219,7 +221,6 @@ def test_join_table(ca, cb):
             assert (getattr(j, "_bn_partial", None) is not None) == fuse
             bn = scn.BatchNormReLU(ca + cb).to(DEV)
             y = bn(j).features
-            g = torch.randn_like(y)
             y.backward(g)
             outs.append((y.detach(), a.grad, b.grad, bn.weight.grad, bn.running_mean.clone(), bn.running_var.clone()))
         finally:
