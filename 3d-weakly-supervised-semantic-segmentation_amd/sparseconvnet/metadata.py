@@ -61,8 +61,9 @@ def tile_rulebook(m, K, n, device, s, tile_rows=64):
 LOCAL_TILE_ROWS = 128
 
 
-def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS):
-    """msp_tile_local: count (one host read of the total), then fill."""
+def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS, lists_only=False):
+    """msp_tile_local: count (one host read of the total), then fill (lists_only: the distinct-row lists
+    without the row grouping and local indices, for the chunk-local weight gradient alone)."""
     T = int(tile_rows)
     n_tiles = (n + T - 1) // T
     u_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=device)
@@ -70,6 +71,11 @@ def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS):
     call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), None, 0, None, None, None, ptr(ws), ws.numel(), s)
     total, max_u = (int(v) for v in u_start[n_tiles:].tolist()) if n_tiles else (0, 0)
     u_rows = torch.empty(max(total, 1), dtype=torch.int32, device=device)
+    if lists_only:
+        if n_tiles:
+            call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), ptr(u_rows), max(total, 1), None, None, None,
+                 ptr(ws), ws.numel(), s)
+        return dict(u_start=u_start, u_rows=u_rows, tile_rows=T, n_tiles=n_tiles, total=total, max_u=max_u)
     lidx = torch.empty((K, max(n_tiles * T, 1)), dtype=torch.int16, device=device)  # uint16 bits
     perm = torch.empty(max(n_tiles * T, 1), dtype=torch.int32, device=device)
     # conv_x6s's per-tile offset lists (128-row tiles, K <= 27)
@@ -189,12 +195,24 @@ class SubmRules:
                                                          _lib.stream(self.nbr.device), tile_rows)
         return t
 
+    def lists(self, tile_rows=LOCAL_TILE_ROWS):
+        """Each tile's sorted distinct input rows (the tile-local rulebook's u_start / u_rows): the full
+        rulebook's when a tile-local convolution built it, else a lists-only build (no row grouping)."""
+        t = self._locals.get(tile_rows)
+        if t is None:
+            t = self.__dict__.setdefault("_lists", {}).get(tile_rows)
+        if t is None:
+            self._plan.append(("lists", self._key, tile_rows))
+            t = self._lists[tile_rows] = local_rulebook(self.nbr, self.K, self._n, self.nbr.device,
+                                                        _lib.stream(self.nbr.device), tile_rows, lists_only=True)
+        return t
+
     def wgrad_index(self):
-        """msp_wgrad_chunk_index over the 128-row tile rulebook and the tile-local rulebook (which lists each
-        tile's distinct input rows) for msp_conv_wgrad_chunk, built on first use.  None when a tile names more
-        distinct rows than the kernel stages (msp_wgrad_chunk_cap): the pair lists serve then."""
+        """msp_wgrad_chunk_index over the 128-row tile rulebook and the tile-local lists of each tile's distinct
+        input rows for msp_conv_wgrad_chunk, built on first use.  None when a tile names more distinct rows than
+        the kernel stages (msp_wgrad_chunk_cap): the pair lists serve then."""
         if self._wchunk is None:
-            loc = self.local()
+            loc = self.lists()
             if loc["max_u"] > int(query("msp_wgrad_chunk_cap")):
                 self._wchunk = False
             else:
@@ -424,7 +442,7 @@ class Metadata:
         for entry in plan:
             # what the recorded uses select is rebuilt by ops.prepare; pair lists too (the weight gradient falls
             # back to them only when its chunk form does not fit, the strided consumers record a "pairs" use)
-            if entry[0] in ("tiles", "dense", "local", "wchunk", "pairs") and entry[1] in used:
+            if entry[0] in ("tiles", "dense", "local", "lists", "wchunk", "pairs") and entry[1] in used:
                 continue
             if entry[0] == "use":
                 rules = self._rules(entry[1])
@@ -440,6 +458,8 @@ class Metadata:
                 self._rules(entry[1]).dense_order()
             elif entry[0] == "local":
                 self._rules(entry[1]).local(entry[2])
+            elif entry[0] == "lists":
+                self._rules(entry[1]).lists(entry[2])
             elif entry[0] == "wchunk":
                 self._rules(entry[1]).wgrad_index()
             elif entry[0] == "pairs":

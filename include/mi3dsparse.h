@@ -143,6 +143,8 @@ int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64
  * Count-then-fill like msp_pair_lists: the counting call (u_cap = 0) writes
  * u_start[0..n_tiles] (u_start[n_tiles] = total) and u_start[n_tiles+1] = the
  * largest tile's count; the filling call (u_cap >= total) reuses u_start.
+ * A filling call with lidx = perm = NULL writes the lists only (u_rows: all
+ * msp_conv_wgrad_chunk needs; no row grouping, the bulk of the fill). 
  * Workspace: msp_tile_local_workspace_size. */
 size_t msp_tile_local_workspace_size(int64_t n, int tile_rows);
 int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t* u_start, int32_t* u_rows,

@@ -9,7 +9,7 @@ TAG=${TAG:-ab}
 ROUNDS=${ROUNDS:-2}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-EXP=$GRAFT_REPO_ROOT/3d-weakly-supervised-semantic-segmentation_amd/lib/libmi3dsparse_exp.so
+EXP=${EXP_LIB:-$GRAFT_REPO_ROOT/3d-weakly-supervised-semantic-segmentation_amd/lib/libmi3dsparse_exp.so}
 : > gpurun_out/ab_$TAG.log
 for i in $(seq 1 $ROUNDS); do
   for v in A B; do

@@ -4,7 +4,8 @@ Runs the bench's C3 workload (SparseConvUNet m=32 r=2 residual, 8 scenes at 2 cm
 Adam, prefetched metadata) and, after warm-up, measures (1) the host enqueue time of each phase with the
 device drained before the phase (so the number is host dispatch cost, not back-pressure from a full launch
 queue) next to the device time of the same phase (events), and (2) a cProfile of one synchronised step,
-top entries by own time.  Usage: python scripts/host_profile.py  (env STEPS, TOP)."""
+top entries by own time.  Usage: python scripts/host_profile.py  (env STEPS, TOP; PRESET=c2 for configs[1]:
+m=16, one block per level, VGG blocks, 4 scenes)."""
 import cProfile
 import io
 import os
@@ -26,13 +27,15 @@ from wsss3d.synthetic import make_batch  # noqa: E402
 _lib.load()
 dev = torch.device("cuda:0")
 batches = []
+PRESET = os.environ.get("PRESET", "c3")
+M, REPS, RES, SCENES = (16, 1, False, 4) if PRESET == "c2" else (32, 2, True, 8)
 for k in range(2):
-    b = make_batch(8, 50, seed=k)
+    b = make_batch(SCENES, 50, seed=k)
     x = EasyDict(coords=torch.from_numpy(b["coords"]).to(dev), feature=torch.from_numpy(b["feats"]).to(dev),
                  batch_offsets=b["batch_offsets"])
     batches.append((x, torch.from_numpy(b["scene_labels"]).to(dev)))
 torch.manual_seed(0)
-pc = EasyDict(name="SparseConvUNet", m=32, dimension=3, full_scale=4096, block_reps=2, residual_blocks=True)
+pc = EasyDict(name="SparseConvUNet", m=M, dimension=3, full_scale=4096, block_reps=REPS, residual_blocks=RES)
 cls, _ = MODEL_REGISTRY.get("MultiLabel")
 model = cls(pc).to(dev)
 opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
