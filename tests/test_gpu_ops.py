@@ -733,6 +733,10 @@ def test_tile_local_rulebook_maps(T, K, mode):
     _check_local_rulebook(nbr, loc, V)
     if mode == "distinct":
         assert loc["max_u"] == K * T
+    # lists only (msp_tile_local with lidx = perm = NULL: what the chunk-local weight gradient reads at level 0)
+    lst = metadata.local_rulebook(nbr, K, V, nbr.device, _lib.stream(), T, lists_only=True)
+    assert lst["total"] == loc["total"] and lst["max_u"] == loc["max_u"]
+    assert torch.equal(lst["u_start"], loc["u_start"]) and torch.equal(lst["u_rows"], loc["u_rows"])
 
 
 @pytest.mark.parametrize("cin,cout,flip", [(64, 64, 2), (64, 64, 1), (96, 96, 2), (192, 96, 1), (48, 64, 2),
