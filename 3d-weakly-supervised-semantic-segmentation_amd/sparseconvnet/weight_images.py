@@ -43,26 +43,41 @@ class WeightImages:
         self.dirty = False
         self.table = None  # (descs device tensor, starts device tensor, n, total units)
         self.hits = 0      # calls that found their image prepared
+        self._descs = {}   # (entry, n_rows, K, c_in, c_out, flip) -> descriptor template (or False)
         self.valid = False  # prepare() ran after the last optimizer step
 
     # ------------------------------------------------------------------ per call
+    def _describe(self, entry, n_rows, K, c_in, c_out, flip):
+        """msp_conv_weight_image for these arguments (memoised: a pure function of them)."""
+        k = (entry, n_rows, K, c_in, c_out, flip)
+        d = self._descs.get(k)
+        if d is None:
+            d = _lib.WeightImage()
+            if _lib.load().msp_conv_weight_image(entry, n_rows, K, c_in, c_out, int(flip), ctypes.byref(d)):
+                d = False
+            if len(self._descs) > 1 << 14:
+                self._descs.clear()
+            self._descs[k] = d
+        return d or None
+
     def lookup(self, entry, wt, n_rows, K, c_in, c_out, flip):
         """The prepared image tensor for this call, or None (the call then splits its own)."""
         owner = self.owners.get(wt.untyped_storage().data_ptr())
         if owner is None:
             return None
-        d = _lib.WeightImage()
-        if _lib.load().msp_conv_weight_image(entry, n_rows, K, c_in, c_out, int(flip), ctypes.byref(d)):
+        d0 = self._describe(entry, n_rows, K, c_in, c_out, flip)
+        if d0 is None:
             return None
-        key = (wt.data_ptr(), tuple(wt.shape), d.kind, d.p, d.wlay, d.K, d.c_in, d.c_out)
+        key = (wt.data_ptr(), tuple(wt.shape), d0.kind, d0.p, d0.wlay, d0.K, d0.c_in, d0.c_out)
         e = self.entries.get(key)
         if e is None:
+            d = _lib.WeightImage.from_buffer_copy(d0)  # the entry's own descriptor (wt / img filled in)
             d.wt = wt.data_ptr()
             self.entries[key] = [d, owner, None, None, owner.untyped_storage().data_ptr()]
             self.dirty = True
             return None
         desc, _, img, version, _ = e
-        if not self.valid or img is None or version is None or version != wt._version or img.numel() < d.bytes:
+        if not self.valid or img is None or version is None or version != wt._version or img.numel() < d0.bytes:
             return None
         self.hits += 1
         return img
