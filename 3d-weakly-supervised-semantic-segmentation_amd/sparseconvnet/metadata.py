@@ -509,6 +509,10 @@ class Metadata:
 _PREFETCHED = {}
 _SIDE = {}
 _CAPTURED = []
+# Priority of the prefetch stream (torch convention: -1 high, 0 default).  The build is a chain of small kernels
+# and count reads that the host waits on, running beside a step that fills the GPU; at default priority each of
+# its kernels queues behind the step's workgroups (bench.py --prefetch-priority).
+PREFETCH_PRIORITY = 0
 
 
 def _coords_key(coords, spatial_size):
@@ -526,7 +530,7 @@ def prefetch(coords, spatial_size, plan, wait_for_producer=True):
     _PREFETCHED.pop(dev.index, None)  # an unconsumed older entry is dropped (its memory goes back)
     side = _SIDE.get(dev.index)
     if side is None:
-        side = _SIDE[dev.index] = torch.cuda.Stream(dev)
+        side = _SIDE[dev.index] = torch.cuda.Stream(dev, priority=PREFETCH_PRIORITY)
     cur = torch.cuda.current_stream(dev)
     if isinstance(wait_for_producer, torch.cuda.Event):
         side.wait_event(wait_for_producer)

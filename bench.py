@@ -294,6 +294,12 @@ def main():
                          "(sparseconvnet.ops.WGRAD_SIDE_ROWS; 0 = never)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="build each batch's metadata inside its own forward (no side-stream input pipelining)")
+    ap.add_argument("--prefetch-priority", type=int, choices=[0, 1], default=0,
+                    help="1: the metadata prefetch on a high-priority stream (its small kernels and the count reads "
+                         "the host waits on no longer queue behind the running step's workgroups)")
+    ap.add_argument("--prefetch-lag", type=int, choices=[1, 2], default=1,
+                    help="graph mode: the metadata build of batch i + 1 waits for step i - lag's graph (1: the host "
+                         "runs at most one step ahead; 2: two)")
     ap.add_argument("--prefetch-at", choices=["end", "fwd"], default="end",
                     help="when the next batch's metadata is built: after the step's optimizer call is queued (end) "
                          "or right after its forward is queued (fwd: the build's host reads overlap the forward)")
@@ -355,6 +361,8 @@ def main():
 
     _lib.load()
     from sparseconvnet import ops as scn_ops
+    from sparseconvnet import metadata as scn_md
+    scn_md.PREFETCH_PRIORITY = -1 if args.prefetch_priority else 0
     scn_ops.WGRAD_CONCURRENT = bool(args.concurrent_wgrad)
     if args.wgrad_side_rows is not None:
         scn_ops.WGRAD_SIDE_ROWS = args.wgrad_side_rows
@@ -552,17 +560,17 @@ def main():
     bounds[0].record(cur)
     t0 = time.perf_counter()
     if use_graph:
-        inflight, done_prev = [], None
+        inflight, dones = [], []
         for i in range(args.steps):
             h0 = time.perf_counter()
             done = replay(entry)
             bounds.append(done)
             inflight.append((entry, done, i))
             h1 = time.perf_counter()
-            # batch i + 1 on the side stream, after step i - 1's graph on the device: the build's count reads
-            # pace the host (at most one step ahead: step i is queued while step i + 1 is captured)
-            prefetch(i, done_prev)
-            done_prev = done
+            # batch i + 1 on the side stream, after step i - lag's graph on the device: the build's count reads
+            # pace the host (lag 1: at most one step ahead -- step i is queued while step i + 1 is captured)
+            prefetch(i, dones[-args.prefetch_lag] if len(dones) >= args.prefetch_lag else None)
+            dones.append(done)
             h2 = time.perf_counter()
             # the step's metadata is released now (its tensors were marked as used by the compute stream); the
             # graphs themselves are kept until the loop has drained: destroying an executable graph here
