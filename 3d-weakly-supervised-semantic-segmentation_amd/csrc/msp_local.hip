@@ -203,12 +203,15 @@ __device__ void group_rows(const uint32_t* __restrict__ msk, int nv, uint8_t* __
 // = 4 x groups + 1 per offset; at most 8 offsets a wave).  Interleaving the halves over the groups evens them
 // out, and the lists even out the waves: the slowest of the 8 waves carries 0.94 of the mean against 0.86 for
 // offsets dealt round-robin (headline batch, levels 1-3).  wo[h][c][k]: offset k of wave c (0xFF: none).
+#ifndef MSP_SHARED_LISTS  // experiments: 1 = both halves walk one list dealt from all 8 groups (their weight loads
+#define MSP_SHARED_LISTS 0  // then coincide, which the vector L1 can serve once)
+#endif
 __device__ void deal_offsets(const uint32_t* __restrict__ gmask, int K, int h, uint8_t* __restrict__ item,
                              int* __restrict__ cost, uint8_t* __restrict__ wo) {
   int n = 0;  // item / cost: this half's LDS scratch, the offsets by cost descending (ties: lower offset first)
   for (int o = 0; o < K; ++o) {
     int a = 0;
-    for (int g = h; g < 8; g += 2) a += (gmask[g] >> o) & 1u;
+    for (int g = MSP_SHARED_LISTS ? 0 : h; g < 8; g += MSP_SHARED_LISTS ? 1 : 2) a += (gmask[g] >> o) & 1u;
     if (a == 0) continue;
     int i = n++;
     while (i > 0 && cost[i - 1] < a) {

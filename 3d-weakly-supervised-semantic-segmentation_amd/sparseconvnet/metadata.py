@@ -15,11 +15,15 @@ the kernels of libmi3dsparse:
                    child map down[K][Vc] + its tile rulebook and pair lists
 
 The only device->host reads are the counts that size the next allocation
-(V per level, rulebook chunk totals, per-offset list starts).
+(V per level, rulebook chunk totals, per-offset list starts).  A replay (the
+prefetch of the next batch) defers the rulebook counts and reads them together:
+one read per coarsening (its V, with every count queued before it) and one at
+the end, instead of one per rulebook.
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -37,54 +41,119 @@ def _log2_ceil(n: int) -> int:
     return max(1, int(math.ceil(math.log2(max(2, int(n))))))
 
 
+class _Deferred:
+    """The count reads of one replay, batched.  read(t, fn) queues fn(values of the int64 device tensor t);
+    then(fn) queues work that needs every queued read applied; flush() applies them with one device->host copy
+    per round (reads first, then the dependent work, until neither is left), on the stream the build runs on --
+    so a flush forced from elsewhere still orders the copy after the counting kernels."""
+
+    def __init__(self, stream):
+        self.stream = stream
+        self.reads, self.after = [], []
+
+    def read(self, t, fn):
+        self.reads.append((t, fn))
+
+    def then(self, fn):
+        self.after.append(fn)
+
+    def flush(self):
+        with torch.cuda.stream(self.stream):
+            while self.reads or self.after:
+                if self.reads:
+                    reads, self.reads = self.reads, []
+                    flat = (reads[0][0] if len(reads) == 1 else torch.cat([t.reshape(-1) for t, _ in reads])).tolist()
+                    k = 0
+                    for t, fn in reads:
+                        fn([int(v) for v in flat[k:k + t.numel()]])
+                        k += t.numel()
+                else:
+                    after, self.after = self.after, []
+                    for fn in after:
+                        fn()
+
+
+_DEFER = None   # the _Deferred of the replay in progress (None: every count is read where it is taken)
+# MSP_DEFER_READS=0: a replay reads every count where it is taken, as an inline build does (A/B switch)
+DEFER_READS = os.environ.get("MSP_DEFER_READS", "1") != "0"
+
+
+def _later(t, fn):
+    """fn(values of the int64 device tensor t): now, or at the next flush of the replay in progress."""
+    if _DEFER is None:
+        fn([int(v) for v in t.tolist()])
+    else:
+        _DEFER.read(t, fn)
+
+
+def _resolve():
+    if _DEFER is not None:
+        _DEFER.flush()
+
+
 def tile_rulebook(m, K, n, device, s, tile_rows=64):
     """Output-tile rulebook of an offset-major map m[K][n] (two passes:
-    count, then fill; one host read of the chunk total)."""
+    count, then fill, sized by one host read of the chunk total -- deferred in a replay: the
+    dict has its chunk arrays once the replay's counts are read)."""
     tr = int(tile_rows)
     n_tiles = (n + tr - 1) // tr
     # tile_start[n_tiles + 1] = largest chunk count of one tile
     tile_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=device)
     ws = _ws((n_tiles + 1) * 8 + query("msp_scan_workspace_size", I64(n_tiles)), device)
     call("msp_tile_rulebook", ptr(m), K, n, tr, ptr(tile_start), None, None, None, 0, ptr(ws), ws.numel(), s)
-    n_chunks, max_chunks = (int(v) for v in tile_start[n_tiles:].tolist())
-    chunk_off = torch.empty(max(n_chunks, 1), dtype=torch.uint8, device=device)
-    chunk_src = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int32, device=device)
-    # uint16 row-in-tile; stored in an int16 tensor (same bytes, rows < 2^15)
-    chunk_row = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int16, device=device)
-    if n_chunks:
-        call("msp_tile_rulebook", ptr(m), K, n, tr, ptr(tile_start), ptr(chunk_off), ptr(chunk_src), ptr(chunk_row),
-             n_chunks, ptr(ws), ws.numel(), s)
-    return dict(tile_start=tile_start, chunk_off=chunk_off, chunk_src=chunk_src, chunk_row=chunk_row,
-                n_chunks=n_chunks, tile_rows=tr, max_chunks=max_chunks)
+    out = dict(tile_start=tile_start, tile_rows=tr)
+
+    def fill(counts):
+        n_chunks, max_chunks = counts
+        chunk_off = torch.empty(max(n_chunks, 1), dtype=torch.uint8, device=device)
+        chunk_src = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int32, device=device)
+        # uint16 row-in-tile; stored in an int16 tensor (same bytes, rows < 2^15)
+        chunk_row = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int16, device=device)
+        if n_chunks:
+            call("msp_tile_rulebook", ptr(m), K, n, tr, ptr(tile_start), ptr(chunk_off), ptr(chunk_src),
+                 ptr(chunk_row), n_chunks, ptr(ws), ws.numel(), s)
+        out.update(chunk_off=chunk_off, chunk_src=chunk_src, chunk_row=chunk_row, n_chunks=n_chunks,
+                   max_chunks=max_chunks)
+    _later(tile_start[n_tiles:], fill)
+    return out
 
 
 LOCAL_TILE_ROWS = 128
 
 
 def local_rulebook(nbr, K, n, device, s, tile_rows=LOCAL_TILE_ROWS, lists_only=False):
-    """msp_tile_local: count (one host read of the total), then fill (lists_only: the distinct-row lists
-    without the row grouping and local indices, for the chunk-local weight gradient alone)."""
+    """msp_tile_local: count (one host read of the total, deferred in a replay), then fill (lists_only: the
+    distinct-row lists without the row grouping and local indices, for the chunk-local weight gradient alone)."""
     T = int(tile_rows)
     n_tiles = (n + T - 1) // T
     u_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=device)
     ws = _ws(query("msp_tile_local_workspace_size", I64(n), T), device)
     call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), None, 0, None, None, None, ptr(ws), ws.numel(), s)
-    total, max_u = (int(v) for v in u_start[n_tiles:].tolist()) if n_tiles else (0, 0)
-    u_rows = torch.empty(max(total, 1), dtype=torch.int32, device=device)
-    if lists_only:
+    out = dict(u_start=u_start, tile_rows=T, n_tiles=n_tiles)
+
+    def fill(counts):
+        total, max_u = counts
+        u_rows = torch.empty(max(total, 1), dtype=torch.int32, device=device)
+        out.update(u_rows=u_rows, total=total, max_u=max_u)
+        if lists_only:
+            if n_tiles:
+                call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), ptr(u_rows), max(total, 1), None, None,
+                     None, ptr(ws), ws.numel(), s)
+            return
+        lidx = torch.empty((K, max(n_tiles * T, 1)), dtype=torch.int16, device=device)  # uint16 bits
+        perm = torch.empty(max(n_tiles * T, 1), dtype=torch.int32, device=device)
+        # conv_x6s's per-tile offset lists (128-row tiles, K <= 27)
+        wave_off = torch.empty(max(n_tiles * 64, 1), dtype=torch.uint8, device=device) \
+            if T == 128 and K <= 27 else None
         if n_tiles:
-            call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), ptr(u_rows), max(total, 1), None, None, None,
-                 ptr(ws), ws.numel(), s)
-        return dict(u_start=u_start, u_rows=u_rows, tile_rows=T, n_tiles=n_tiles, total=total, max_u=max_u)
-    lidx = torch.empty((K, max(n_tiles * T, 1)), dtype=torch.int16, device=device)  # uint16 bits
-    perm = torch.empty(max(n_tiles * T, 1), dtype=torch.int32, device=device)
-    # conv_x6s's per-tile offset lists (128-row tiles, K <= 27)
-    wave_off = torch.empty(max(n_tiles * 64, 1), dtype=torch.uint8, device=device) if T == 128 and K <= 27 else None
+            call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), ptr(u_rows), max(total, 1), ptr(lidx),
+                 ptr(perm), ptr(wave_off) if wave_off is not None else None, ptr(ws), ws.numel(), s)
+        out.update(lidx=lidx, perm=perm, wave_off=wave_off)
     if n_tiles:
-        call("msp_tile_local", ptr(nbr), K, n, T, ptr(u_start), ptr(u_rows), max(total, 1), ptr(lidx), ptr(perm),
-             ptr(wave_off) if wave_off is not None else None, ptr(ws), ws.numel(), s)
-    return dict(u_start=u_start, u_rows=u_rows, lidx=lidx, perm=perm, wave_off=wave_off, tile_rows=T,
-                n_tiles=n_tiles, total=total, max_u=max_u)
+        _later(u_start[n_tiles:], fill)
+    else:
+        fill((0, 0))
+    return out
 
 
 class PairLists:
@@ -106,23 +175,35 @@ class PairLists:
         ws = _ws((2 * mm + 1) * 8 + query("msp_scan_workspace_size", I64(mm)), device)
         self.off_start = torch.empty(K + 1, dtype=torch.int64, device=device)
         call("msp_pair_lists", ptr(m), K, n, None, None, 0, ptr(self.off_start), ptr(ws), ws.numel(), s)
-        starts = self.off_start.tolist()
-        self.total = int(starts[-1])
-        self.counts = [starts[o + 1] - starts[o] for o in range(K)]
         # the filling call reuses the count's workspace (kept: a fill captured into a graph reads it at replay)
         self._m, self._n, self._ws, self._dev = m, n, ws, device
         self._plan, self._key = plan, key
         self._pin = self._pout = None
         self.K = K
+        _later(self.off_start, self._counted)
+
+    def _counted(self, starts):
+        self.total = starts[-1]
+        self.counts = [starts[o + 1] - starts[o] for o in range(self.K)]
         # 16-pair chunks per offset (msp_conv_pairs)
         cs = [0]
         for c in self.counts:
             cs.append(cs[-1] + (c + CHUNK - 1) // CHUNK)
         self.n_chunks = cs[-1]
-        self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(device, non_blocking=True)
+        self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(self._dev, non_blocking=True)
+
+    def __getattr__(self, name):
+        # a count still queued in the replay in progress: read it now
+        if name in ("total", "counts", "n_chunks", "chunk_start") and _DEFER is not None:
+            _DEFER.flush()
+            return object.__getattribute__(self, name)
+        raise AttributeError(name)
 
     def fill(self):
         if self._pin is None:
+            if "total" not in self.__dict__:   # counted in a replay, not read yet: fill once it is
+                _DEFER.then(self.fill)
+                return self
             if self._plan is not None:
                 self._plan.append(("pairs", self._key))
             pin = torch.empty(max(self.total, 1), dtype=torch.int32, device=self._dev)
@@ -163,7 +244,10 @@ class SubmRules:
         self._dense = None
         self._map, self._n = self.nbr, V
         self.pairs = PairLists(self.nbr, K, V, dev, s, self._plan, self._key)
-        self.n_rules = self.pairs.total  # = SCN rulebook size (centre included)
+
+    @property
+    def n_rules(self):
+        return self.pairs.total  # = SCN rulebook size (centre included)
 
     def dense_order(self):
         """(perm, permuted neighbour map) for the dense row-group convolution
@@ -213,17 +297,29 @@ class SubmRules:
         the kernel stages (msp_wgrad_chunk_cap): the pair lists serve then."""
         if self._wchunk is None:
             loc = self.lists()
-            if loc["max_u"] > int(query("msp_wgrad_chunk_cap")):
+            if "max_u" in loc and loc["max_u"] > int(query("msp_wgrad_chunk_cap")):
                 self._wchunk = False
-            else:
-                tiles = self.tiles_for(128)
-                self._plan.append(("wchunk", self._key))
-                lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=self.nbr.device)
-                if self._n:  # no rule can lie past the cap (checked above): no overflow count needed
-                    call("msp_wgrad_chunk_index", ptr(tiles["tile_start"]), ptr(tiles["chunk_src"]),
-                         ptr(tiles["chunk_row"]), I64(self._n), ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(lr),
-                         None, _lib.stream(self.nbr.device))
-                self._wchunk = dict(tiles=tiles, chunk_lr=lr, u_start=loc["u_start"], u_rows=loc["u_rows"])
+                return None
+            tiles = self.tiles_for(128)
+            if "max_u" not in loc or "n_chunks" not in tiles:
+                # in a replay, counts not read yet (the tiles are asked for before the lists' count is known: one
+                # read for both, the tiles unused in the rare batch whose lists exceed the cap): decide -- chunk
+                # index, else pair lists -- once they are read
+                self._wchunk = "pending"
+
+                def decide():
+                    self._wchunk = None
+                    if self.wgrad_index() is None:
+                        self.pairs.fill()
+                _DEFER.then(decide)
+                return self._wchunk
+            self._plan.append(("wchunk", self._key))
+            lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=self.nbr.device)
+            if self._n:  # no rule can lie past the cap (checked above): no overflow count needed
+                call("msp_wgrad_chunk_index", ptr(tiles["tile_start"]), ptr(tiles["chunk_src"]),
+                     ptr(tiles["chunk_row"]), I64(self._n), ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(lr),
+                     None, _lib.stream(self.nbr.device))
+            self._wchunk = dict(tiles=tiles, chunk_lr=lr, u_start=loc["u_start"], u_rows=loc["u_rows"])
         return self._wchunk or None
 
     def note_use(self, purpose, c_in, c_out):
@@ -402,7 +498,10 @@ class Metadata:
         ws = _ws(((n + 2047) // 2048 + 1) * 8, dev)
         call("msp_segment", ptr(fine.keys), n, 3 * k, None, ptr(parent), None, ptr(uniq), ptr(cstart), ptr(nu),
              ptr(ws), ws.numel(), s)
-        Vc = int(nu.item())
+        got = []
+        _later(nu, got.extend)
+        _resolve()   # in a replay: one read for Vc and every count queued since the last one
+        Vc = got[0]
         csize = fine.size // stride
         coarse = self.levels.get(csize)
         if coarse is None:
@@ -433,10 +532,21 @@ class Metadata:
 
     def replay(self, plan):
         """Build, in order, the rulebooks another forward of the same network
-        requested (its `plan`); later requests then find them built.  Rules
-        with recorded uses ("use": a convolution or weight gradient and its
+        requested (its `plan`); later requests then find them built (their count reads batched:
+        _Deferred).  Rules with recorded uses ("use": a convolution or weight gradient and its
         channel counts) get what those uses select for this batch's sizes
         (ops.prepare) instead of the concrete rulebooks the other batch built."""
+        global _DEFER
+        if not DEFER_READS:
+            return self._replay(plan)
+        outer, _DEFER = _DEFER, _Deferred(torch.cuda.current_stream(self.device))
+        try:
+            self._replay(plan)
+            _DEFER.flush()
+        finally:
+            _DEFER = outer
+
+    def _replay(self, plan):
         from . import ops
         used = {e[1] for e in plan if e[0] == "use"}
         for entry in plan:

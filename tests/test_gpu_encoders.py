@@ -192,6 +192,69 @@ def test_metadata_prefetch_matches_inline():
         assert torch.equal(a, b)
 
 
+def test_prefetch_batches_count_reads():
+    """A replay reads its rulebook counts together (metadata._Deferred): the prefetch synchronises the host
+    with the device twice for the voxelisation, once per coarsening and once at the end, and every rulebook it
+    built -- tile, tile-local and pair-list counts -- equals the one an inline build of the same batch makes."""
+    import warnings
+    from sparseconvnet import metadata as md
+    from wsss3d import EasyDict
+    torch.manual_seed(0)
+    cls, _ = MODEL_REGISTRY.get("SparseConvUNet")
+    model = cls("SparseConvUNet", m=16, dimension=3, full_scale=4096, block_reps=1, residual_blocks=True).to(DEV)
+    bs = [make_batch(2, 20, seed=s) for s in (31, 32)]
+    xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(DEV), feature=torch.from_numpy(b["feats"]).to(DEV),
+                   batch_offsets=b["batch_offsets"]) for b in bs]
+    model(xs[0]).square().sum().backward()    # records the plan (forward and backward uses)
+    inline = md.Metadata(DEV)
+    inline.build_input(xs[1].coords, 4096)
+    plan = list(model.encoder[0].last_plan)
+    n_down = sum(1 for e in plan if e[0] == "down")
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("warn")
+    try:
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            m = md.Metadata(DEV)
+            m.build_input(xs[1].coords, 4096)
+            n_input = len(w)
+            m.replay(plan)
+            n_replay = len(w) - n_input
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert n_replay <= n_down + 1, (n_replay, n_down)
+    for e in plan:   # the inline build: the same levels, each count read where it is taken
+        if e[0] == "down":
+            inline.downsample(e[1], e[2])
+        elif e[0] == "subm":
+            inline.level(e[1]).subm_rules(e[2])
+    for size, lvl in m.levels.items():
+        ref = inline.levels[size]
+        assert lvl.n == ref.n and torch.equal(lvl.keys, ref.keys)
+        for fs, r in lvl.subm.items():
+            q = ref.subm[fs]
+            assert r.n_rules == q.n_rules and r.pairs.counts == q.pairs.counts
+            for tr, t in r._tiles.items():
+                u = q.tiles_for(tr)
+                assert t["n_chunks"] == u["n_chunks"] and t["max_chunks"] == u["max_chunks"]
+                for k in ("tile_start", "chunk_off", "chunk_src", "chunk_row"):
+                    assert torch.equal(t[k][:u[k].numel()], u[k]), (size, tr, k)
+            for tr, t in r._locals.items():
+                u = q.local(tr)
+                assert (t["total"], t["max_u"]) == (u["total"], u["max_u"])
+                for k in ("u_start", "u_rows", "lidx", "perm"):
+                    assert torch.equal(t[k], u[k]), (size, tr, k)
+            if r.pairs._pin is not None:
+                assert torch.equal(r.pairs.pair_in, q.pairs.pair_in)
+                assert torch.equal(r.pairs.pair_out, q.pairs.pair_out)
+            if r._wchunk:
+                wq = q.wgrad_index()
+                assert wq is not None and torch.equal(r._wchunk["chunk_lr"], wq["chunk_lr"])
+        for stride, (csize, r) in lvl.down.items():
+            q = ref.down[stride][1]
+            assert r.pairs.counts == q.pairs.counts and torch.equal(r.down, q.down)
+
+
 def _prefetch_model():
     from wsss3d import EasyDict
     torch.manual_seed(0)
