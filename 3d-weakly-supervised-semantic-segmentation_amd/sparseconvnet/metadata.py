@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 
 import torch
 
@@ -62,7 +63,7 @@ class _Deferred:
             while self.reads or self.after:
                 if self.reads:
                     reads, self.reads = self.reads, []
-                    flat = (reads[0][0] if len(reads) == 1 else torch.cat([t.reshape(-1) for t, _ in reads])).tolist()
+                    flat = _host(reads[0][0] if len(reads) == 1 else torch.cat([t.reshape(-1) for t, _ in reads]))
                     k = 0
                     for t, fn in reads:
                         fn([int(v) for v in flat[k:k + t.numel()]])
@@ -73,22 +74,61 @@ class _Deferred:
                         fn()
 
 
-_DEFER = None   # the _Deferred of the replay in progress (None: every count is read where it is taken)
+_TLS = threading.local()  # .defer: this thread's replay in progress (a prefetch may build on a worker thread)
 # MSP_DEFER_READS=0: a replay reads every count where it is taken, as an inline build does (A/B switch)
 DEFER_READS = os.environ.get("MSP_DEFER_READS", "1") != "0"
 
 
+# MSP_PINNED_READS=0: count reads as Tensor.cpu() (A/B switch; see _host)
+PINNED_READS = os.environ.get("MSP_PINNED_READS", "1") != "0"
+
+
+READ_STATS = None  # [seconds, reads]: host time spent in count reads (bench.py BENCH_HOST_TIMING), None: off
+
+
+def _host(t):
+    if READ_STATS is not None:
+        import time
+        t0 = time.perf_counter()
+        v = _host_read(t)
+        READ_STATS[0] += time.perf_counter() - t0
+        READ_STATS[1] += 1
+        return v
+    return _host_read(t)
+
+
+def _host_read(t):
+    """Values of a device tensor as a Python list.  The copy goes into pinned host memory without blocking and
+    the host then waits on an event of the current stream alone (a blocking copy to pageable memory may wait for
+    more than that stream's work).  Both waits let go of the GIL: a prefetch on a worker thread does not hold up
+    the thread capturing a step."""
+    if not PINNED_READS or t.device.type != "cuda":
+        return t.cpu().tolist()
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    ev.synchronize()
+    return h.tolist()
+
+
+def _defer():
+    return getattr(_TLS, "defer", None)
+
+
 def _later(t, fn):
     """fn(values of the int64 device tensor t): now, or at the next flush of the replay in progress."""
-    if _DEFER is None:
-        fn([int(v) for v in t.tolist()])
+    d = _defer()
+    if d is None:
+        fn([int(v) for v in _host(t)])
     else:
-        _DEFER.read(t, fn)
+        d.read(t, fn)
 
 
 def _resolve():
-    if _DEFER is not None:
-        _DEFER.flush()
+    d = _defer()
+    if d is not None:
+        d.flush()
 
 
 def tile_rulebook(m, K, n, device, s, tile_rows=64):
@@ -185,24 +225,24 @@ class PairLists:
     def _counted(self, starts):
         self.total = starts[-1]
         self.counts = [starts[o + 1] - starts[o] for o in range(self.K)]
-        # 16-pair chunks per offset (msp_conv_pairs)
-        cs = [0]
-        for c in self.counts:
-            cs.append(cs[-1] + (c + CHUNK - 1) // CHUNK)
-        self.n_chunks = cs[-1]
-        self.chunk_start = torch.tensor(cs, dtype=torch.int64).to(self._dev, non_blocking=True)
+        # 16-pair chunks per offset (msp_conv_pairs): the starts computed on the device from off_start (a
+        # host-to-device copy from pageable memory would wait for a copy kernel that queues beside the step)
+        self.n_chunks = sum((c + CHUNK - 1) // CHUNK for c in self.counts)
+        cs = torch.zeros(self.K + 1, dtype=torch.int64, device=self._dev)
+        torch.cumsum(torch.div(self.off_start.diff() + (CHUNK - 1), CHUNK, rounding_mode="floor"), 0, out=cs[1:])
+        self.chunk_start = cs
 
     def __getattr__(self, name):
         # a count still queued in the replay in progress: read it now
-        if name in ("total", "counts", "n_chunks", "chunk_start") and _DEFER is not None:
-            _DEFER.flush()
+        if name in ("total", "counts", "n_chunks", "chunk_start") and _defer() is not None:
+            _defer().flush()
             return object.__getattribute__(self, name)
         raise AttributeError(name)
 
     def fill(self):
         if self._pin is None:
             if "total" not in self.__dict__:   # counted in a replay, not read yet: fill once it is
-                _DEFER.then(self.fill)
+                _defer().then(self.fill)
                 return self
             if self._plan is not None:
                 self._plan.append(("pairs", self._key))
@@ -311,7 +351,7 @@ class SubmRules:
                     self._wchunk = None
                     if self.wgrad_index() is None:
                         self.pairs.fill()
-                _DEFER.then(decide)
+                _defer().then(decide)
                 return self._wchunk
             self._plan.append(("wchunk", self._key))
             lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=self.nbr.device)
@@ -431,7 +471,7 @@ class Metadata:
         stats = torch.zeros(3, dtype=torch.int64, device=dev)
         if n:
             call("msp_point_keys", ptr(coords), n, 4, log2, size, ptr(keys), ptr(vals), ptr(stats), s)
-        n_bad, max_b, n_desc = stats.tolist()
+        n_bad, max_b, n_desc = _host(stats)
         if n_bad:
             raise ValueError(f"InputLayer: {n_bad} points outside [0, {size})^3 or with a negative batch index")
         end_bit = min(64, 3 * log2 + max(1, int(max_b).bit_length()))
@@ -456,7 +496,7 @@ class Metadata:
              ptr(ws), ws.numel(), s)
         if monotonic:
             call("msp_batch_starts", ptr(coords), n, 4, n_batch, ptr(tail[1:]), s)
-        got = tail.tolist()
+        got = _host(tail)
         V = int(got[0])
         lvl = Level(size, log2, uniq[:max(V, 1)], V, dev, self.plan)
         self.levels[size] = lvl
@@ -536,15 +576,15 @@ class Metadata:
         _Deferred).  Rules with recorded uses ("use": a convolution or weight gradient and its
         channel counts) get what those uses select for this batch's sizes
         (ops.prepare) instead of the concrete rulebooks the other batch built."""
-        global _DEFER
         if not DEFER_READS:
             return self._replay(plan)
-        outer, _DEFER = _DEFER, _Deferred(torch.cuda.current_stream(self.device))
+        outer = _defer()
+        _TLS.defer = _Deferred(torch.cuda.current_stream(self.device))
         try:
             self._replay(plan)
-            _DEFER.flush()
+            _TLS.defer.flush()
         finally:
-            _DEFER = outer
+            _TLS.defer = outer
 
     def _replay(self, plan):
         from . import ops
@@ -612,16 +652,18 @@ class Metadata:
 # InputLayer forward then finds it ready (its stream waits on an event) and
 # the forward issues no device-to-host reads at all.  Nothing is skipped:
 # each batch's metadata is still built once, inside the step before it.
-# device index -> (coords tensor, its key, Metadata, event): at most one pending
-# entry per device; the entry holds the coords tensor itself and a hit needs the
-# very same tensor object (not just the same address), so freed coords whose
-# memory was handed to a new tensor can never pick up another batch's rulebooks.
+# device index -> [(coords tensor, its key, Metadata, event), ...]: at most PREFETCH_DEPTH pending entries per
+# device (a newer prefetch drops the oldest beyond that); an entry holds the coords tensor itself and a hit needs
+# the very same tensor object (not just the same address), so freed coords whose memory was handed to a new tensor
+# can never pick up another batch's rulebooks.
 _PREFETCHED = {}
 _SIDE = {}
 _CAPTURED = []
-# Priority of the prefetch stream (torch convention: -1 high, 0 default).  The build is a chain of small kernels
-# and count reads that the host waits on, running beside a step that fills the GPU; at default priority each of
-# its kernels queues behind the step's workgroups (bench.py --prefetch-priority).
+_LOCK = threading.Lock()  # _PREFETCHED / _CAPTURED: a prefetch may run on a worker thread beside a capture
+# Pending entries kept per device: 1 (the default) -- the next batch; 2 -- a worker thread prefetches the batch
+# after next while the next one's step is captured (bench.py --prefetch-thread).
+PREFETCH_DEPTH = 1
+BUILD_EVENT_TIMING = False  # True: the build events carry timestamps (bench.py BENCH_HOST_TIMING diagnostics)
 PREFETCH_PRIORITY = 0
 
 
@@ -637,10 +679,13 @@ def prefetch(coords, spatial_size, plan, wait_for_producer=True):
     dev = coords.device
     if dev.type != "cuda":
         raise RuntimeError("sparseconvnet.prefetch: coords must be on a HIP device")
-    _PREFETCHED.pop(dev.index, None)  # an unconsumed older entry is dropped (its memory goes back)
-    side = _SIDE.get(dev.index)
-    if side is None:
-        side = _SIDE[dev.index] = torch.cuda.Stream(dev, priority=PREFETCH_PRIORITY)
+    with _LOCK:
+        pend = _PREFETCHED.setdefault(dev.index, [])
+        # an unconsumed entry for the same coords, and the oldest beyond the depth, are dropped (memory goes back)
+        pend[:] = [e for e in pend if e[0] is not coords][-(PREFETCH_DEPTH - 1):] if PREFETCH_DEPTH > 1 else []
+        side = _SIDE.get(dev.index)
+        if side is None:
+            side = _SIDE[dev.index] = torch.cuda.Stream(dev, priority=PREFETCH_PRIORITY)
     cur = torch.cuda.current_stream(dev)
     if isinstance(wait_for_producer, torch.cuda.Event):
         side.wait_event(wait_for_producer)
@@ -650,9 +695,12 @@ def prefetch(coords, spatial_size, plan, wait_for_producer=True):
         m = Metadata(dev)
         m.build_input(coords, spatial_size)
         m.replay(plan)
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(enable_timing=BUILD_EVENT_TIMING)
         ev.record(side)
-    _PREFETCHED[dev.index] = (coords, _coords_key(coords, spatial_size), m, ev)
+    with _LOCK:
+        pend = _PREFETCHED.setdefault(dev.index, [])
+        pend[:] = [e for e in pend if e[0] is not coords][-(PREFETCH_DEPTH - 1):] if PREFETCH_DEPTH > 1 else []
+        pend.append((coords, _coords_key(coords, spatial_size), m, ev))
     return m
 
 
@@ -662,17 +710,20 @@ def take_prefetched(coords, spatial_size):
     the current stream; None if there is none."""
     if not _PREFETCHED:
         return None
-    hit = _PREFETCHED.get(coords.device.index)
-    if hit is None or hit[0] is not coords or hit[1] != _coords_key(coords, spatial_size):
-        return None
-    del _PREFETCHED[coords.device.index]
+    with _LOCK:
+        pend = _PREFETCHED.get(coords.device.index) or []
+        hit = next((e for e in pend if e[0] is coords), None)
+        if hit is None or hit[1] != _coords_key(coords, spatial_size):
+            return None
+        pend[:] = [e for e in pend if e is not hit]   # by identity (== on the tuples would compare tensors)
     _, _, m, ev = hit
     cur = torch.cuda.current_stream(coords.device)
     if torch.cuda.is_current_stream_capturing():
         # inside a graph capture (bench.py --graph): the replaying stream waits on the build before the graph
         # runs (prefetch_event, taken before the capture), and the Metadata must outlive every replay: it is
         # parked here until the capturer takes it with captured_metadata()
-        _CAPTURED.append(m)
+        with _LOCK:
+            _CAPTURED.append(m)
         return m
     cur.wait_event(ev)
     for t in m.tensors():
@@ -680,16 +731,26 @@ def take_prefetched(coords, spatial_size):
     return m
 
 
+def pending_count():
+    """Prefetched entries not consumed yet, over all devices."""
+    with _LOCK:
+        return sum(len(v) for v in _PREFETCHED.values())
+
+
 def captured_metadata():
     """The Metadata consumed inside graph captures since the last call (the capturer keeps them alive for
     as long as it replays the graph)."""
-    out = list(_CAPTURED)
-    _CAPTURED.clear()
+    with _LOCK:
+        out = list(_CAPTURED)
+        _CAPTURED.clear()
     return out
 
 
-def prefetch_event(device):
-    """The build event of the entry pending on `device` (None if none): a stream that will replay a graph
-    capturing the consumption of that entry must wait on it first."""
-    hit = _PREFETCHED.get(torch.device(device).index)
-    return None if hit is None else hit[3]
+def prefetch_event(device, coords=None):
+    """The build event of the entry pending on `device` for `coords` (None: the newest entry; None if there is
+    none): a stream that will replay a graph capturing the consumption of that entry must wait on it first."""
+    with _LOCK:
+        pend = _PREFETCHED.get(torch.device(device).index) or []
+        if coords is not None:
+            pend = [e for e in pend if e[0] is coords]
+        return pend[-1][3] if pend else None

@@ -60,6 +60,11 @@ FAMILIES = {"wgrad": "wgrad", "nin_wgrad": "wgrad", "wgrad_strided": "wgrad", "w
             "nin_fwd": "nin", "nin_bwd_data": "nin", "bn_fwd": "bn", "bn_bwd": "bn", "bn_join": "bn"}
 
 
+# BENCH_SKIP_DONE_WAIT=1: a replay whose metadata build has already completed (Event.query) issues no stream
+# wait on it (diagnostic: what a cross-stream wait on a completed event costs the compute stream)
+SKIP_DONE_WAIT = os.environ.get("BENCH_SKIP_DONE_WAIT") == "1"
+
+
 def family(kind):
     base = kind.split("/")[0]
     return "conv" if base in CONV_KINDS else FAMILIES.get(base, base)
@@ -300,6 +305,10 @@ def main():
     ap.add_argument("--prefetch-lag", type=int, choices=[1, 2], default=1,
                     help="graph mode: the metadata build of batch i + 1 waits for step i - lag's graph (1: the host "
                          "runs at most one step ahead; 2: two)")
+    ap.add_argument("--prefetch-thread", type=int, choices=[0, 1], default=0,
+                    help="graph mode, 1: the metadata of the batch after next is built on a worker thread while the "
+                         "next step is captured (two prefetched batches pending; the build waits for the step two "
+                         "back); 0: prefetch, then capture, on the loop's thread")
     ap.add_argument("--prefetch-at", choices=["end", "fwd"], default="end",
                     help="when the next batch's metadata is built: after the step's optimizer call is queued (end) "
                          "or right after its forward is queued (fwd: the build's host reads overlap the forward)")
@@ -505,7 +514,7 @@ def main():
         t = time.perf_counter()
         if wimg is not None:
             wimg.build()  # eagerly: images and descriptor table for what the last step added
-        ev = scn_meta.prefetch_event(dev)
+        ev = scn_meta.prefetch_event(dev, batches[i % len(batches)][0].coords)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(cap_stream):
             g.capture_begin(pool=graph_pool, capture_error_mode="relaxed")
@@ -520,16 +529,22 @@ def main():
         return g, keep, ev
 
     replay_ev = []
+    build_ev = []  # BENCH_HOST_TIMING: each replay's metadata build event (when the build finished on the device)
+    if host_t is not None:
+        scn_meta.BUILD_EVENT_TIMING = True
+        scn_meta.READ_STATS = [0.0, 0]
 
     def replay(entry):
         g, keep, ev = entry
-        cur.wait_event(ev)  # the metadata build (side stream) before the graph reads it
+        if not (SKIP_DONE_WAIT and ev.query()):
+            cur.wait_event(ev)  # the metadata build (side stream) before the graph reads it
         for m in keep:
             for t in m.tensors():
                 t.record_stream(cur)
         if host_t is not None:
             replay_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
             replay_ev[-1][0].record(cur)
+            build_ev.append(ev)
         g.replay()
         if gsync is not None:  # N ranks: Adam after the replayed backward (+ the exchange unless captured)
             if not gsync.overlap:
@@ -546,9 +561,16 @@ def main():
     rec = KernelRecorder(args.record if not use_graph else "none", pool=2 * 700 * args.steps)
     _lib.set_recorder(rec if args.record != "none" and not use_graph else None)
     entry = None
+    worker, fut = None, None
+    if use_graph and args.prefetch_thread:
+        from concurrent.futures import ThreadPoolExecutor
+        scn_meta.PREFETCH_DEPTH = 2
+        worker = ThreadPoolExecutor(max_workers=1)
     if use_graph:  # the first step's metadata and graph, before the timed region (as eager's last warm-up does)
         prefetch(-1)
         entry = capture(0)
+        if worker is not None:  # batch 1, on the worker (finished before the timed region, like batch 0)
+            worker.submit(prefetch, 0).result()
     if world > 1:
         dist.barrier()
         if graph_dp:
@@ -567,10 +589,20 @@ def main():
             bounds.append(done)
             inflight.append((entry, done, i))
             h1 = time.perf_counter()
-            # batch i + 1 on the side stream, after step i - lag's graph on the device: the build's count reads
-            # pace the host (lag 1: at most one step ahead -- step i is queued while step i + 1 is captured)
-            prefetch(i, dones[-args.prefetch_lag] if len(dones) >= args.prefetch_lag else None)
-            dones.append(done)
+            if worker is None:
+                # batch i + 1 on the side stream, after step i - lag's graph on the device: the build's count reads
+                # pace the host (lag 1: at most one step ahead -- step i is queued while step i + 1 is captured)
+                prefetch(i, dones[-args.prefetch_lag] if len(dones) >= args.prefetch_lag else None)
+                dones.append(done)
+            else:
+                # batch i + 1 was built on the worker during the last capture; batch i + 2 goes there now, after
+                # step i - 1 on the device, and is built while step i + 1 is captured here (the worker waits for
+                # the device with the GIL released: metadata._host)
+                if fut is not None:
+                    fut.result()
+                dones.append(done)
+                fut = worker.submit(prefetch, i + 1, dones[-2] if len(dones) >= 2 else None) \
+                    if i + 2 <= args.steps else None
             h2 = time.perf_counter()
             # the step's metadata is released now (its tensors were marked as used by the compute stream); the
             # graphs themselves are kept until the loop has drained: destroying an executable graph here
@@ -585,6 +617,8 @@ def main():
             med = [1e3 * statistics.median(c) for c in zip(*host_t[-args.steps:])]
             print(f"bench.py graph loop host ms per step (median): replay call {med[0]:.2f}  prefetch {med[1]:.2f}  "
                   f"release {med[2]:.2f}  capture {med[3]:.2f}", file=sys.stderr)
+            print(f"bench.py metadata count reads: {scn_meta.READ_STATS[1]} reads, "
+                  f"{1e3 * scn_meta.READ_STATS[0]:.1f} ms of host wait in total", file=sys.stderr)
             host_t.clear()
             torch.cuda.synchronize()
             print("bench.py graph replays, device ms:", [round(a.elapsed_time(b), 1) for a, b in replay_ev],
@@ -592,6 +626,15 @@ def main():
             print("bench.py graph replays, device idle before each, ms:",
                   [round(replay_ev[k][1].elapsed_time(replay_ev[k + 1][0]), 1) for k in range(len(replay_ev) - 1)],
                   file=sys.stderr)
+            # when the next step's metadata build finished, relative to the end of the step before it (> 0: the
+            # replay waited for the build)
+            print("bench.py metadata build done, ms after the previous step's end:",
+                  [round(replay_ev[k][1].elapsed_time(build_ev[k + 1]), 2) for k in range(len(replay_ev) - 1)],
+                  file=sys.stderr)
+        if fut is not None:
+            fut.result()
+        if worker is not None:
+            worker.shutdown()
     else:
         for i in range(args.steps):
             step(i)

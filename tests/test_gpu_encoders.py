@@ -306,12 +306,27 @@ def test_prefetch_entry_needs_the_same_tensor():
         m = scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False)
         twin = xs[1].coords.clone()
         assert md.take_prefetched(twin, 4096) is None
-        assert md._PREFETCHED                  # still pending for the original tensor
+        assert md.pending_count() == 1         # still pending for the original tensor
         m2 = scn.prefetch_metadata(model, xs[0].coords, wait_for_producer=False)
-        assert len(md._PREFETCHED) == 1        # the older entry was dropped
+        assert md.pending_count() == 1         # the older entry was dropped
         assert md.take_prefetched(xs[1].coords, 4096) is None
         assert md.take_prefetched(xs[0].coords, 4096) is m2 and m2 is not m
-        assert not md._PREFETCHED
+        assert md.pending_count() == 0
+        # depth 2 (bench.py --prefetch-thread): two batches pending at once, each found through its own tensor,
+        # a third drops the oldest, and the same tensor again replaces its own entry
+        md.PREFETCH_DEPTH = 2
+        try:
+            a = scn.prefetch_metadata(model, xs[1].coords, wait_for_producer=False)
+            b = scn.prefetch_metadata(model, xs[0].coords, wait_for_producer=False)
+            assert md.pending_count() == 2 and md.prefetch_event(DEV, xs[1].coords) is not None
+            b2 = scn.prefetch_metadata(model, xs[0].coords, wait_for_producer=False)
+            assert md.pending_count() == 2 and b2 is not b
+            c = scn.prefetch_metadata(model, twin, wait_for_producer=False)
+            assert md.pending_count() == 2 and md.take_prefetched(xs[1].coords, 4096) is None   # a was dropped
+            assert md.take_prefetched(twin, 4096) is c and md.take_prefetched(xs[0].coords, 4096) is b2
+            assert md.pending_count() == 0 and a is not None
+        finally:
+            md.PREFETCH_DEPTH = 1
 
 
 def test_graph_captured_step_matches_eager():
@@ -345,11 +360,75 @@ def test_graph_captured_step_matches_eager():
         body(twin, opts[1], 1)
         g.capture_end()
     keep = md.captured_metadata()
-    assert len(keep) == 1 and not md._PREFETCHED
+    assert len(keep) == 1 and md.pending_count() == 0
     cur = torch.cuda.current_stream()
     cur.wait_event(ev)
     g.replay()
     torch.cuda.synchronize()
+    for (na, a), (nb, b) in zip(model.named_parameters(), twin.named_parameters()):
+        assert torch.equal(a, b), na
+        assert torch.equal(a.grad, b.grad), na
+    for sa, sb in zip(opts[0].state.values(), opts[1].state.values()):
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(sa[k], sb[k])
+
+
+def test_graph_capture_beside_worker_prefetch():
+    """bench.py --prefetch-thread: each step is captured while a worker thread builds the metadata of the next
+    batch on the side stream (two prefetched batches pending, PREFETCH_DEPTH = 2); three captured and replayed
+    steps leave parameters, gradients and Adam state bit-identical to the same steps launched eagerly."""
+    import copy
+    from concurrent.futures import ThreadPoolExecutor
+    import torch.nn.functional as F
+    from sparseconvnet import metadata as md
+    model, xs, ys = _prefetch_model()
+    twin = copy.deepcopy(model)
+    opts = [torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=True) for m in (model, twin)]
+
+    def body(m, opt, k):
+        opt.zero_grad(set_to_none=True)
+        logits, _ = m((xs[k], None), istrain=True)
+        F.multilabel_soft_margin_loss(logits, ys[k]).backward()
+        opt.step()
+
+    for m, opt in zip((model, twin), opts):   # plan + optimizer state, eagerly
+        body(m, opt, 0)
+    torch.cuda.synchronize()
+    seq = [1, 0, 1]
+    for k in seq:                             # eager reference, prefetched on the loop's thread
+        scn.prefetch_metadata(model, xs[k].coords, wait_for_producer=False)
+        body(model, opts[0], k)
+    torch.cuda.synchronize()
+    md.PREFETCH_DEPTH = 2
+    pool = ThreadPoolExecutor(max_workers=1)
+    graphs, keeps = [], []
+    try:
+        scn.prefetch_metadata(twin, xs[seq[0]].coords, wait_for_producer=False)
+        fut = pool.submit(scn.prefetch_metadata, twin, xs[seq[1]].coords, False)
+        side = torch.cuda.Stream()
+        cur = torch.cuda.current_stream()
+        for j, k in enumerate(seq):
+            ev = md.prefetch_event(DEV, xs[k].coords)
+            assert ev is not None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                g.capture_begin(capture_error_mode="relaxed")
+                body(twin, opts[1], k)
+                g.capture_end()
+            keeps.append(md.captured_metadata())
+            assert len(keeps[-1]) == 1
+            cur.wait_event(ev)
+            g.replay()
+            graphs.append(g)
+            if fut is not None:
+                fut.result()
+                fut = pool.submit(scn.prefetch_metadata, twin, xs[seq[j + 2]].coords, False) \
+                    if j + 2 < len(seq) else None
+        torch.cuda.synchronize()
+    finally:
+        pool.shutdown()
+        md.PREFETCH_DEPTH = 1
+    assert md.pending_count() == 0
     for (na, a), (nb, b) in zip(model.named_parameters(), twin.named_parameters()):
         assert torch.equal(a, b), na
         assert torch.equal(a.grad, b.grad), na
