@@ -60,11 +60,6 @@ FAMILIES = {"wgrad": "wgrad", "nin_wgrad": "wgrad", "wgrad_strided": "wgrad", "w
             "nin_fwd": "nin", "nin_bwd_data": "nin", "bn_fwd": "bn", "bn_bwd": "bn", "bn_join": "bn"}
 
 
-# BENCH_SKIP_DONE_WAIT=1: a replay whose metadata build has already completed (Event.query) issues no stream
-# wait on it (diagnostic: what a cross-stream wait on a completed event costs the compute stream)
-SKIP_DONE_WAIT = os.environ.get("BENCH_SKIP_DONE_WAIT") == "1"
-
-
 def family(kind):
     base = kind.split("/")[0]
     return "conv" if base in CONV_KINDS else FAMILIES.get(base, base)
@@ -489,6 +484,7 @@ def main():
     graph_pool = torch.cuda.graph_pool_handle() if use_graph else None
 
     capture_s = []
+    capture_parts = []  # BENCH_HOST_TIMING: (capture_begin, body, capture_end) host seconds
 
     def body(i):  # one training step without its prefetch (what a graph captures; N ranks: up to backward)
         x, y, _, text = batches[i % len(batches)]
@@ -517,9 +513,15 @@ def main():
         ev = scn_meta.prefetch_event(dev, batches[i % len(batches)][0].coords)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(cap_stream):
+            c0 = time.perf_counter()
             g.capture_begin(pool=graph_pool, capture_error_mode="relaxed")
+            c1 = time.perf_counter()
             body(i)
+            c2 = time.perf_counter()
             g.capture_end()
+            c3 = time.perf_counter()
+        if host_t is not None:
+            capture_parts.append((c1 - c0, c2 - c1, c3 - c2))
         keep = scn_meta.captured_metadata()
         if gsync is not None:
             gsync.check_views()
@@ -536,8 +538,7 @@ def main():
 
     def replay(entry):
         g, keep, ev = entry
-        if not (SKIP_DONE_WAIT and ev.query()):
-            cur.wait_event(ev)  # the metadata build (side stream) before the graph reads it
+        cur.wait_event(ev)  # the metadata build (side stream) before the graph reads it
         for m in keep:
             for t in m.tensors():
                 t.record_stream(cur)
@@ -617,6 +618,9 @@ def main():
             med = [1e3 * statistics.median(c) for c in zip(*host_t[-args.steps:])]
             print(f"bench.py graph loop host ms per step (median): replay call {med[0]:.2f}  prefetch {med[1]:.2f}  "
                   f"release {med[2]:.2f}  capture {med[3]:.2f}", file=sys.stderr)
+            cp = [1e3 * statistics.median(c) for c in zip(*capture_parts[-args.steps:])]
+            print(f"bench.py capture host ms (median): begin {cp[0]:.2f}  body {cp[1]:.2f}  end {cp[2]:.2f}",
+                  file=sys.stderr)
             print(f"bench.py metadata count reads: {scn_meta.READ_STATS[1]} reads, "
                   f"{1e3 * scn_meta.READ_STATS[0]:.1f} ms of host wait in total", file=sys.stderr)
             host_t.clear()
