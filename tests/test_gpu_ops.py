@@ -841,7 +841,6 @@ def test_conv_wgrad_chunk_over_cap_falls_back():
     r._tiles, r._locals, r._wchunk, r._dense = {}, {}, None, None
     r._map, r._n = r.nbr, V
     r.pairs = metadata.PairLists(r.nbr, K, V, DEV, _lib.stream(), r._plan, r._key)
-    r.n_rules = r.pairs.total
     loc = r.local()
     assert loc["max_u"] > int(_lib.query("msp_wgrad_chunk_cap"))  # random rows: ~27 x 0.8 x 128 per tile
     assert r.wgrad_index() is None
