@@ -669,6 +669,67 @@ __global__ __launch_bounds__(kLT) void chunk_lidx_kernel(const int64_t* __restri
   if (n_far && n_over) atomicAdd(n_far, (unsigned long long)n_over);
 }
 
+// Rules whose input row lies past a tile's staged capacity (chunk_lr 0xFFFF with a real row): one block per tile
+// hands each such entry a slot of the list (slots in arrival order; msp_wgrad_far_list then sorts the list by
+// (offset, entry), so the correction below sums in a fixed order).
+constexpr int kFarShift = 40;  // far_key = offset << 40 | chunk entry
+__global__ __launch_bounds__(kLT) void far_collect_kernel(const int64_t* __restrict__ tile_start,
+                                                          const uint8_t* __restrict__ chunk_off,
+                                                          const uint32_t* __restrict__ chunk_lr, int64_t n_far,
+                                                          unsigned long long* __restrict__ ctr,
+                                                          uint64_t* __restrict__ keys, int32_t* __restrict__ tiles) {
+  const int64_t t = blockIdx.x;
+  const int64_t e0 = tile_start[t] * MSP_CHUNK, e1 = tile_start[t + 1] * MSP_CHUNK;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kLT) {
+    const uint32_t w = chunk_lr[e];
+    if ((w & 0xFFFFu) != kWFar || (w >> 16) >= (uint32_t)kWTile) continue;
+    const unsigned long long slot = atomicAdd(ctr, 1ull);
+    if ((int64_t)slot >= n_far) continue;  // more than counted: cannot happen for the index that counted them
+    keys[slot] = ((uint64_t)chunk_off[e / MSP_CHUNK] << kFarShift) | (uint64_t)e;
+    tiles[slot] = (int32_t)t;
+  }
+}
+
+// dw[o][ci0 .. +32][co0 .. +32] += the far rules of offset o, in list order (fp64 sums): block = one (offset,
+// 32 x 32 slice), thread = (one input channel, four output channels).
+__global__ __launch_bounds__(256) void wgrad_far_kernel(const float* __restrict__ x, int c_in,
+                                                        const float* __restrict__ dy, int c_out,
+                                                        const int32_t* __restrict__ chunk_src,
+                                                        const uint16_t* __restrict__ chunk_row,
+                                                        const uint64_t* __restrict__ keys,
+                                                        const int32_t* __restrict__ tiles, int64_t n_far,
+                                                        float* __restrict__ dw) {
+  const int n_sl_o = c_out / 32, n_slices = (c_in / 32) * n_sl_o;
+  const int o = (int)(blockIdx.x / n_slices), sl = (int)(blockIdx.x % n_slices);
+  const int ci0 = 32 * (sl / n_sl_o), co0 = 32 * (sl % n_sl_o);
+  const int ci = threadIdx.x >> 3, co = 4 * (threadIdx.x & 7);
+  auto first_at_least = [&](uint64_t k) {  // first list position with key >= k
+    int64_t lo = 0, hi = n_far;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const int64_t k0 = first_at_least((uint64_t)o << kFarShift), k1 = first_at_least((uint64_t)(o + 1) << kFarShift);
+  if (k0 >= k1) return;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};  // fp64: exact products, the list's sum rounded once into dw
+  for (int64_t k = k0; k < k1; ++k) {
+    const int64_t e = (int64_t)(keys[k] & ((1ull << kFarShift) - 1));
+    const int64_t i = chunk_src[e], j = (int64_t)tiles[k] * kWTile + chunk_row[e];
+    const double xv = x[i * c_in + ci0 + ci];
+    const floatx4 d = *reinterpret_cast<const floatx4*>(dy + j * c_out + co0 + co);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += xv * (double)d[q];
+  }
+  floatx4* out = reinterpret_cast<floatx4*>(dw + ((int64_t)o * c_in + ci0 + ci) * c_out + co0 + co);
+  floatx4 v = *out;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = (float)((double)v[q] + acc[q]);
+  *out = v;
+}
+
 constexpr int kWMaxCh = 216;                   // chunks of one 128-row tile (K <= 27 offsets x 8)
 constexpr int kWXImg = (kWCap + 1) * 32;       // bf16 elements of one x piece image (+ zero row kWCap)
 constexpr int kWDImg = (kWTile + 1) * 32;      // dy piece image (+ zero row 128)
@@ -1041,6 +1102,50 @@ int msp_wgrad_chunk_index(const int64_t* tile_start, const int32_t* chunk_src, c
   chunk_lidx_kernel<<<(unsigned)n_tiles, kLT, 0, s>>>(tile_start, chunk_src, chunk_row, u_start, u_rows, chunk_lr,
                                                       reinterpret_cast<unsigned long long*>(n_far));
   return check_launch("msp_wgrad_chunk_index");
+}
+
+size_t msp_wgrad_far_workspace_size(int64_t n_far) {
+  const int64_t n = n_far > 0 ? n_far : 0;
+  return 8 + (size_t)n * 8 + (size_t)((n * 4 + 7) / 8) * 8 + msp_sort_workspace_size(n, kFarShift + 5);
+}
+
+int msp_wgrad_far_list(const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
+                       int64_t n_rows, int64_t n_far, int64_t* far_key, int32_t* far_tile, void* ws,
+                       size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(n_rows >= 0 && n_rows < (1ll << 31) && n_far >= 0 && n_far < (1ll << 31),
+              "msp_wgrad_far_list: bad sizes (n_rows=%lld n_far=%lld)", (long long)n_rows, (long long)n_far);
+  if (n_far == 0) return MSP_OK;
+  MSP_REQUIRE(tile_start && chunk_off && chunk_lr && far_key && far_tile, "msp_wgrad_far_list: NULL pointer");
+  const size_t need = msp_wgrad_far_workspace_size(n_far);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_wgrad_far_list: workspace too small (%zu < %zu)", ws_bytes, need);
+  hipStream_t s = as_stream(stream);
+  char* w = static_cast<char*>(ws);
+  auto* ctr = reinterpret_cast<unsigned long long*>(w);
+  auto* keys = reinterpret_cast<uint64_t*>(w + 8);
+  auto* tiles = reinterpret_cast<int32_t*>(w + 8 + n_far * 8);
+  void* sws = w + 8 + n_far * 8 + ((n_far * 4 + 7) / 8) * 8;
+  MSP_HIP(hipMemsetAsync(ctr, 0, 8, s), "msp_wgrad_far_list");
+  const int64_t n_tiles = ceil_div(n_rows, kWTile);
+  far_collect_kernel<<<(unsigned)n_tiles, kLT, 0, s>>>(tile_start, chunk_off, chunk_lr, n_far, ctr, keys, tiles);
+  const int rc = check_launch("msp_wgrad_far_list");
+  if (rc != MSP_OK) return rc;
+  return msp_sort_pairs(keys, reinterpret_cast<uint64_t*>(far_key), tiles, far_tile, n_far, kFarShift + 5, sws,
+                        msp_sort_workspace_size(n_far, kFarShift + 5), stream);
+}
+
+int msp_conv_wgrad_far(const float* x, int c_in, const float* dy, int c_out, int K, const int32_t* chunk_src,
+                       const uint16_t* chunk_row, const int64_t* far_key, const int32_t* far_tile, int64_t n_far,
+                       float* dw, msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && K <= 32 && c_in > 0 && c_in % 32 == 0 && c_out > 0 && c_out % 32 == 0 && n_far >= 0,
+              "msp_conv_wgrad_far: needs K <= 32 and channels in multiples of 32 (K=%d c_in=%d c_out=%d)", K, c_in,
+              c_out);
+  if (n_far == 0) return MSP_OK;
+  MSP_REQUIRE(x && dy && chunk_src && chunk_row && far_key && far_tile && dw, "msp_conv_wgrad_far: NULL pointer");
+  hipStream_t s = as_stream(stream);
+  const unsigned grid = (unsigned)(K * (c_in / 32) * (c_out / 32));
+  wgrad_far_kernel<<<grid, 256, 0, s>>>(x, c_in, dy, c_out, chunk_src, chunk_row,
+                                        reinterpret_cast<const uint64_t*>(far_key), far_tile, n_far, dw);
+  return check_launch("msp_conv_wgrad_far");
 }
 
 int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,

@@ -50,6 +50,9 @@ PROTOTYPES = {
     "msp_wgrad_chunk_cap": (I64, []),
     "msp_wgrad_chunk_index": (I, [P, P, P, I64, P, P, P, P, P]),
     "msp_conv_wgrad_chunk": (I, [P, I, P, I, I, I, P, P, P, P, P, I64, I64, P, P, P]),
+    "msp_wgrad_far_workspace_size": (SZ, [I64]),
+    "msp_wgrad_far_list": (I, [P, P, P, I64, I64, P, P, P, SZ, P]),
+    "msp_conv_wgrad_far": (I, [P, I, P, I, I, P, P, P, P, I64, P, P]),
     "msp_conv_local_workspace_size": (SZ, [I, I, I]),
     "msp_conv_local": (I, [P, I, P, I, I, I, I, P, P, P, P, P, I64, P, P, SZ, P]),
     "msp_conv_tile_rows": (I, [I64, I, I]),

@@ -333,34 +333,45 @@ class SubmRules:
 
     def wgrad_index(self):
         """msp_wgrad_chunk_index over the 128-row tile rulebook and the tile-local lists of each tile's distinct
-        input rows for msp_conv_wgrad_chunk, built on first use.  None when a tile names more distinct rows than
-        the kernel stages (msp_wgrad_chunk_cap): the pair lists serve then."""
+        input rows for msp_conv_wgrad_chunk, built on first use.  Rules whose input row lies past the rows a tile
+        stages (a tile listing more than msp_wgrad_chunk_cap rows) are listed apart (msp_wgrad_far_list, sorted)
+        and added by msp_conv_wgrad_far: the chunk form serves every map."""
         if self._wchunk is None:
             loc = self.lists()
-            if "max_u" in loc and loc["max_u"] > int(query("msp_wgrad_chunk_cap")):
-                self._wchunk = False
-                return None
             tiles = self.tiles_for(128)
             if "max_u" not in loc or "n_chunks" not in tiles:
-                # in a replay, counts not read yet (the tiles are asked for before the lists' count is known: one
-                # read for both, the tiles unused in the rare batch whose lists exceed the cap): decide -- chunk
-                # index, else pair lists -- once they are read
+                # in a replay, counts not read yet: build the index once they are read (one read for both)
                 self._wchunk = "pending"
 
                 def decide():
                     self._wchunk = None
-                    if self.wgrad_index() is None:
-                        self.pairs.fill()
+                    self.wgrad_index()
                 _defer().then(decide)
                 return self._wchunk
             self._plan.append(("wchunk", self._key))
-            lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=self.nbr.device)
-            if self._n:  # no rule can lie past the cap (checked above): no overflow count needed
+            dev, s = self.nbr.device, _lib.stream(self.nbr.device)
+            lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=dev)
+            over = loc["max_u"] > int(query("msp_wgrad_chunk_cap"))
+            n_far = torch.zeros(1, dtype=torch.int64, device=dev) if over else None
+            if self._n:
                 call("msp_wgrad_chunk_index", ptr(tiles["tile_start"]), ptr(tiles["chunk_src"]),
                      ptr(tiles["chunk_row"]), I64(self._n), ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(lr),
-                     None, _lib.stream(self.nbr.device))
-            self._wchunk = dict(tiles=tiles, chunk_lr=lr, u_start=loc["u_start"], u_rows=loc["u_rows"])
-        return self._wchunk or None
+                     ptr(n_far), s)
+            idx = self._wchunk = dict(tiles=tiles, chunk_lr=lr, u_start=loc["u_start"], u_rows=loc["u_rows"],
+                                      n_far=0)
+            if over and self._n:
+                def far(vals):
+                    nf = vals[0]
+                    idx["n_far"] = nf
+                    if nf:
+                        key = torch.empty(nf, dtype=torch.int64, device=dev)
+                        tile = torch.empty(nf, dtype=torch.int32, device=dev)
+                        ws = _ws(query("msp_wgrad_far_workspace_size", I64(nf)), dev)
+                        call("msp_wgrad_far_list", ptr(tiles["tile_start"]), ptr(tiles["chunk_off"]), ptr(lr),
+                             I64(self._n), I64(nf), ptr(key), ptr(tile), ptr(ws), ws.numel(), _lib.stream(dev))
+                        idx.update(far_key=key, far_tile=tile, far_ws=ws)
+                _later(n_far, far)
+        return self._wchunk
 
     def note_use(self, purpose, c_in, c_out):
         """Record in the plan that a convolution / weight gradient with these channel counts runs over these

@@ -235,11 +235,9 @@ def conv_wgrad(x, dy, pairs, pin, pout, K, kind="wgrad", flops=None):
 def conv_wgrad_chunk(x, dy, rules, K, kind="wgrad", flops=None):
     """Submanifold weight gradient over the 128-row tile rulebook (SubmRules.wgrad_index): per tile the distinct
     x rows and the 128 dy rows staged in LDS once per 32 x 32 channel slice, the compacted chunks as MFMA
-    k-steps (msp_conv_wgrad_chunk); partial sums per tile range added in order.  None when a tile names more
-    distinct rows than the kernel stages."""
+    k-steps (msp_conv_wgrad_chunk); partial sums per tile range added in order; then the rules of rows past a
+    tile's staged capacity, if any (msp_conv_wgrad_far)."""
     idx = rules.wgrad_index()
-    if idx is None:
-        return None
     c_in, c_out = x.size(1), dy.size(1)
     n = dy.size(0)
     tiles = idx["tiles"]
@@ -256,6 +254,9 @@ def conv_wgrad_chunk(x, dy, rules, K, kind="wgrad", flops=None):
         "msp_conv_wgrad_chunk", ptr(x), c_in, ptr(dy), c_out, K, tiles["tile_rows"], ptr(tiles["tile_start"]),
         ptr(tiles["chunk_off"]), ptr(idx["chunk_lr"]), ptr(idx["u_start"]), ptr(idx["u_rows"]), n, ranges,
         ptr(slab), ptr(dw), _stream(x)), nbytes)
+    if idx["n_far"]:
+        call("msp_conv_wgrad_far", ptr(x), c_in, ptr(dy), c_out, K, ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]),
+             ptr(idx["far_key"]), ptr(idx["far_tile"]), idx["n_far"], ptr(dw), _stream(x))
     return dw
 
 

@@ -202,11 +202,14 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
  * writes per chunk entry e chunk_lr[e] = (position of its input row in its tile's u_rows list) | (row in the
  * tile, 128 for a padding slot) << 16.  msp_conv_wgrad_chunk stages per tile the listed x rows and the 128 dy
  * rows in LDS once per 32 x 32 channel slice (exact bf16 pieces); the rulebook's chunks are the MFMA k-steps.
- * Needs every tile's list (msp_tile_local's largest count, u_start[n_tiles + 1]) <= msp_wgrad_chunk_cap(): a rule
- * whose input row lies past the cap is marked 0xFFFF and contributes nothing, so the caller checks the largest
- * count first and otherwise takes the pair-list form (msp_conv_wgrad); n_far (device int64, nullable) receives
- * the number of such rules (0 when the cap holds).  K <= 27, channels in multiples of 32 (msp_wgrad_chunk_ok;
- * msp_wgrad_chunk_preferred: the shapes the library takes it for).
+ * A tile lists at most msp_wgrad_chunk_cap() rows in LDS: a rule whose input row lies past the cap is marked
+ * 0xFFFF and contributes nothing to msp_conv_wgrad_chunk; n_far (device int64, nullable) receives the number of
+ * such rules (0 when every tile's list, msp_tile_local's largest count u_start[n_tiles + 1], is within the cap).
+ * Their products are added afterwards (round 4): msp_wgrad_far_list writes those n_far chunk entries sorted by
+ * (offset, entry) -- far_key[k] = offset << 40 | entry, far_tile[k] = the entry's tile; workspace
+ * msp_wgrad_far_workspace_size(n_far) -- and msp_conv_wgrad_far adds, after msp_conv_wgrad_chunk filled dw,
+ * dw[o][ci][co] += the far rules' x[i][ci] dy[j][co] of offset o, fp64 sums in list order.  K <= 27, channels in
+ * multiples of 32 (msp_wgrad_chunk_ok; msp_wgrad_chunk_preferred: the shapes the library takes it for).
  * Blocks run n_ranges contiguous tile ranges (msp_wgrad_chunk_ranges) per slice; slab holds n_ranges x K x
  * c_in x c_out floats of partial sums, added in range order into dw. */
 /* Per-step split-weight images (round 3).  msp_conv_tile, msp_conv_local and msp_conv_nbr split their fp32
@@ -241,6 +244,13 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
                          const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
                          const int64_t* u_start, const int32_t* u_rows, int64_t n_rows, int64_t n_ranges,
                          float* slab, float* dw, msp_stream_t stream);
+size_t msp_wgrad_far_workspace_size(int64_t n_far);
+int msp_wgrad_far_list(const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
+                       int64_t n_rows, int64_t n_far, int64_t* far_key, int32_t* far_tile, void* ws,
+                       size_t ws_bytes, msp_stream_t stream);
+int msp_conv_wgrad_far(const float* x, int c_in, const float* dy, int c_out, int K, const int32_t* chunk_src,
+                       const uint16_t* chunk_row, const int64_t* far_key, const int32_t* far_tile, int64_t n_far,
+                       float* dw, msp_stream_t stream);
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows);
 int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,

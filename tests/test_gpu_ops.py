@@ -823,11 +823,11 @@ def test_conv_wgrad_chunk_accuracy(cin, cout):
     assert (dw - dwp).abs().max().item() / scale < 2e-6
 
 
-def test_conv_wgrad_chunk_over_cap_falls_back():
+def test_conv_wgrad_chunk_over_cap_far_rules():
     """A map whose 128-row tiles name more distinct input rows than the chunk weight gradient stages
-    (msp_wgrad_chunk_cap, 448): SubmRules.wgrad_index refuses it (None), the module's backward takes the
-    pair-list weight gradient, and that gradient matches fp64; msp_wgrad_chunk_index reports the rules it would
-    drop through its n_far count (no silent loss at the C ABI)."""
+    (msp_wgrad_chunk_cap, 448): msp_wgrad_chunk_index counts the rules whose row lies past the cap (n_far, ADVICE
+    r02: no silent loss at the C ABI), msp_wgrad_far_list lists exactly those, sorted by (offset, entry), and the
+    module's backward -- the chunk form plus msp_conv_wgrad_far for the listed rules -- matches fp64."""
     from sparseconvnet import _lib, metadata, ops
     from sparseconvnet._lib import ptr
     torch.manual_seed(9)
@@ -842,18 +842,26 @@ def test_conv_wgrad_chunk_over_cap_falls_back():
     r._map, r._n = r.nbr, V
     r.pairs = metadata.PairLists(r.nbr, K, V, DEV, _lib.stream(), r._plan, r._key)
     loc = r.local()
-    assert loc["max_u"] > int(_lib.query("msp_wgrad_chunk_cap"))  # random rows: ~27 x 0.8 x 128 per tile
-    assert r.wgrad_index() is None
-    # the C ABI: the over-cap rules are counted, not silently dropped
+    cap = int(_lib.query("msp_wgrad_chunk_cap"))
+    assert loc["max_u"] > cap  # random rows: ~27 x 0.8 x 128 per tile
+    idx = r.wgrad_index()
+    assert idx is not None and idx["n_far"] > 0
+    # the C ABI: the over-cap rules are counted, not silently dropped, and the list names exactly them
     tiles = r.tiles_for(128)
     lr = torch.empty(tiles["n_chunks"] * 16, dtype=torch.int32, device=DEV)
     n_far = torch.full((1,), -1, dtype=torch.int64, device=DEV)
     _lib.call("msp_wgrad_chunk_index", ptr(tiles["tile_start"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]),
               _lib.I64(V), ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(lr), ptr(n_far), _lib.stream())
     u = loc["u_start"][:loc["n_tiles"] + 1].cpu()
-    cap = int(_lib.query("msp_wgrad_chunk_cap"))
-    assert int(n_far.item()) > 0 and bool(((u[1:] - u[:-1]) > cap).any())
-    # the fallback weight gradient through the autograd Function
+    assert int(n_far.item()) == idx["n_far"] and bool(((u[1:] - u[:-1]) > cap).any())
+    w_lr = lr.cpu().long() & 0xFFFFFFFF
+    far_e = torch.nonzero(((w_lr & 0xFFFF) == 0xFFFF) & ((w_lr >> 16) < 128)).flatten()
+    off = tiles["chunk_off"].cpu().long()[far_e // 16]
+    want = torch.sort((off << 40) | far_e).values
+    assert torch.equal(idx["far_key"].cpu(), want)
+    ts = tiles["tile_start"].cpu()
+    assert torch.equal(idx["far_tile"].cpu().long(), torch.searchsorted(ts[1:loc["n_tiles"] + 1], (want & ((1 << 40) - 1)) // 16, right=True))
+    # the weight gradient through the autograd Function
     assert int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, 32, 64))
     x = torch.randn(V, 32, device=DEV, requires_grad=True)
     w = (torch.randn(K, 1, 32, 64, device=DEV) / (K * 32) ** 0.5).requires_grad_(True)
