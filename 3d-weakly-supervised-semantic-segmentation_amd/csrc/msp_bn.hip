@@ -480,7 +480,6 @@ __global__ __launch_bounds__(kSmallT) void bn_small_fwd_kernel(const float* __re
         }
       }
     } else {
-#pragma unroll 4
       for (int64_t v = t; v < V; v += kSmallT) {
         const float4 a = x4[v * C4 + blockIdx.x];
         const float xs[4] = {a.x, a.y, a.z, a.w};
@@ -535,7 +534,6 @@ __global__ __launch_bounds__(kSmallT) void bn_small_fwd_kernel(const float* __re
     return z > 0.f ? z : z * leak;
   };
   float4* y4 = reinterpret_cast<float4*>(y);
-#pragma unroll 4
   for (int64_t v = t; v < V; v += kSmallT) {
     const float4 a = x4[v * C4 + blockIdx.x];
     y4[v * C4 + blockIdx.x] = make_float4(f(a.x, 0), f(a.y, 1), f(a.z, 2), f(a.w, 3));
@@ -565,7 +563,6 @@ __global__ __launch_bounds__(kSmallT) void bn_small_bwd_kernel(const float* __re
   const float4* x4 = reinterpret_cast<const float4*>(x);
   const float4* g4 = reinterpret_cast<const float4*>(dy);
   double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
   for (int64_t v = t; v < V; v += kSmallT) {  // bn_reduce4_kernel<1>'s terms
     const float4 a = x4[v * C4 + blockIdx.x], g = g4[v * C4 + blockIdx.x];
     const float xs[4] = {a.x, a.y, a.z, a.w}, gs[4] = {g.x, g.y, g.z, g.w};
@@ -598,7 +595,6 @@ __global__ __launch_bounds__(kSmallT) void bn_small_bwd_kernel(const float* __re
     return ws[k] * (dz - mdz[k] - (xc * is[k]) * mdzx[k]);
   };
   float4* d4 = reinterpret_cast<float4*>(dx);
-#pragma unroll 4
   for (int64_t v = t; v < V; v += kSmallT) {
     const float4 a = x4[v * C4 + blockIdx.x], g = g4[v * C4 + blockIdx.x];
     float4 d = make_float4(f(a.x, g.x, 0), f(a.y, g.y, 1), f(a.z, g.z, 2), f(a.w, g.w, 3));

@@ -505,19 +505,12 @@ def test_weight_layout_flag(cin, cout, nbr_form):
 @pytest.mark.parametrize("V,C", [(5000, 32), (3001, 64), (777, 36), (1200, 6), (0, 32)])
 def test_residual_join_stats(V, C):
     """msp_add_bn_stats: the sum bit-equal to a + b and its partials bit-equal
-    to msp_bn_stats on that sum (vector form; C = 6 takes the scalar form).  (These sizes are small levels: with
-    the one-launch BatchNormalization on, the join leaves no partials -- the BN sums its own.)"""
+    to msp_bn_stats on that sum (vector form; C = 6 takes the scalar form)."""
     from sparseconvnet import _lib, ops
     torch.manual_seed(V + C)
     a = torch.randn(V, C, device=DEV) * 2 + 0.5
     b = torch.randn(V, C, device=DEV)
     f, part = ops.ResidualJoinFunction.apply(a, b)
-    assert torch.equal(f, a + b) and (part is None) == ops.bn_small(V, C)
-    ops.BN_SMALL = False
-    try:
-        f, part = ops.ResidualJoinFunction.apply(a, b)
-    finally:
-        ops.BN_SMALL = True
     assert torch.equal(f, a + b)
     ref = ops._bn_partial_buf(V, C, a.device)
     ref.zero_()
