@@ -422,190 +422,6 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply4_kernel(const float* __restri
   }
 }
 
-// ---------------------------------------------------------------- small levels: one launch per direction
-// Below kSmallV rows (levels 4-6 of the headline UNet: 8.3 k, 2.1 k, 0.5 k rows) each of the three launches of a
-// BatchNormalization (statistics, per-channel finalize, apply) is a 4-6 us launch-bound kernel.  Here one block of
-// kSmallT threads owns four channels for all rows: it sums the statistics (fp64, each thread's rows in order, then
-// a fixed butterfly over the wave and the 16 waves in order: deterministic), finalizes them like bn_finalize_kernel
-// and applies them -- one launch of C / 4 blocks.  The backward likewise: sums of dz and dz * xhat, the parameter
-// gradients, then dx (+ the residual fork's addend).
-constexpr int kSmallT = 1024;
-constexpr int64_t kSmallV = 16384;
-
-__device__ inline double wave_sum_f64(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  return v;  // lane 0
-}
-
-// s[0..3], s[4..7] of every thread -> the block's totals in tot[0..7] (every thread reads them after the barrier)
-__device__ inline void block_sum8(double (&s)[8], double* __restrict__ red /* [16][8] */,
-                                  double* __restrict__ tot /* [8] */) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const double w = wave_sum_f64(s[k]);
-    if (lane == 0) red[wave * 8 + k] = w;
-  }
-  __syncthreads();
-  if (threadIdx.x < 8) {
-    double a = 0.0;
-    for (int w = 0; w < kSmallT / 64; ++w) a += red[w * 8 + threadIdx.x];
-    tot[threadIdx.x] = a;
-  }
-  __syncthreads();
-}
-
-// partial: the batch-statistic partials a join left (P blocks of [2][C], bn_parts layout), or NULL (sum x here)
-__global__ __launch_bounds__(kSmallT) void bn_small_fwd_kernel(const float* __restrict__ x, int64_t V, int C,
-                                                               const double* __restrict__ partial, int64_t P,
-                                                               double eps, double momentum, int train,
-                                                               float* __restrict__ rmean, float* __restrict__ rvar,
-                                                               const float* __restrict__ weight,
-                                                               const float* __restrict__ bias,
-                                                               float* __restrict__ stats, float leak,
-                                                               float* __restrict__ y) {
-  __shared__ double red[16 * 8], tot[8];
-  __shared__ float cst[4][4];  // [mh, ml, sc, sh][k]
-  const int c0 = 4 * blockIdx.x, C4 = C >> 2, t = threadIdx.x;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  if (train) {
-    double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    if (partial) {
-      for (int64_t p = t; p < P; p += kSmallT) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          s[k] += partial[p * 2 * C + c0 + k];
-          s[4 + k] += partial[p * 2 * C + C + c0 + k];
-        }
-      }
-    } else {
-      for (int64_t v = t; v < V; v += kSmallT) {
-        const float4 a = x4[v * C4 + blockIdx.x];
-        const float xs[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          s[k] += xs[k];
-          s[4 + k] += (double)xs[k] * xs[k];
-        }
-      }
-    }
-    block_sum8(s, red, tot);
-  }
-  if (t < 4) {  // finalize channel c0 + t (bn_finalize_kernel's arithmetic)
-    const int c = c0 + t;
-    double mu, var;
-    if (train) {
-      mu = V > 0 ? tot[t] / (double)V : 0.0;
-      var = V > 0 ? tot[4 + t] / (double)V - mu * mu : 0.0;
-      if (var < 0.0) var = 0.0;
-      const double unb = V > 1 ? var * (double)V / (double)(V - 1) : var;
-      rmean[c] = (float)(momentum * rmean[c] + (1.0 - momentum) * mu);
-      rvar[c] = (float)(momentum * rvar[c] + (1.0 - momentum) * unb);
-    } else {
-      mu = rmean[c];
-      var = rvar[c];
-    }
-    const double is = 1.0 / sqrt(var + eps);
-    const double w = weight ? weight[c] : 1.0, b = bias ? bias[c] : 0.0;
-    const float hi = (float)mu;
-    const float lo = (float)(mu - (double)hi), sc = (float)(w * is), sh = (float)b;
-    stats[c] = hi;
-    stats[C + c] = lo;
-    stats[2 * C + c] = (float)is;
-    stats[3 * C + c] = sc;
-    stats[4 * C + c] = sh;
-    cst[0][t] = hi;
-    cst[1][t] = lo;
-    cst[2][t] = sc;
-    cst[3][t] = sh;
-  }
-  __syncthreads();
-  float mh[4], ml[4], sc[4], sh[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    mh[k] = cst[0][k];
-    ml[k] = cst[1][k];
-    sc[k] = cst[2][k];
-    sh[k] = cst[3][k];
-  }
-  auto f = [&](float v, int k) {  // bn_apply4_kernel's arithmetic
-    const float z = ((v - mh[k]) - ml[k]) * sc[k] + sh[k];
-    return z > 0.f ? z : z * leak;
-  };
-  float4* y4 = reinterpret_cast<float4*>(y);
-  for (int64_t v = t; v < V; v += kSmallT) {
-    const float4 a = x4[v * C4 + blockIdx.x];
-    y4[v * C4 + blockIdx.x] = make_float4(f(a.x, 0), f(a.y, 1), f(a.z, 2), f(a.w, 3));
-  }
-}
-
-__global__ __launch_bounds__(kSmallT) void bn_small_bwd_kernel(const float* __restrict__ x,
-                                                               const float* __restrict__ dy, int64_t V, int C,
-                                                               const float* __restrict__ stats,
-                                                               const float* __restrict__ weight, float leak,
-                                                               int train, const float* __restrict__ addend,
-                                                               float* __restrict__ dx, float* __restrict__ dweight,
-                                                               float* __restrict__ dbias) {
-  __shared__ double red[16 * 8], tot[8];
-  const int c0 = 4 * blockIdx.x, C4 = C >> 2, t = threadIdx.x;
-  const BnStats st(stats, C);
-  float mh[4], ml[4], is[4], sc[4], sh[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int c = c0 + k;
-    mh[k] = st.mh[c];
-    ml[k] = st.ml[c];
-    is[k] = st.is[c];
-    sc[k] = st.sc[c];
-    sh[k] = st.sh[c];
-  }
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  const float4* g4 = reinterpret_cast<const float4*>(dy);
-  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int64_t v = t; v < V; v += kSmallT) {  // bn_reduce4_kernel<1>'s terms
-    const float4 a = x4[v * C4 + blockIdx.x], g = g4[v * C4 + blockIdx.x];
-    const float xs[4] = {a.x, a.y, a.z, a.w}, gs[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float xc = (xs[k] - mh[k]) - ml[k];
-      const float z = xc * sc[k] + sh[k];
-      const float dz = z > 0.f ? gs[k] : gs[k] * leak;
-      s[k] += dz;
-      s[4 + k] += (double)dz * ((double)xc * is[k]);
-    }
-  }
-  block_sum8(s, red, tot);
-  if (t < 4) {
-    if (dbias) dbias[c0 + t] = (float)tot[t];
-    if (dweight) dweight[c0 + t] = (float)tot[4 + t];
-  }
-  const double invV = V > 0 ? 1.0 / (double)V : 0.0;
-  float ws[4], mdz[4], mdzx[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    ws[k] = (weight ? weight[c0 + k] : 1.f) * is[k];
-    mdz[k] = train ? (float)(tot[k] * invV) : 0.f;
-    mdzx[k] = train ? (float)(tot[4 + k] * invV) : 0.f;
-  }
-  auto f = [&](float xv, float g, int k) {  // bn_bwd_apply4_kernel's arithmetic
-    const float xc = (xv - mh[k]) - ml[k];
-    const float dz = xc * sc[k] + sh[k] > 0.f ? g : g * leak;
-    if (!train) return ws[k] * dz;
-    return ws[k] * (dz - mdz[k] - (xc * is[k]) * mdzx[k]);
-  };
-  float4* d4 = reinterpret_cast<float4*>(dx);
-  for (int64_t v = t; v < V; v += kSmallT) {
-    const float4 a = x4[v * C4 + blockIdx.x], g = g4[v * C4 + blockIdx.x];
-    float4 d = make_float4(f(a.x, g.x, 0), f(a.y, g.y, 1), f(a.z, g.z, 2), f(a.w, g.w, 3));
-    if (addend) {
-      const float4 e = reinterpret_cast<const float4*>(addend)[v * C4 + blockIdx.x];
-      d = make_float4(d.x + e.x, d.y + e.y, d.z + e.z, d.w + e.w);
-    }
-    d4[v * C4 + blockIdx.x] = d;
-  }
-}
-
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // blocks for the column-owning vector kernels: R = 256 / (C/4) rows per block pass
@@ -748,33 +564,6 @@ int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const do
                      msp_stream_t stream) {
   return msp_bn_bwd_apply_add(x, dy, V, C, partial, stats, weight, leak, train, nullptr, dx, dweight, dbias,
                               stream);
-}
-
-int msp_bn_small_ok(int64_t V, int C) { return (V >= 0 && V <= kSmallV && C > 0 && C % 4 == 0) ? 1 : 0; }
-
-int msp_bn_forward_small(const float* x, int64_t V, int C, const double* partial, double eps, double momentum,
-                         int train, float* running_mean, float* running_var, const float* weight, const float* bias,
-                         float* stats, float leak, float* y, msp_stream_t stream) {
-  MSP_REQUIRE(msp_bn_small_ok(V, C), "msp_bn_forward_small: needs V <= %lld and C %% 4 == 0 (V=%lld C=%d)",
-              (long long)kSmallV, (long long)V, C);
-  MSP_REQUIRE((V == 0 || (aligned16(x) && aligned16(y))) && running_mean && running_var && stats,
-              "msp_bn_forward_small: bad pointers");
-  bn_small_fwd_kernel<<<(unsigned)(C / 4), kSmallT, 0, as_stream(stream)>>>(
-      x, V, C, partial, bn_parts(V, C), eps, momentum, train, running_mean, running_var, weight, bias, stats, leak, y);
-  return check_launch("msp_bn_forward_small");
-}
-
-int msp_bn_backward_small(const float* x, const float* dy, int64_t V, int C, const float* stats, const float* weight,
-                          float leak, int train, const float* addend, float* dx, float* dweight, float* dbias,
-                          msp_stream_t stream) {
-  MSP_REQUIRE(msp_bn_small_ok(V, C), "msp_bn_backward_small: needs V <= %lld and C %% 4 == 0 (V=%lld C=%d)",
-              (long long)kSmallV, (long long)V, C);
-  MSP_REQUIRE(V == 0 || (aligned16(x) && aligned16(dy) && aligned16(dx) && (!addend || aligned16(addend))),
-              "msp_bn_backward_small: rows must be 16-byte aligned");
-  MSP_REQUIRE(addend == nullptr || addend != dx || V * C == 0, "msp_bn_backward_small: addend must not alias dx");
-  bn_small_bwd_kernel<<<(unsigned)(C / 4), kSmallT, 0, as_stream(stream)>>>(x, dy, V, C, stats, weight, leak, train,
-                                                                            addend, dx, dweight, dbias);
-  return check_launch("msp_bn_backward_small");
 }
 
 int msp_join_cols(const float* a, int ca, const float* b, int cb, int64_t V, float* out, double* partial,

@@ -81,9 +81,6 @@ PROTOTYPES = {
     "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),
-    "msp_bn_small_ok": (I, [I64, I]),
-    "msp_bn_forward_small": (I, [P, I64, I, P, D, D, I, P, P, P, P, P, F, P, P]),
-    "msp_bn_backward_small": (I, [P, P, I64, I, P, P, F, I, P, P, P, P, P]),
     "msp_join_cols": (I, [P, I, P, I, I64, P, P, P]),
     "msp_split_cols": (I, [P, I64, I, I, P, P, P]),
     "msp_nin_gemm_ok": (I, [I64, I, I]),

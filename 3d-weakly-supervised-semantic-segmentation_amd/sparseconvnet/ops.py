@@ -533,17 +533,6 @@ def _bn_partial_buf(V, C, device):
     return torch.empty((P + 1) * 2 * C, dtype=torch.float64, device=device)
 
 
-# Small levels (msp_bn_small_ok: up to 16384 rows): one launch per direction (msp_bn_forward_small /
-# msp_bn_backward_small); the joins feeding them skip their statistics (bn_small).  False (MSP_BN_SMALL=0): the
-# three-launch form.
-BN_SMALL = os.environ.get("MSP_BN_SMALL", "1") != "0"
-
-
-def bn_small(V, C):
-    """Whether a BatchNormalization over V rows of C channels takes the one-launch small-level form."""
-    return BN_SMALL and bool(int(_lib.query("msp_bn_small_ok", _lib.I64(V), C)))
-
-
 def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial):
     """y, stats of BN + (leaky) ReLU; `partial` = the msp_bn_stats partials of
     x when a residual join already produced them (msp_add_bn_stats), else None."""
@@ -551,12 +540,6 @@ def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, tra
     s = _stream(x)
     stats = torch.empty((5, C), dtype=torch.float32, device=x.device)
     y = torch.empty_like(x)
-    if bn_small(V, C):
-        _record(_shape("bn_fwd/hbm", C, C, V), 0, lambda: call(
-            "msp_bn_forward_small", ptr(x), V, C, ptr(partial), float(eps), float(momentum), int(train),
-            ptr(running_mean), ptr(running_var), ptr(weight), ptr(bias), ptr(stats), float(leak), ptr(y), s),
-            4 * V * C * (3 if (partial is None and train) else 2))
-        return y, stats
 
     def run(partial=partial):
         if partial is None:
@@ -577,16 +560,10 @@ def _bn_bwd(x, weight, stats, cfg, gy, addend):
     gy = gy.contiguous()
     V, C = x.shape
     s = _stream(x)
+    partial = _bn_partial_buf(V, C, x.device)
     dx = torch.empty_like(x)
     dw = torch.empty(C, dtype=torch.float32, device=x.device)
     db = torch.empty(C, dtype=torch.float32, device=x.device)
-    if bn_small(V, C):
-        _record(_shape("bn_bwd/hbm", C, C, V), 0, lambda: call(
-            "msp_bn_backward_small", ptr(x), ptr(gy), V, C, ptr(stats), ptr(weight) if has_w else None, leak, train,
-            ptr(addend) if addend is not None else None, ptr(dx), ptr(dw), ptr(db), s),
-            4 * V * C * (5 + (addend is not None)))
-        return dx, (dw if has_w else None), (db if has_b else None)
-    partial = _bn_partial_buf(V, C, x.device)
 
     def run():
         call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
@@ -658,9 +635,6 @@ class ResidualJoinFunction(torch.autograd.Function):
         _check_feats(b)
         a, b = a.contiguous(), b.contiguous()
         V, C = a.shape
-        if bn_small(V, C):  # the BatchNormalization it feeds sums its own statistics (one launch): plain add
-            ctx.set_materialize_grads(False)
-            return torch.add(a, b), None
         out = torch.empty_like(a)
         partial = _bn_partial_buf(V, C, a.device)
         _record(_shape("bn_join/hbm", C, C, V), 0, lambda: call("msp_add_bn_stats", ptr(a), ptr(b), V, C, ptr(out), ptr(partial),
@@ -689,7 +663,7 @@ class JoinFunction(torch.autograd.Function):
         cb = b.size(1)
         C = ca + cb
         out = torch.empty((V, C), dtype=torch.float32, device=a.device)
-        partial = _bn_partial_buf(V, C, a.device) if stats and not bn_small(V, C) else None
+        partial = _bn_partial_buf(V, C, a.device) if stats else None
         _record(_shape("bn_join/hbm", C, C, V), 0, lambda: call(
             "msp_join_cols", ptr(a), ca, ptr(b), cb, V, ptr(out), ptr(partial), _stream(a)), 8 * V * C)
         ctx.dims = (ca, cb)

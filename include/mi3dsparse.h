@@ -345,19 +345,6 @@ int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, cons
                          float* dx, float* dweight, float* dbias, msp_stream_t stream);
 int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,
                      msp_stream_t stream);
-/* Small levels (round 4): V <= 16384 rows and C % 4 == 0 (msp_bn_small_ok) -- one launch per direction instead of
- * statistics + finalize + apply, one block per four channels.  msp_bn_forward_small = msp_bn_stats (skipped when
- * partial is non-NULL: a join's partials, msp_bn_partials(V, C) blocks) + msp_bn_finalize + msp_bn_apply;
- * msp_bn_backward_small = msp_bn_bwd_stats + msp_bn_bwd_apply_add (dweight / dbias / addend may be NULL).  Same
- * arithmetic per element; the statistics are summed in a different fixed order (deterministic), so results agree
- * with the three-launch form to rounding, not bit for bit.  Rows 16-byte aligned. */
-int msp_bn_small_ok(int64_t V, int C);
-int msp_bn_forward_small(const float* x, int64_t V, int C, const double* partial, double eps, double momentum,
-                         int train, float* running_mean, float* running_var, const float* weight, const float* bias,
-                         float* stats, float leak, float* y, msp_stream_t stream);
-int msp_bn_backward_small(const float* x, const float* dy, int64_t V, int C, const float* stats, const float* weight,
-                          float leak, int train, const float* addend, float* dx, float* dweight, float* dbias,
-                          msp_stream_t stream);
 /* Channel join (SCN JoinTable, the UNet / FCN skip joins: identity branch first, then the upsampled deeper
  * level): out[v] = [a[v] | b[v]], a [V][ca], b [V][cb], out [V][ca + cb].  With partial
  * non-NULL also the msp_bn_stats partials of out (identical to msp_bn_stats on it), for the BatchNormalization

@@ -218,10 +218,7 @@ def test_join_table(ca, cb):
             tb = scn.SparseConvNetTensor(b, t.metadata, t.spatial_size)
             j = scn.JoinTable().train()([ta, tb])
             assert torch.equal(j.features, torch.cat([a, b], 1))
-            # partials for the BN it feeds, unless that BN sums its own (one-launch small-level form)
-            from sparseconvnet import ops
-            want = fuse and not ops.bn_small(a.size(0), ca + cb)
-            assert (getattr(j, "_bn_partial", None) is not None) == want
+            assert (getattr(j, "_bn_partial", None) is not None) == fuse
             bn = scn.BatchNormReLU(ca + cb).to(DEV)
             y = bn(j).features
             y.backward(g)
@@ -563,51 +560,6 @@ def test_residual_block_fused_matches_unfused(C, leak, nin):
         assert n1 == n2 and torch.equal(p1.grad, p2.grad), n1
     for (n1, b1), (n2, b2) in zip(fused.named_buffers(), plain.named_buffers()):
         assert torch.equal(b1, b2), n1
-
-
-@pytest.mark.parametrize("C,leak,train", [(32, 0.0, True), (64, 0.333, True), (160, 0.0, False), (224, 0.0, True)])
-def test_bn_small_matches_three_launch(C, leak, train):
-    """Small levels (msp_bn_small_ok): the one-launch BatchNormalization (msp_bn_forward_small /
-    msp_bn_backward_small, the residual join skipping its statistics) against the three-launch form on a residual
-    block (fork, BN-SubM-BN-SubM, join, BN): outputs, input and parameter gradients and running statistics agree to
-    rounding (the statistics are summed in another fixed order), and each form is deterministic."""
-    from sparseconvnet import ops
-    torch.manual_seed(C)
-    coords, feats = _inputs(3000, 24, n_feat=C)
-    g, _ = _pair(coords, feats)
-    assert ops.bn_small(g.features.size(0), C)
-
-    def run(small):
-        ops.BN_SMALL = small
-        try:
-            torch.manual_seed(1)
-            blk = scn.Sequential().add(
-                scn.ConcatTable().add(scn.Identity()).add(
-                    scn.Sequential().add(scn.BatchNormLeakyReLU(C, leakiness=leak))
-                    .add(scn.SubmanifoldConvolution(3, C, C, 3, False))
-                    .add(scn.BatchNormLeakyReLU(C, leakiness=leak))
-                    .add(scn.SubmanifoldConvolution(3, C, C, 3, False)))).add(scn.AddTable()).add(
-                scn.BatchNormReLU(C)).to(DEV)
-            with torch.no_grad():
-                for m in blk.modules():
-                    if isinstance(m, scn.BatchNormalization):
-                        m.running_mean.copy_(torch.linspace(-0.5, 0.5, C))
-                        m.running_var.copy_(torch.linspace(0.5, 2.0, C))
-            blk.train(train)
-            x = g.features.detach().clone().requires_grad_(True)
-            y = blk(type(g)(x, g.metadata, g.spatial_size)).features
-            w = torch.linspace(-1, 1, y.numel(), device=DEV).view_as(y)
-            (y * w).square().sum().backward()
-            return ([y.detach(), x.grad] + [p.grad for p in blk.parameters()] + [b.clone() for b in blk.buffers()])
-        finally:
-            ops.BN_SMALL = True
-
-    a, a2, b = run(True), run(True), run(False)
-    for u, v in zip(a, a2):
-        assert torch.equal(u, v)
-    for k, (u, v) in enumerate(zip(a, b)):
-        err = (u - v).abs().max().item()
-        assert err <= 2e-6 * max(1.0, v.abs().max().item()), (k, err)
 
 
 @pytest.mark.parametrize("M,K,N", [(300007, 64, 32), (40000, 128, 64), (9001, 192, 96), (5000, 320, 160),
