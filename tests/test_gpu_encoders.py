@@ -250,6 +250,9 @@ def test_prefetch_batches_count_reads():
             if r._wchunk:
                 wq = q.wgrad_index()
                 assert wq is not None and torch.equal(r._wchunk["chunk_lr"], wq["chunk_lr"])
+                assert r._wchunk["n_far"] == wq["n_far"]  # rules past a tile's staged rows, counted in the replay
+                if wq["n_far"]:
+                    assert torch.equal(r._wchunk["far_key"], wq["far_key"])
         for stride, (csize, r) in lvl.down.items():
             q = ref.down[stride][1]
             assert r.pairs.counts == q.pairs.counts and torch.equal(r.down, q.down)
