@@ -3,8 +3,7 @@
 // convolution (msp_dense_order) and the deterministic index_add_ (msp_tail.hip).  Written for gfx950 instead of
 // a library sort so that no third-party kernel runs in the step.
 //
-// 8-bit digits, one pass per digit.  Up to 2048 tiles of 16384 pairs (every sort of the step), two launches per
-// pass (radix_hist_big_kernel / radix_scatter_big_kernel, below); larger sorts: tiles of 4096 pairs (256 threads x 16 rounds of one pair per thread,
+// 8-bit digits, one pass per digit.  Tiles of kTile = 4096 pairs (256 threads x 16 rounds of one pair per thread,
 // each round 256 consecutive pairs).  Per pass:
 //   radix_hist_kernel     per-tile digit counts (LDS integer atomics), written digit-major: counts[d][tile];
 //   scan_exclusive_i64    over the counts -> for every (digit, tile) the first output position;
@@ -98,101 +97,6 @@ __global__ __launch_bounds__(kSortT) void radix_scatter_kernel(const uint64_t* _
   }
 }
 
-// ---- two-kernel passes (n <= kBigTileMax * kBigTile pairs: every sort the step runs).  Tiles of kBigTile pairs;
-// the histogram kernel writes counts[tile][digit] (digit-minor: the scatter's prologue reads them coalesced), and
-// each scatter block derives its own starts from them -- digit totals over all tiles, their exclusive scan over
-// digits, plus its digit's count in the tiles before it -- so a pass is 2 launches instead of 6 (the scan of the
-// counts was 3 more kernels and a dispatch wait each beside a running step).  Pairs are streamed a round ahead
-// instead of held in registers.
-constexpr int kBigRounds = 64;
-constexpr int kBigTile = kSortT * kBigRounds;  // 16384 pairs
-constexpr int64_t kBigTileMax = 2048;
-
-__global__ __launch_bounds__(kSortT) void radix_hist_big_kernel(const uint64_t* __restrict__ keys, int64_t n,
-                                                                int shift, int bits, int32_t* __restrict__ counts) {
-  __shared__ int h[kRadix];
-  const int t = threadIdx.x;
-  h[t] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kBigTile + t;
-  const uint64_t mask = (1ull << bits) - 1;
-#pragma unroll 8
-  for (int r = 0; r < kBigRounds; ++r) {
-    const int64_t i = base + (int64_t)r * kSortT;
-    if (i < n) atomicAdd(&h[(int)((keys[i] >> shift) & mask)], 1);
-  }
-  __syncthreads();
-  counts[(int64_t)blockIdx.x * kRadix + t] = h[t];
-}
-
-__global__ __launch_bounds__(kSortT) void radix_scatter_big_kernel(const uint64_t* __restrict__ kin,
-                                                                   const int32_t* __restrict__ vin,
-                                                                   uint64_t* __restrict__ kout,
-                                                                   int32_t* __restrict__ vout, int64_t n, int shift,
-                                                                   int bits, int64_t n_tiles,
-                                                                   const int32_t* __restrict__ counts) {
-  __shared__ int64_t base_s[kRadix];
-  __shared__ int cnt_s[kSortT / 64][kRadix];
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const int64_t tile = blockIdx.x;
-  // this block's start of digit t: (pairs of smaller digits) + (pairs of digit t in earlier tiles)
-  int64_t tot = 0, pre = 0;
-  for (int64_t u = 0; u < n_tiles; ++u) {
-    const int c = counts[u * kRadix + t];
-    tot += c;
-    if (u < tile) pre += c;
-  }
-  int64_t below;
-  const int64_t ex = block_excl_scan<kSortT>(tot, &below);
-  base_s[t] = ex + pre;
-#pragma unroll
-  for (int w = 0; w < kSortT / 64; ++w) cnt_s[w][t] = 0;
-  const uint64_t mask = (1ull << bits) - 1;
-  const int64_t tile0 = tile * kBigTile + t;
-  const unsigned long long below_lane = (1ull << lane) - 1;
-  uint64_t kn = tile0 < n ? kin[tile0] : 0;
-  int32_t vn = tile0 < n ? vin[tile0] : 0;
-  __syncthreads();
-#pragma unroll 1
-  for (int r = 0; r < kBigRounds; ++r) {
-    const int64_t i = tile0 + (int64_t)r * kSortT;
-    const bool live = i < n;
-    const uint64_t k = kn;
-    const int32_t v = vn;
-    if (r + 1 < kBigRounds) {  // the next round's pair in flight while this one is ranked
-      const int64_t j = i + kSortT;
-      kn = j < n ? kin[j] : 0;
-      vn = j < n ? vin[j] : 0;
-    }
-    const int d = (int)((k >> shift) & mask);
-    unsigned long long peers = ballot64(live);
-    for (int b = 0; b < bits; ++b) {
-      const bool bit = (d >> b) & 1;
-      const unsigned long long m = ballot64(bit);
-      peers &= bit ? m : ~m;
-    }
-    const int rank = __popcll(peers & below_lane);
-    if (live && rank == 0) cnt_s[wave][d] = __popcll(peers);
-    __syncthreads();
-    if (live) {
-      int64_t pos = base_s[d] + rank;
-      for (int w = 0; w < wave; ++w) pos += cnt_s[w][d];
-      kout[pos] = k;
-      vout[pos] = v;
-    }
-    __syncthreads();
-    int add = 0;
-#pragma unroll
-    for (int w = 0; w < kSortT / 64; ++w) {
-      add += cnt_s[w][t];
-      cnt_s[w][t] = 0;
-    }
-    base_s[t] += add;
-    __syncthreads();
-    if (tile * kBigTile + (int64_t)(r + 1) * kSortT >= n) break;  // block-uniform: past the last pair
-  }
-}
-
 inline size_t al256s(size_t b) { return (b + 255) & ~(size_t)255; }
 
 }  // namespace msp
@@ -204,8 +108,6 @@ extern "C" {
 size_t msp_sort_workspace_size(int64_t n, int end_bit) {
   (void)end_bit;
   if (n <= 0) return 256;
-  if (ceil_div(n, kBigTile) <= kBigTileMax)
-    return al256s((size_t)n * 8) + al256s((size_t)n * 4) + al256s((size_t)ceil_div(n, kBigTile) * kRadix * 4);
   const int64_t n_tiles = ceil_div(n, kSortTile);
   const int64_t m = (int64_t)kRadix * n_tiles;
   return al256s((size_t)n * 8) + al256s((size_t)n * 4) + 2 * al256s((size_t)m * 8) + al256s(8) +
@@ -221,27 +123,6 @@ int msp_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* v
   MSP_REQUIRE(ws && ws_bytes >= need, "msp_sort_pairs: workspace too small (%zu < %zu)", ws_bytes, need);
   MSP_REQUIRE(keys_out != keys_in && vals_out != vals_in, "msp_sort_pairs: outputs must not alias the inputs");
   hipStream_t s = as_stream(stream);
-  const int passes = (end_bit + 7) / 8;
-  if (ceil_div(n, kBigTile) <= kBigTileMax) {  // two launches per pass
-    const int64_t nt = ceil_div(n, kBigTile);
-    char* w = static_cast<char*>(ws);
-    uint64_t* kt = reinterpret_cast<uint64_t*>(w);
-    int32_t* vt = reinterpret_cast<int32_t*>(w + al256s((size_t)n * 8));
-    int32_t* counts = reinterpret_cast<int32_t*>(w + al256s((size_t)n * 8) + al256s((size_t)n * 4));
-    const uint64_t* ksrc = keys_in;
-    const int32_t* vsrc = vals_in;
-    for (int p = 0; p < passes; ++p) {
-      const int shift = 8 * p, bits = end_bit - shift < 8 ? end_bit - shift : 8;
-      const bool to_out = ((passes - 1 - p) & 1) == 0;
-      uint64_t* kdst = to_out ? keys_out : kt;
-      int32_t* vdst = to_out ? vals_out : vt;
-      radix_hist_big_kernel<<<(unsigned)nt, kSortT, 0, s>>>(ksrc, n, shift, bits, counts);
-      radix_scatter_big_kernel<<<(unsigned)nt, kSortT, 0, s>>>(ksrc, vsrc, kdst, vdst, n, shift, bits, nt, counts);
-      ksrc = kdst;
-      vsrc = vdst;
-    }
-    return check_launch("msp_sort_pairs");
-  }
   const int64_t n_tiles = ceil_div(n, kSortTile);
   const int64_t m = (int64_t)kRadix * n_tiles;
   char* w = static_cast<char*>(ws);
@@ -256,6 +137,7 @@ int msp_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* v
   int64_t* total = reinterpret_cast<int64_t*>(w);
   w += al256s(8);
   void* sws = w;
+  const int passes = (end_bit + 7) / 8;
   const uint64_t* ksrc = keys_in;
   const int32_t* vsrc = vals_in;
   for (int p = 0; p < passes; ++p) {
