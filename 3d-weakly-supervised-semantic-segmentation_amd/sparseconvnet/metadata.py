@@ -59,7 +59,8 @@ class _Deferred:
         self.after.append(fn)
 
     def flush(self):
-        with torch.cuda.stream(self.stream):
+        import contextlib
+        with torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext():
             while self.reads or self.after:
                 if self.reads:
                     reads, self.reads = self.reads, []
