@@ -358,9 +358,6 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 // AC (accumulation): 1 = the six piece products of a step go straight into the group's running sums, smallest
 // first (the product form); 0 = summed in a zeroed accumulator and added with a vector add (round 2-3 form:
 // about a third of the rounding error, 6-9 % slower -- profiles/r03/kbexp_r03x_accumulate.log).
-#ifndef MSP_X6S_SETPRIO  // experiments build: 1 = s_setprio 2 around each group's MFMAs
-#define MSP_X6S_SETPRIO 0
-#endif
 template <int NT, int AB = 0, int AC = 1>
 __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
@@ -517,9 +514,6 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
 #pragma unroll
           for (int p = 0; p < 3; ++p) cur[p] = f ? fp[p] : cur[p];
         }
-#if MSP_X6S_SETPRIO
-        __builtin_amdgcn_s_setprio(2);  // experiment: the wave issuing its MFMAs ahead of the others
-#endif
         if constexpr (AC == 1) {  // smallest products first, straight into the running sums
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[g][t] = mfma_bf16(w[t][2], cur[0], acc[g][t]);
@@ -550,9 +544,6 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[g][t] += c[t];
         }
-#if MSP_X6S_SETPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
       }
     }
   };
