@@ -376,7 +376,29 @@ __global__ __launch_bounds__(kThreads) void conv_x6d_kernel(
 // the current run's first chunk (uniform branches; the chunk values keep
 // their D-deep pipeline across runs).
 // TR: output rows per wave tile (128, or 64: half the LDS accumulator tile per wave, so twice the blocks per CU).
-template <int NT, int NKK, int D, int NW, int TR = 128>
+#ifdef MSP_EXPERIMENTS
+// x [n][c] fp32 (c % 32 == 0) -> its exact split image: row i, 32-channel slice kk, piece p, k-octet q at 16-byte
+// unit (i * c / 32 + kk) * 12 + p * 4 + q.  One thread per (row, k-octet).
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ x, int64_t n, int c,
+                                                         u32x4* __restrict__ img) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int oc = c / 8;
+  if (g >= n * oc) return;
+  const int64_t row = g / oc;
+  const int o = (int)(g - row * oc), kk = o >> 2, q = o & 3;
+  const floatx4* src = reinterpret_cast<const floatx4*>(x + row * c + 8 * o);
+  u32x4 pc[3];
+  split8(src[0], src[1], pc);
+  u32x4* dst = img + (row * (c / 32) + kk) * 12 + q;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) dst[p * 4] = pc[p];
+}
+#endif
+
+// PS 1 (experiments build only; measured slower): x is the exact split image of the input rows (split_rows_kernel: per row and 32-channel slice, 3 pieces x 4
+// k-octets of 16 bytes, row stride 6 c_in bytes), so the chunk loop loads the pieces instead of splitting every
+// gathered row per rule.
+template <int NT, int NKK, int D, int NW, int TR = 128, int PS = 0>
 __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -443,7 +465,7 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
     int src, row;
   };
   struct Val {
-    floatx4 a[NKK][2];
+    floatx4 a[NKK][PS ? 3 : 2];
   };
   auto ld_idx = [&](int64_t c, St& d) {
     const int64_t cc = c < clast ? c : clast;
@@ -451,6 +473,14 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
     d.row = chunk_row[cc * MSP_CHUNK + r];
   };
   auto ld_val = [&](const St& d, Val& v) {
+    if constexpr (PS) {  // the row's units (kk, p, q): 16 bytes each, 12 per 32-channel slice
+      const floatx4* xs = reinterpret_cast<const floatx4*>(x) + (uint32_t)d.src * (uint32_t)(NKK * 12) + q;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) v.a[kk][p] = xs[kk * 12 + p * 4];
+      return;
+    }
     const char* xs = reinterpret_cast<const char*>(x) + (uint32_t)d.src * (uint32_t)c_in * 4u;
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
@@ -467,7 +497,12 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
       u32x4 xp[3];
-      split8(v.a[kk][0], v.a[kk][1], xp);
+      if constexpr (PS) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) xp[p] = __builtin_bit_cast(u32x4, v.a[kk][p]);
+      } else {
+        split8(v.a[kk][0], v.a[kk][1], xp);
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         floatx4 c = acc[t];
@@ -514,7 +549,10 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
       }
       if (i < n) run(S[k], Wc, rowR[k]);
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) asm volatile("" ::"v"(S[k].a[kk][0]), "v"(S[k].a[kk][1]));
+      for (int kk = 0; kk < NKK; ++kk) {
+        asm volatile("" ::"v"(S[k].a[kk][0]), "v"(S[k].a[kk][1]));
+        if constexpr (PS) asm volatile("" ::"v"(S[k].a[kk][PS ? 2 : 0]));
+      }
       ld_val(J[k], S[k]);  // chunk c+k+D
       rowR[k] = J[k].row;
       ld_idx(c + k + 2 * D, J[k]);
@@ -578,17 +616,34 @@ int launch_x6r_exp(int variant, const float* x, int c_in, const float* wt, int K
                                                                        (flip >> 1) & 1);
   flip &= 1;
   const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
+  // variant 100 + v: pre-split rows (the split pass into the workspace past the weight image, then the PS kernel);
+  // 200 + v: the PS kernel alone on whatever the workspace holds (timing only)
+  const int ps = variant / 100;
+  variant %= 100;
   const int D = variant / 10, T = variant % 10 == 1 ? 64 : 128;
   if (T != tile_rows) return MSP_EINVAL;
+  const float* xin = x;
+  if (ps) {
+    if (c_in % 32) return MSP_EINVAL;
+    u32x4* img = wimg + (units + 63) / 64 * 64;
+    if (ps == 1)
+      split_rows_kernel<<<(unsigned)ceil_div(n_rows * (c_in / 8), 256), 256, 0, s>>>(x, n_rows, c_in, img);
+    xin = reinterpret_cast<const float*>(img);
+  }
 #define LE(N, C, DD, TT)                                                                                        \
   if (NT == N && NKK == C && D == DD && T == TT) {                                                             \
-    conv_x6r_kernel<N, C, DD, 2, TT><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,      \
-                                                               chunk_off, chunk_src, chunk_row, n_rows,        \
-                                                               n_tiles, n_y, out);                             \
+    if (ps)                                                                                                    \
+      conv_x6r_kernel<N, C, DD, 2, TT, 1><<<grid, kThreads, 0, s>>>(xin, c_in, wimg, K, flip, c_out,           \
+                                                                    tile_start, chunk_off, chunk_src,          \
+                                                                    chunk_row, n_rows, n_tiles, n_y, out);     \
+    else                                                                                                       \
+      conv_x6r_kernel<N, C, DD, 2, TT><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,    \
+                                                                 chunk_off, chunk_src, chunk_row, n_rows,      \
+                                                                 n_tiles, n_y, out);                           \
     return MSP_OK;                                                                                             \
   }
   LE(2, 1, 3, 128) LE(2, 1, 3, 64) LE(2, 1, 2, 128) LE(2, 1, 2, 64)
-  LE(2, 2, 3, 128) LE(2, 2, 3, 64) LE(2, 2, 2, 64)
+  LE(2, 2, 3, 128) LE(2, 2, 3, 64) LE(2, 2, 2, 64) LE(2, 2, 2, 128)
 #undef LE
   set_error("launch_x6r_exp: no variant %d for c_in=%d c_out=%d", variant, c_in, c_out);
   return MSP_EINVAL;
@@ -1166,7 +1221,8 @@ int msp_exp_conv_x6r(int variant, const float* x, int c_in, const float* wt, int
                      const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
                      msp_stream_t stream) {
   MSP_REQUIRE(c_out <= 32 && c_in <= 64 && c_in % 16 == 0 && c_out % 16 == 0, "msp_exp_conv_x6r: shape");
-  MSP_REQUIRE(ws && ws_bytes >= x6p_ws_bytes(K, c_in, c_out), "msp_exp_conv_x6r: workspace");
+  const size_t need = x6p_ws_bytes(K, c_in, c_out) + 1024 + (variant >= 100 ? (size_t)n_rows * c_in * 6 : 0);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_exp_conv_x6r: workspace");
   if (n_rows <= 0) return MSP_OK;
   const int rc = launch_x6r_exp(variant, x, c_in, wt, K, flip, c_out, tile_rows, tile_start, chunk_off, chunk_src,
                                 chunk_row, n_rows, out, ws, as_stream(stream));

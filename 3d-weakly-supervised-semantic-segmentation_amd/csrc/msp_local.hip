@@ -1141,6 +1141,8 @@ int msp_conv_wgrad_far(const float* x, int c_in, const float* dy, int c_out, int
               c_out);
   if (n_far == 0) return MSP_OK;
   MSP_REQUIRE(x && dy && chunk_src && chunk_row && far_key && far_tile && dw, "msp_conv_wgrad_far: NULL pointer");
+  MSP_REQUIRE(((uintptr_t)dy & 15) == 0 && ((uintptr_t)dw & 15) == 0,
+              "msp_conv_wgrad_far: dy and dw must be 16-byte aligned (float4 rows)");
   hipStream_t s = as_stream(stream);
   const unsigned grid = (unsigned)(K * (c_in / 32) * (c_out / 32));
   wgrad_far_kernel<<<grid, 256, 0, s>>>(x, c_in, dy, c_out, chunk_src, chunk_row,

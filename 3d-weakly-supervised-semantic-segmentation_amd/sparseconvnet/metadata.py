@@ -117,6 +117,17 @@ def _defer():
     return getattr(_TLS, "defer", None)
 
 
+class _PendingIndex:
+    """SubmRules._wchunk while a replay's count reads are still queued (wgrad_index decides once they are read).
+    Not an index: consumers call wgrad_index(wait=True), which flushes the replay's reads first."""
+
+    def __repr__(self):
+        return "<weight-gradient index pending>"
+
+
+_PENDING = _PendingIndex()
+
+
 def _later(t, fn):
     """fn(values of the int64 device tensor t): now, or at the next flush of the replay in progress."""
     d = _defer()
@@ -332,17 +343,29 @@ class SubmRules:
                                                         _lib.stream(self.nbr.device), tile_rows, lists_only=True)
         return t
 
-    def wgrad_index(self):
+    def wgrad_index(self, wait=False):
         """msp_wgrad_chunk_index over the 128-row tile rulebook and the tile-local lists of each tile's distinct
         input rows for msp_conv_wgrad_chunk, built on first use.  Rules whose input row lies past the rows a tile
         stages (a tile listing more than msp_wgrad_chunk_cap rows) are listed apart (msp_wgrad_far_list, sorted)
-        and added by msp_conv_wgrad_far: the chunk form serves every map."""
+        and added by msp_conv_wgrad_far: the chunk form serves every map.
+
+        Inside a replay whose counts are not read yet this returns the _PENDING sentinel (the index is built when
+        the replay flushes its reads); wait=True (every consumer of the index) flushes them first, so the caller
+        always gets the index itself."""
+        if self._wchunk is _PENDING:
+            if not wait:
+                return self._wchunk
+            d = _defer()
+            if d is not None:
+                d.flush()
+            if self._wchunk is _PENDING:  # the replay ended without deciding (its flush failed): build it now
+                self._wchunk = None
         if self._wchunk is None:
             loc = self.lists()
             tiles = self.tiles_for(128)
             if "max_u" not in loc or "n_chunks" not in tiles:
                 # in a replay, counts not read yet: build the index once they are read (one read for both)
-                self._wchunk = "pending"
+                self._wchunk = _PENDING
 
                 def decide():
                     self._wchunk = None
@@ -597,6 +620,11 @@ class Metadata:
             _TLS.defer.flush()
         finally:
             _TLS.defer = outer
+            # a flush that raised leaves weight-gradient indices undecided: forget them (built again on use)
+            for lvl in self.levels.values():
+                for r in getattr(lvl, "subm", {}).values():
+                    if getattr(r, "_wchunk", None) is _PENDING:
+                        r._wchunk = None
 
     def _replay(self, plan):
         from . import ops
@@ -695,9 +723,10 @@ def prefetch(coords, spatial_size, plan, wait_for_producer=True):
         pend = _PREFETCHED.setdefault(dev.index, [])
         # an unconsumed entry for the same coords, and the oldest beyond the depth, are dropped (memory goes back)
         pend[:] = [e for e in pend if e[0] is not coords][-(PREFETCH_DEPTH - 1):] if PREFETCH_DEPTH > 1 else []
-        side = _SIDE.get(dev.index)
+        # one side stream per (device, priority): a later change of PREFETCH_PRIORITY takes effect
+        side = _SIDE.get((dev.index, PREFETCH_PRIORITY))
         if side is None:
-            side = _SIDE[dev.index] = torch.cuda.Stream(dev, priority=PREFETCH_PRIORITY)
+            side = _SIDE[(dev.index, PREFETCH_PRIORITY)] = torch.cuda.Stream(dev, priority=PREFETCH_PRIORITY)
     cur = torch.cuda.current_stream(dev)
     if isinstance(wait_for_producer, torch.cuda.Event):
         side.wait_event(wait_for_producer)

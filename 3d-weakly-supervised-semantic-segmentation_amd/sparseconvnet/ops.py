@@ -237,7 +237,7 @@ def conv_wgrad_chunk(x, dy, rules, K, kind="wgrad", flops=None):
     x rows and the 128 dy rows staged in LDS once per 32 x 32 channel slice, the compacted chunks as MFMA
     k-steps (msp_conv_wgrad_chunk); partial sums per tile range added in order; then the rules of rows past a
     tile's staged capacity, if any (msp_conv_wgrad_far)."""
-    idx = rules.wgrad_index()
+    idx = rules.wgrad_index(wait=True)
     c_in, c_out = x.size(1), dy.size(1)
     n = dy.size(0)
     tiles = idx["tiles"]
@@ -323,7 +323,7 @@ class SubmanifoldConvFunction(torch.autograd.Function):
             dwp = None
             rules.note_use("wgrad", cin_p, cout_p)
             if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)) and \
-                    rules.wgrad_index() is not None:
+                    rules.wgrad_index(wait=True) is not None:
                 dwp, join = _on_side(xp, V, lambda: conv_wgrad_chunk(xp, g, rules, K, flops=2.0 * p.total * cin * cout))
             if dwp is None:  # pair lists (beside the backward-data on small levels or when WGRAD_CONCURRENT)
                 dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)
@@ -658,6 +658,11 @@ class JoinFunction(torch.autograd.Function):
     def forward(ctx, a, b, stats):
         _check_feats(a)
         _check_feats(b)
+        if a.dim() != 2 or b.dim() != 2 or b.size(0) != a.size(0):
+            raise ValueError(f"JoinTable: inputs must be [V, C] with the same row count, got {tuple(a.shape)} and "
+                             f"{tuple(b.shape)}")
+        if a.device != b.device:
+            raise ValueError(f"JoinTable: inputs on different devices ({a.device} and {b.device})")
         a, b = a.contiguous(), b.contiguous()
         V, ca = a.shape
         cb = b.size(1)

@@ -25,6 +25,9 @@ from __future__ import annotations
 
 import os
 
+import threading
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -234,7 +237,31 @@ def settle(device=None):
     if not (dist.is_initialized() and dist.get_backend() == "nccl"):
         return
     torch.cuda.synchronize(device)
-    dist.distributed_c10d._get_default_group()._wait_for_pending_works()
+    pg = dist.distributed_c10d._get_default_group()
+    wait = getattr(pg, "_wait_for_pending_works", None)
+    if wait is None:  # a torch build without the binding: wait out a few watchdog passes (the round-3 form)
+        time.sleep(SETTLE_FALLBACK_S)
+        return
+    # bounded: the binding polls with no timeout of its own, so it runs on a helper thread with a deadline
+    err = []
+
+    def run():
+        try:
+            wait()
+        except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
+            err.append(e)
+    th = threading.Thread(target=run, name="dp-settle", daemon=True)
+    th.start()
+    th.join(SETTLE_TIMEOUT_S)
+    if th.is_alive():
+        raise RuntimeError(f"dp.settle: the process group's watchdog did not retire its pending collectives within "
+                           f"{SETTLE_TIMEOUT_S:.0f} s (a collective that never completed?)")
+    if err:
+        raise err[0]
+
+
+SETTLE_TIMEOUT_S = 120.0   # dp.settle's deadline for the watchdog to retire the eager collectives
+SETTLE_FALLBACK_S = 0.35   # without _wait_for_pending_works: about three watchdog passes
 
 
 def max_over_ranks(x: float) -> float:

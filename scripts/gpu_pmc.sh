@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-3 PMC passes over the eager bench (2 timed steps): MFMA busy, wait states, LDS activity and bank
+# PMC passes over the eager bench (2 timed steps): MFMA busy, wait states, LDS activity and bank
 # conflicts, instruction mix, L2 hits per dispatch of the conv / wgrad / BN kernels.
-# Usage (GPU box): TAG=r03a bash scripts/gpu_pmc_r03.sh
+# Usage (GPU box): TAG=x bash scripts/gpu_pmc.sh
 set -o pipefail
 TAG=${TAG:-r03a}
 cd /tmp && export TMPDIR=/tmp

@@ -98,7 +98,7 @@ def conv_forms(rules, V, cin, cout):
             def f(x, wt, flip):
                 tl = rules.tiles_for(tr)
                 out = torch.empty(V, cout, device=DEV)
-                wsb = 27 * cout * ((cin + 31) // 32) * 32 * 6
+                wsb = 27 * cout * ((cin + 31) // 32) * 32 * 6 + 1024 + (V * cin * 6 if variant >= 100 else 0)
                 ws = torch.empty(max(wsb // 4, 1), device=DEV)
                 rc = fx(variant, ptr(x), cin, ptr(wt), 27, flip, cout, tr, ptr(tl["tile_start"]), ptr(tl["chunk_off"]),
                         ptr(tl["chunk_src"]), ptr(tl["chunk_row"]), V, ptr(out), ptr(ws), wsb, _lib.stream())

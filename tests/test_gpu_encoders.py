@@ -248,7 +248,7 @@ def test_prefetch_batches_count_reads():
                 assert torch.equal(r.pairs.pair_in, q.pairs.pair_in)
                 assert torch.equal(r.pairs.pair_out, q.pairs.pair_out)
             if r._wchunk:
-                wq = q.wgrad_index()
+                wq = q.wgrad_index(wait=True)
                 assert wq is not None and torch.equal(r._wchunk["chunk_lr"], wq["chunk_lr"])
                 assert r._wchunk["n_far"] == wq["n_far"]  # rules past a tile's staged rows, counted in the replay
                 if wq["n_far"]:

@@ -7,7 +7,11 @@
   scale 20, 8 scenes (`make_batch(8, 20, seed=0)`, bench.py --preset c5's first batch) -- whose 896-wide
   features are the case the fused eval head exists for.
 
-Each runs the reference's eval call `model(x)` (train.py:106; models/MultiLabelContrastive.py:43-45, 64-70)
+A third test runs the C3 TRAINING step's backward on the same 8-scene batch (train.py:69-81: MultiLabel head,
+Classification loss on the scene labels) against the fp64 oracle with the device's ReLU decisions shared
+(oracle/parity.py), and requires every parameter gradient within 1e-3 of its tensor's max.
+
+Each of the first two runs the reference's eval call `model(x)` (train.py:106; models/MultiLabelContrastive.py:43-45, 64-70)
 on the device -- the per-point logits through the fused voxel-level head (heads.point_logits) -- with
 train-mode BatchNorm (the batch statistics of all 8 scenes, as the timed training step normalises), under
 no_grad, and an INDEPENDENT fp64 oracle forward of the same weights (oracle/scn_oracle.py, its own ReLU
@@ -21,12 +25,13 @@ unpinned" against SCN itself).
 """
 import pytest
 import torch
+import torch.nn.functional as F
 
 import sparseconvnet as scn  # noqa: F401
 from sparseconvnet import _lib
 from oracle import scn_oracle as O
 from oracle.encoders import OracleEncoder
-from oracle.parity import raster_perm
+from oracle.parity import raster_perm, run_shared_masks
 from wsss3d import EasyDict, MODEL_REGISTRY
 from wsss3d.synthetic import make_batch
 
@@ -163,3 +168,82 @@ def test_c5_batch_logits_parity_without_per_point_features():
     print(f"C5: per-point logits max err {err:.3e} (bar {LOGIT_BAR:g} absolute, max |logit| "
           f"{logits_o.abs().max().item():.3e})")
     assert err <= LOGIT_BAR, f"C5 per-point logits: {err:.3e} > {LOGIT_BAR}"
+
+
+@pytest.mark.timeout(1100)
+def test_headline_batch_backward_parity():
+    """C3's training step on the exact 8-scene batch bench.py times on rank 0 (1,908,804 points): forward in train
+    mode (batch-statistic BatchNorm over all 8 scenes, fused per-scene mean tail), the Classification loss of
+    train.py:75 on the scene labels, backward.  The fp64 oracle (memory-lean adjoints, oracle/scn_oracle.py LEAN)
+    runs with the device's ReLU decisions; every parameter gradient of the encoder and the Linear must be within
+    1e-3 of its tensor's max, and the ReLU decisions the oracle would take differently must lie at |z| < 1e-4."""
+    torch.manual_seed(0)
+    pc = EasyDict(name="SparseConvUNet", m=32, dimension=3, full_scale=4096, block_reps=2, residual_blocks=True)
+    model = MODEL_REGISTRY.get("MultiLabel")[0](pc).to(DEV)
+    b = make_batch(8, 50, seed=0)
+    xg, xo = _inputs(b)
+    ref, lin = _oracle_twin(model, "SparseConvUNet", 32, 2, True)
+    y = torch.from_numpy(b["scene_labels"]).double()
+    rec = _Kinds()
+    _lib.set_recorder(rec)
+    try:
+        # scene features (the encoder's training output, train.py:69 through MultiLabel) with shared ReLU decisions
+        logits_g, logits_o, st = run_shared_masks(model.pc_encoder, ref, xg, xo, istrain=True)
+        logits_g, logits_o = model.linear(logits_g), lin(logits_o)
+        err = (logits_g.detach().double().cpu() - logits_o.detach()).abs().max().item()
+        print(f"C3 training forward: scene logits max err {err:.3e}; ReLU decisions the oracle would flip: "
+              f"{st['flips']} (max |z| {st['max_flip_margin']:.2e})")
+        assert err <= LOGIT_BAR, err
+        assert st["max_flip_margin"] < 1e-4, st
+        F.multilabel_soft_margin_loss(logits_g, y.float().to(DEV)).backward()
+        F.multilabel_soft_margin_loss(logits_o, y).backward()
+    finally:
+        _lib.set_recorder(None)
+    gg = dict(model.named_parameters())
+    worst, n = 0.0, 0
+    for k, p in list(ref.named_parameters()) + list(lin.named_parameters()):
+        key = ("pc_encoder." + k) if ("pc_encoder." + k) in gg else ("linear." + k)
+        g_gpu = gg[key].grad
+        assert g_gpu is not None, key
+        scale = max(p.grad.abs().max().item(), 1e-12)
+        e = (g_gpu.double().cpu() - p.grad).abs().max().item()
+        worst = max(worst, e / scale)
+        n += 1
+        assert e <= 1e-3 * scale + 1e-9, f"grad {key}: {e:.3e} vs scale {scale:.3e}"
+    print(f"C3 backward: {n} parameter gradients, worst max err / tensor max {worst:.3e} (bar 1e-3)")
+    need = ["subm_bwd_data/x6r", "subm_bwd_data/x6s", "subm_bwd_data/x6g", "wgrad/x6c", "wgrad/x6", "nin_wgrad/x6",
+            "wgrad/f32n", "conv_bwd_data/f32", "deconv_bwd_data/x6d", "bn_bwd/hbm"]
+    missing = [k for k in need if k not in rec.kinds]
+    assert not missing, f"production forms that did not run: {missing} (ran: {sorted(rec.kinds)})"
+
+
+@pytest.mark.timeout(900)
+def test_fused_eval_head_matches_oracle_eval_mode():
+    """The fused eval head (heads.point_logits: the Linear on the level-0 voxel rows, msp_nin_gemm +
+    msp_point_rows_bias) against the fp64 ORACLE's lin(ref(x)) with eval-mode BatchNorm (running statistics
+    after one training forward), on two whole scenes: per-point logits within 1e-4 absolute
+    (models/MultiLabelContrastive.py:64-70, train.py:106)."""
+    torch.manual_seed(0)
+    pc = EasyDict(name="SparseConvUNet", m=32, dimension=3, full_scale=4096, block_reps=2, residual_blocks=True)
+    model = MODEL_REGISTRY.get("MultiLabel")[0](pc).to(DEV)
+    b = make_batch(2, 50, seed=3)
+    xg, xo = _inputs(b)
+    with torch.no_grad():  # one training forward moves the running statistics off their (0, 1) start
+        model((xg, None), istrain=True)
+    model.eval()
+    ref, lin = _oracle_twin(model, "SparseConvUNet", 32, 2, True)
+    ref.eval()
+    rec = _Kinds()
+    _lib.set_recorder(rec)
+    try:
+        with torch.no_grad():
+            logits = model(xg)
+    finally:
+        _lib.set_recorder(None)
+    with torch.no_grad():
+        logits_o = lin(ref(xo))
+    err = (logits.double().cpu() - logits_o).abs().max().item()
+    print(f"fused eval head, eval-mode BN, {logits_o.size(0)} points: logits max err {err:.3e} "
+          f"(max |logit| {logits_o.abs().max().item():.3e})")
+    assert err <= LOGIT_BAR, err
+    assert any(k.startswith("logits_fwd") for k in rec.kinds), sorted(rec.kinds)

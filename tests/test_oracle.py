@@ -142,3 +142,39 @@ def test_oracle_reproduces_golden(tag):
     assert np.allclose(pp.detach().numpy()[z["rows"]], z["per_point"], atol=1e-10)
     assert np.allclose(glob.detach().numpy(), z["scene"], atol=1e-10)
     assert np.allclose(ref.encoder[1].weight.grad.numpy(), z["grad_first"], atol=1e-10)
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_lean_adjoints_equal_autograd(train):
+    """The oracle's hand-written adjoints (LEAN: submanifold convolution and BatchNorm-(leaky)ReLU saving only their
+    inputs, oracle/scn_oracle.py) give the forward and every parameter / input gradient of autograd over the
+    plain op composition, on a residual UNet with leaky ReLUs (fp64, 1e-12 relative)."""
+    from wsss3d.synthetic import make_batch
+    b = make_batch(2, 8, seed=5, spacing=0.04)
+    coords = torch.from_numpy(b["coords"])
+    outs = {}
+    for lean in (False, True):
+        O.LEAN = lean
+        try:
+            torch.manual_seed(3)
+            ref = OracleEncoder("SparseConvUNet", m=8, block_reps=2, residual_blocks=True).double()
+            for mod in ref.modules():  # leaky ReLUs and non-trivial affines exercise every term
+                if isinstance(mod, O.BatchNormalization):
+                    mod.leak = 0.1
+                    with torch.no_grad():
+                        mod.weight.uniform_(0.5, 1.5)
+                        mod.bias.uniform_(-0.2, 0.2)
+            ref.train(train)
+            feats = torch.from_numpy(b["feats"]).double().requires_grad_(True)
+            x = dict(coords=coords, feature=feats, batch_offsets=b["batch_offsets"])
+            out = ref(x, istrain=True)
+            w = torch.linspace(-1, 1, out.numel(), dtype=torch.float64).view_as(out)
+            (out * w).sum().backward()
+            outs[lean] = (out.detach(), feats.grad, {k: p.grad for k, p in ref.named_parameters()})
+        finally:
+            O.LEAN = True
+    (o0, f0, g0), (o1, f1, g1) = outs[False], outs[True]
+    assert torch.allclose(o1, o0, rtol=0, atol=1e-12 * o0.abs().max().item())
+    assert torch.allclose(f1, f0, rtol=0, atol=1e-12 * f0.abs().max().item())
+    for k in g0:
+        assert torch.allclose(g1[k], g0[k], rtol=0, atol=1e-12 * max(g0[k].abs().max().item(), 1e-30)), k
