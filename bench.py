@@ -349,6 +349,14 @@ def main():
         sock.close()
         be = "gloo" if os.environ["BENCH_DP_SELFTEST"] == "gloo" else "nccl"
         dist.init_process_group(be, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    # N ranks on one host: each rank's torch intra-op pool bounded to its share of the CPUs the job may use (the
+    # default sizes it by every core the machine reports, so N ranks oversubscribe a cgroup quota N x cores-fold;
+    # BENCH_THREADS overrides)
+    host_threads = None
+    if world > 1:
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        host_threads = int(os.environ.get("BENCH_THREADS", max(1, host_cores()[0] // max(local, 1))))
+        torch.set_num_threads(host_threads)
     if rank == 0 and world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
               file=sys.stderr)
@@ -582,6 +590,7 @@ def main():
     bounds = [torch.cuda.Event(enable_timing=True)]
     bounds[0].record(cur)
     t0 = time.perf_counter()
+    loop_t = []  # graph loop host seconds per step: (replay call incl. an eager exchange, prefetch, capture)
     if use_graph:
         inflight, dones = [], []
         for i in range(args.steps):
@@ -612,6 +621,7 @@ def main():
             inflight[-1] = (inflight[-1][0][0], None, i)
             h3 = time.perf_counter()
             entry = capture(i + 1) if i + 1 < args.steps else None
+            loop_t.append((h1 - h0, h2 - h1, time.perf_counter() - h3))
             if host_t is not None:
                 host_t.append((h1 - h0, h2 - h1, h3 - h2, time.perf_counter() - h3))
         if host_t:
@@ -661,6 +671,9 @@ def main():
     dt_max, vox_all = dp.max_over_ranks(dt), dp.sum_over_ranks(float(vox))
     med_step = dp.max_over_ranks(statistics.median(step_ms))
     rank_vox = dp.gather_floats(float(vox) / args.steps)  # level-0 voxels per step of every rank
+    # every rank's graph-loop host time per step (medians): where an N-rank step's wall time goes on the host
+    loop_med = [1e3 * statistics.median(c) for c in zip(*loop_t)] if loop_t else [0.0, 0.0, 0.0]
+    rank_host = [dp.gather_floats(v) for v in loop_med] if world > 1 else [[v] for v in loop_med]
     _lib.set_recorder(None)
     fams = rec.summary()
     fam_steps = args.family_steps if (args.record != "all" or use_graph) else 0
@@ -744,6 +757,10 @@ def main():
                      "dp.GradSync: one all-reduce over a flat gradient buffer after each graph replay, then Adam")
                     if graph_dp else "DDP, 64 MB buckets overlapped with backward"),
                 "comm_backend": dist.get_backend() if dist.is_initialized() else None,
+                "host_threads_per_rank": host_threads if host_threads is not None else torch.get_num_threads(),
+                "rank_host_ms_per_step": {"replay_call_incl_eager_exchange": rank_host[0],
+                                          "prefetch": rank_host[1], "capture": rank_host[2],
+                                          "note": "graph loop, median per rank (rank order)"} if loop_t else None,
                 "input_pipeline": "none" if args.no_prefetch else
                 "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step "
                 f"(after its {'optimizer' if args.prefetch_at == 'end' else 'forward'} call is queued; host "
