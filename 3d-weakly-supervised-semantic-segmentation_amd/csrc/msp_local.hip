@@ -31,6 +31,8 @@
 // msp_conv_x6.hip, six piece products summed in a zeroed accumulator and added
 // once).  The four waves' partial sums are added in wave order through LDS at
 // the end (deterministic).  Input channels are staged 32 at a time.
+#include <type_traits>
+
 #include "msp_x6.h"
 
 namespace msp {
@@ -358,7 +360,10 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 // AC (accumulation): 1 = the six piece products of a step go straight into the group's running sums, smallest
 // first (the product form); 0 = summed in a zeroed accumulator and added with a vector add (round 2-3 form:
 // about a third of the rounding error, 6-9 % slower -- profiles/r03/kbexp_r03x_accumulate.log).
-template <int NT, int AB = 0, int AC = 1>
+// WB (weight fragment register sets): 1 = one set, the next step's fragments loaded after the step's MFMAs (their
+// latency exposed at the next step's start); 2 = two sets alternating, the next step's fragments loaded before the
+// step's MFMAs, so a whole step hides their latency (the first step of each slice loads after the staging).
+template <int NT, int AB = 0, int AC = 1, int WB = 1>
 __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
@@ -435,6 +440,16 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const int ks = sc / n_j, j = sc - ks * n_j;
     const int o = off_of(j);
     const int ow = flip ? K - 1 - o : o;
+    if constexpr (WB == 2) {  // wave-uniform row base (scalar registers) + the lane's 32-bit byte offset
+      const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * 3 * 64;
+      const char* b = reinterpret_cast<const char*>(src);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          w[t][p] = *reinterpret_cast<const u32x4*>(b + (uint32_t)(((t * 3 + p) * 64 + lane) * 16));
+      return;
+    }
     const u32x4* src = wimg + ((((int64_t)ow * n_y + cy) * nks + ks) * NT) * 3 * 64 + lane;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -455,6 +470,9 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     floatx4 v[MI][2];
 #pragma unroll
     for (int b = 0; b < MI; ++b) {
+      // WB 2: the row addresses are formed here, per slice (hoisted out of the slice loop they hold 6 registers
+      // for the whole kernel, which the second weight set needs)
+      if constexpr (WB == 2) asm volatile("" : "+v"(srow[b]));
       const int i = tid + NTH * b;
       const int k = k0 + 8 * (i & 3);
       v[b][0] = v[b][1] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -479,8 +497,8 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       }
     }
   };
-  // one (k-slice, offset) step of this wave over its row groups
-  auto run = [&](int ks, int o, const u32x4 (&w)[NT][3]) {
+  // one (k-slice, offset) step of this wave over its row groups; FAR: the tile lists rows past the staged capacity
+  auto run = [&](int ks, int o, const u32x4 (&w)[NT][3], auto FAR) {
     const uint16_t* lo = ls + o * T + 16 * rp + r;
     int li[G];
 #pragma unroll
@@ -490,7 +508,7 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     for (int g = 0; g < G; ++g) {
       const bool pres = li[g] != kAbsent;
       act |= (ballot64(pres) != 0 ? 1u : 0u) << g;
-      far |= (ballot64(pres && li[g] >= kUCap) != 0 ? 1u : 0u) << g;
+      if constexpr (decltype(FAR)::value) far |= (ballot64(pres && li[g] >= kUCap) != 0 ? 1u : 0u) << g;
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -500,7 +518,7 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
         if constexpr ((AB & 8) != 0) jr = li[g] < kUCap ? 16 * g + r : kUCap;  // ablation: conflict-free reads
 #pragma unroll
         for (int p = 0; p < 3; ++p) cur[p] = xs[xs_unit(jr, p, q)];
-        if ((far >> g) & 1) {  // rows past the staged capacity: straight from global memory (rare)
+        if (decltype(FAR)::value && ((far >> g) & 1)) {  // rows past the staged capacity: from global memory (rare)
           const bool f = li[g] != kAbsent && li[g] >= kUCap;
           const int k = 32 * ks + 8 * q;
           floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
@@ -548,15 +566,43 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     }
   };
 
-  u32x4 wf[NT][3];
-  if (n_j) ld_w(0, wf);
-  for (int ks = 0; ks < nks; ++ks) {
-    if (ks) __syncthreads();  // previous slice's readers done
-    stage(ks);
-    __syncthreads();
-    for (int j = 0; j < n_j; ++j) {
-      run(ks, off_of(j), wf);
-      if constexpr (!(AB & 4)) ld_w(ks * n_j + j + 1, wf);
+  using Far = std::true_type;
+  using Near = std::false_type;
+  if (WB == 2 && U <= kUCap) {  // block-uniform: every listed row is staged (all but 0-0.09 % of tiles)
+    // Two fragment sets: step j of a slice runs on set j & 1 while the next step's fragments load into the other.
+    // The step loop has a fixed trip count of 8 (the longest offset list) and is unrolled, with every load
+    // unconditional (steps past the list reload a valid step; the last one of a slice loads the next slice's
+    // first), so the compiler's in-order load count waits only for the older set at each step's first MFMA --
+    // data-dependent branches around the loads would leave a vmcnt(0) there instead.
+    u32x4 wa[NT][3], wb[NT][3];
+    auto ld_next = [&](int ks, int j, u32x4 (&w)[NT][3]) {  // fragments of the step after (ks, j)
+      const int s1 = j + 1 < n_j ? ks * n_j + j + 1 : (ks + 1 < nks ? (ks + 1) * n_j : ks * n_j + n_j - 1);
+      ld_w(s1, w);
+    };
+    if (n_j) ld_w(0, wa);
+    for (int ks = 0; ks < nks; ++ks) {
+      if (ks) __syncthreads();  // previous slice's readers done
+      stage(ks);
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        ld_next(ks, j, wb);
+        if (j < n_j) run(ks, off_of(j), wa, Near{});
+        ld_next(ks, j + 1, wa);
+        if (j + 1 < n_j) run(ks, off_of(j + 1), wb, Near{});
+      }
+    }
+  } else {
+    u32x4 wf[NT][3];
+    if (n_j) ld_w(0, wf);
+    for (int ks = 0; ks < nks; ++ks) {
+      if (ks) __syncthreads();  // previous slice's readers done
+      stage(ks);
+      __syncthreads();
+      for (int j = 0; j < n_j; ++j) {
+        run(ks, off_of(j), wf, Far{});
+        if constexpr (!(AB & 4)) ld_w(ks * n_j + j + 1, wf);
+      }
     }
   }
   // the four waves' partial sums of each half, added in wave order
@@ -1273,7 +1319,8 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
 #ifdef MSP_EXPERIMENTS
 // Kernel-variant entry for scripts/kbench.py (built only into lib/libmi3dsparse_exp.so by
 // scripts/build_exp.sh; the product library has no such symbol): msp_conv_local with the conv_x6s
-// template form selected by `variant` = 100 AB + 10 AC + RR (RR = 1: offsets dealt round-robin, wave_off ignored).
+// template form selected by `variant` = 1000 (WB - 1) + 100 AB + 10 AC + RR (RR = 1: offsets dealt round-robin,
+// wave_off ignored).
 int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
                        int tile_rows, const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows,
                        const int32_t* perm, const uint8_t* wave_off, int64_t n_rows, float* out, void* ws,
@@ -1291,13 +1338,15 @@ int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, i
   const unsigned grid = (unsigned)(n_tiles * n_y);
   const int64_t n_pad = n_tiles * tile_rows;
   const uint8_t* wo = variant % 10 == 1 ? nullptr : wave_off;
-#define EV(A, C)                                                                                               \
-  if (variant / 100 == A && (variant / 10) % 10 == C) {                                                        \
-    conv_x6s_kernel<2, A, C><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows,     \
-                                                  perm, wo, n_pad, n_y, out);                                  \
+  const int wbv = variant / 1000 + 1;
+  variant %= 1000;
+#define EV(A, C, W)                                                                                            \
+  if (wbv == W && variant / 100 == A && (variant / 10) % 10 == C) {                                            \
+    conv_x6s_kernel<2, A, C, W><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows,  \
+                                                     perm, wo, n_pad, n_y, out);                               \
     return check_launch("msp_exp_conv_local");                                                                 \
   }
-  EV(0, 0) EV(0, 1) EV(1, 0) EV(1, 1) EV(4, 0) EV(5, 0) EV(8, 1)
+  EV(0, 0, 1) EV(0, 1, 1) EV(1, 0, 1) EV(1, 1, 1) EV(4, 0, 1) EV(5, 0, 1) EV(8, 1, 1) EV(0, 1, 2)
 #undef EV
 
   set_error("msp_exp_conv_local: no variant %d", variant);
