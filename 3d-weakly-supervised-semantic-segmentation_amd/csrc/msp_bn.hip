@@ -45,90 +45,6 @@ struct BnStats {
   __device__ float z(float x, int c) const { return centred(x, c) * sc[c] + sh[c]; }
 };
 
-// The per-channel sums of the P partial blocks, in ONE fixed order shared by the standalone finalize kernels and
-// the statistics kernels that finalize in their last block: for slot s (of 2C), lane j < 8 of an 8-lane group adds
-// partial[p][s] for p = j, j + 8, ... in p order, and the eight sums meet as ((a0+a1)+(a2+a3))+((a4+a5)+(a6+a7))
-// through xor shuffles (every lane ends with the same bits: each level adds the same two values).
-__device__ __forceinline__ double slot_sum8(const double* __restrict__ partial, int64_t P, int C2, int s, int j) {
-  double a = 0.0;
-  for (int64_t p = j; p < P; p += 8) a += partial[p * C2 + s];
-#pragma unroll
-  for (int m = 1; m < 8; m <<= 1) a += __shfl_xor(a, m, 8);
-  return a;
-}
-
-// train-mode statistics of channel c from its two sums (one thread): running statistics and stats[5][C]
-__device__ __forceinline__ void finalize_channel(int c, int C, int64_t V, double s0, double s1, double eps,
-                                                 double momentum, int train, float* __restrict__ rmean,
-                                                 float* __restrict__ rvar, const float* __restrict__ weight,
-                                                 const float* __restrict__ bias, float* __restrict__ stats) {
-  double mu, var;
-  if (train) {
-    mu = V > 0 ? s0 / (double)V : 0.0;
-    var = V > 0 ? s1 / (double)V - mu * mu : 0.0;
-    if (var < 0.0) var = 0.0;
-    const double unb = V > 1 ? var * (double)V / (double)(V - 1) : var;
-    rmean[c] = (float)(momentum * rmean[c] + (1.0 - momentum) * mu);
-    rvar[c] = (float)(momentum * rvar[c] + (1.0 - momentum) * unb);
-  } else {
-    mu = rmean[c];
-    var = rvar[c];
-  }
-  const double is = 1.0 / sqrt(var + eps);
-  const double w = weight ? weight[c] : 1.0, b = bias ? bias[c] : 0.0;
-  const float hi = (float)mu;
-  stats[c] = hi;
-  stats[C + c] = (float)(mu - (double)hi);
-  stats[2 * C + c] = (float)is;
-  stats[3 * C + c] = (float)(w * is);
-  stats[4 * C + c] = (float)b;
-}
-
-// What a statistics kernel's last block does with the sums (FIN != 0): 1 = the forward finalize (stats, running
-// statistics), 2 = the backward's (sums to the partial buffer's tail for the apply, dweight / dbias).
-struct BnFin {
-  unsigned* counter;  // caller-owned, 0 between launches (atomicInc wraps it back to 0 at the last block)
-  double eps, momentum;
-  float *rmean, *rvar;
-  const float *weight, *bias;
-  float* stats;
-  float *dweight, *dbias;
-};
-
-// The last block of the grid to finish (agent-scope release by every thread, one atomic, acquire) sums every
-// block's partials in the shared order and finalizes: no further launch, no other block waits.
-template <int FIN>
-__device__ __forceinline__ void bn_last_block(double* __restrict__ partial, int64_t P, int C, int64_t V,
-                                              const BnFin& fin, double* __restrict__ lds_tot) {
-  __shared__ int s_last;
-  __threadfence();  // this thread's partial stores complete and visible device-wide
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicInc(fin.counter, (unsigned)(P - 1)) == (unsigned)(P - 1);
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // acquire: every block's partials
-  const int C2 = 2 * C, g = threadIdx.x >> 3, j = threadIdx.x & 7;
-  for (int s0 = 0; s0 < C2; s0 += kT / 8) {
-    const int sl = s0 + g;
-    const double t = sl < C2 ? slot_sum8(partial, P, C2, sl < C2 ? sl : 0, j) : 0.0;
-    if (sl < C2 && j == 0) lds_tot[sl] = t;
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += kT) {
-    const double a = lds_tot[c], b = lds_tot[C + c];
-    if (FIN == 1) {
-      finalize_channel(c, C, V, a, b, fin.eps, fin.momentum, 1, fin.rmean, fin.rvar, fin.weight, fin.bias,
-                       fin.stats);
-    } else {
-      double* sums = partial + P * C2;
-      sums[c] = a;
-      sums[C + c] = b;
-      if (fin.dbias) fin.dbias[c] = (float)a;
-      if (fin.dweight) fin.dweight[c] = (float)b;
-    }
-  }
-}
-
 // MODE 0: (sum x, sum x^2).  MODE 1: (sum dz, sum dz*xhat).
 // Vector form (C % 4 == 0, C <= 1024): each thread owns 4 channels (one
 // float4 column) and strides over rows with 4 independent loads in flight;
@@ -139,13 +55,11 @@ __device__ __forceinline__ void bn_last_block(double* __restrict__ partial, int6
 // MODE 3: channel join (SCN JoinTable) fused with the statistics of its
 // output: x = a [V][ca], dy = b [V][C - ca], the row [a | b] is written to
 // sum_out [V][C] and reduced as in MODE 0 (identical partials again).
-// FIN (MODE 0: 1, MODE 1: 2): the last block finalizes (bn_last_block).
-template <int MODE, int FIN = 0>
+template <int MODE>
 __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                         int64_t V, int C, const float* __restrict__ stats,
                                                         float leak, double* __restrict__ partial,
-                                                        float* __restrict__ sum_out = nullptr, int ca = 0,
-                                                        BnFin fin = BnFin{}) {
+                                                        float* __restrict__ sum_out = nullptr, int ca = 0) {
   __shared__ double red[kT][8];
   const int64_t P = gridDim.x;
   const int64_t per = (V + P - 1) / P;
@@ -269,10 +183,6 @@ __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict_
       out0[C + 4 * t + j] = b[j];
     }
   }
-  if constexpr (FIN != 0) {
-    __syncthreads();  // red is reused for the totals
-    bn_last_block<FIN>(partial, P, C, V, fin, &red[0][0]);
-  }
 }
 
 // MODE 0: (sum x, sum x^2).  MODE 1: (sum dz, sum dz*xhat).
@@ -328,20 +238,59 @@ __global__ __launch_bounds__(kT) void bn_reduce_kernel(const float* __restrict__
   }
 }
 
-// 16 channels per 256-thread block: 8 lanes per slot, slots c and C + c of channel c (the shared order)
+// Sum of partial[p][slot][c] over p for one channel per block, fixed order
+// (strided per thread, then a tree over the block): deterministic.
+__device__ inline void sum_partials(const double* __restrict__ partial, int64_t P, int C, int c, double* out2) {
+  __shared__ double red[2][kT];
+  double a = 0.0, b = 0.0;
+  for (int64_t p = threadIdx.x; p < P; p += kT) {
+    a += partial[p * 2 * C + c];
+    b += partial[p * 2 * C + C + c];
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int w = kT / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  out2[0] = red[0][0];
+  out2[1] = red[1][0];
+}
+
+// one block per channel
 __global__ __launch_bounds__(kT) void bn_finalize_kernel(const double* __restrict__ partial, int64_t P, int C,
                                                          int64_t V, double eps, double momentum, int train,
                                                          float* __restrict__ rmean, float* __restrict__ rvar,
                                                          const float* __restrict__ weight,
                                                          const float* __restrict__ bias, float* __restrict__ stats) {
-  const int g = threadIdx.x >> 3, j = threadIdx.x & 7;
-  const int c = (int)blockIdx.x * (kT / 16) + (g >> 1), half = g & 1;
-  const int cc = c < C ? c : C - 1;
-  double sum = 0.0;
-  if (train) sum = slot_sum8(partial, P, 2 * C, half * C + cc, j);
-  const double other = __shfl_xor(sum, 8);  // the channel's other slot (the neighbouring 8-lane group)
-  if (c >= C || j != 0 || half) return;
-  finalize_channel(c, C, V, sum, other, eps, momentum, train, rmean, rvar, weight, bias, stats);
+  const int c = blockIdx.x;
+  double sums[2] = {0.0, 0.0};
+  if (train) sum_partials(partial, P, C, c, sums);
+  if (threadIdx.x != 0) return;
+  double mu, var;
+  if (train) {
+    mu = V > 0 ? sums[0] / (double)V : 0.0;
+    var = V > 0 ? sums[1] / (double)V - mu * mu : 0.0;
+    if (var < 0.0) var = 0.0;
+    const double unb = V > 1 ? var * (double)V / (double)(V - 1) : var;
+    rmean[c] = (float)(momentum * rmean[c] + (1.0 - momentum) * mu);
+    rvar[c] = (float)(momentum * rvar[c] + (1.0 - momentum) * unb);
+  } else {
+    mu = rmean[c];
+    var = rvar[c];
+  }
+  const double is = 1.0 / sqrt(var + eps);
+  const double w = weight ? weight[c] : 1.0, b = bias ? bias[c] : 0.0;
+  const float hi = (float)mu;
+  stats[c] = hi;
+  stats[C + c] = (float)(mu - (double)hi);
+  stats[2 * C + c] = (float)is;
+  stats[3 * C + c] = (float)(w * is);
+  stats[4 * C + c] = (float)b;
 }
 
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const float* __restrict__ x, int64_t n, int C,
@@ -387,20 +336,18 @@ __global__ __launch_bounds__(kT) void bn_apply4_kernel(const float* __restrict__
   }
 }
 
-// 16 channels per block, as bn_finalize_kernel
+// one block per channel
 __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const double* __restrict__ partial, int64_t P, int C,
                                                              float* __restrict__ dweight,
                                                              float* __restrict__ dbias, double* __restrict__ sums) {
-  const int g = threadIdx.x >> 3, j = threadIdx.x & 7;
-  const int c = (int)blockIdx.x * (kT / 16) + (g >> 1), half = g & 1;
-  const int cc = c < C ? c : C - 1;
-  const double sum = slot_sum8(partial, P, 2 * C, half * C + cc, j);
-  const double other = __shfl_xor(sum, 8);
-  if (c >= C || j != 0 || half) return;
-  sums[c] = sum;        // sum dz
-  sums[C + c] = other;  // sum dz * xhat
-  if (dbias) dbias[c] = (float)sum;
-  if (dweight) dweight[c] = (float)other;
+  const int c = blockIdx.x;
+  double s2[2];
+  sum_partials(partial, P, C, c, s2);
+  if (threadIdx.x != 0) return;
+  sums[c] = s2[0];      // sum dz
+  sums[C + c] = s2[1];  // sum dz * xhat
+  if (dbias) dbias[c] = (float)s2[0];
+  if (dweight) dweight[c] = (float)s2[1];
 }
 
 __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restrict__ x,
@@ -566,7 +513,7 @@ int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double 
                     float* running_mean, float* running_var, const float* weight, const float* bias, float* stats,
                     msp_stream_t stream) {
   MSP_REQUIRE(C > 0, "msp_bn_finalize: bad C");
-  bn_finalize_kernel<<<(unsigned)ceil_div(C, kT / 16), kT, 0, as_stream(stream)>>>(
+  bn_finalize_kernel<<<(unsigned)C, kT, 0, as_stream(stream)>>>(
       partial, bn_parts(V, C), C, V, eps, momentum, train, running_mean, running_var, weight, bias, stats);
   return check_launch("msp_bn_finalize");
 }
@@ -591,18 +538,15 @@ int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const fl
   return check_launch("msp_bn_bwd_stats");
 }
 
-namespace {
-// fin_done: the sums are already in the partial buffer's tail (msp_bn_bwd_stats_finalize), else summed here first
-int bwd_apply_impl(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,
-                   const float* weight, float leak, int train, const float* addend, float* dx, float* dweight,
-                   float* dbias, int fin_done, hipStream_t s) {
+int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, const double* partial,
+                         const float* stats, const float* weight, float leak, int train, const float* addend,
+                         float* dx, float* dweight, float* dbias, msp_stream_t stream) {
   MSP_REQUIRE(addend == nullptr || addend != dx || V * C == 0, "msp_bn_bwd_apply_add: addend must not alias dx");
+  hipStream_t s = as_stream(stream);
   // The combined per-channel sums go to the extra 2*C doubles at the tail of
   // the partial buffer (it holds (P + 1) * 2 * C doubles, see the header).
   double* sums = const_cast<double*>(partial) + bn_parts(V, C) * 2 * C;
-  if (fin_done == 0)
-    bn_bwd_finalize_kernel<<<(unsigned)ceil_div(C, kT / 16), kT, 0, s>>>(partial, bn_parts(V, C), C, dweight, dbias,
-                                                                          sums);
+  bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V, C), C, dweight, dbias, sums);
   const int64_t n = V * C;
   if (n > 0) {
     if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx) &&
@@ -613,55 +557,6 @@ int bwd_apply_impl(const float* x, const float* dy, int64_t V, int C, const doub
       bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, addend, dx);
   }
   return check_launch("msp_bn_bwd_apply");
-}
-inline bool bn_vec_ok(int C, const void* a, const void* b = nullptr) {
-  return C % 4 == 0 && C <= 4 * kT && aligned16(a) && (b == nullptr || aligned16(b));
-}
-}  // namespace
-
-int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, const double* partial,
-                         const float* stats, const float* weight, float leak, int train, const float* addend,
-                         float* dx, float* dweight, float* dbias, msp_stream_t stream) {
-  return bwd_apply_impl(x, dy, V, C, partial, stats, weight, leak, train, addend, dx, dweight, dbias, 0,
-                        as_stream(stream));
-}
-
-int msp_bn_bwd_apply_sums(const float* x, const float* dy, int64_t V, int C, const double* partial,
-                          const float* stats, const float* weight, float leak, int train, const float* addend,
-                          float* dx, msp_stream_t stream) {
-  return bwd_apply_impl(x, dy, V, C, partial, stats, weight, leak, train, addend, dx, nullptr, nullptr, 1,
-                        as_stream(stream));
-}
-
-int msp_bn_stats_finalize(const float* x, int64_t V, int C, double* partial, unsigned* counter, double eps,
-                          double momentum, float* running_mean, float* running_var, const float* weight,
-                          const float* bias, float* stats, msp_stream_t stream) {
-  MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_stats_finalize: bad shape");
-  if (!(bn_vec_ok(C, x) && counter)) {  // the two-launch form
-    const int rc = msp_bn_stats(x, V, C, partial, stream);
-    if (rc) return rc;
-    return msp_bn_finalize(partial, V, C, eps, momentum, 1, running_mean, running_var, weight, bias, stats, stream);
-  }
-  BnFin fin{counter, eps, momentum, running_mean, running_var, weight, bias, stats, nullptr, nullptr};
-  bn_reduce4_kernel<0, 1><<<(unsigned)bn_parts(V, C), kT, 0, as_stream(stream)>>>(x, nullptr, V, C, nullptr, 0.f,
-                                                                                 partial, nullptr, 0, fin);
-  return check_launch("msp_bn_stats_finalize");
-}
-
-int msp_bn_bwd_stats_finalize(const float* x, const float* dy, int64_t V, int C, const float* stats, float leak,
-                              double* partial, unsigned* counter, float* dweight, float* dbias, msp_stream_t stream) {
-  MSP_REQUIRE(C > 0 && C <= 4096 && V >= 0, "msp_bn_bwd_stats_finalize: bad shape");
-  if (!(bn_vec_ok(C, x, dy) && counter)) {  // the two-launch form
-    const int rc = msp_bn_bwd_stats(x, dy, V, C, stats, leak, partial, stream);
-    if (rc) return rc;
-    bn_bwd_finalize_kernel<<<(unsigned)ceil_div(C, kT / 16), kT, 0, as_stream(stream)>>>(
-        partial, bn_parts(V, C), C, dweight, dbias, partial + bn_parts(V, C) * 2 * C);
-    return check_launch("msp_bn_bwd_stats_finalize");
-  }
-  BnFin fin{counter, 0.0, 0.0, nullptr, nullptr, nullptr, nullptr, nullptr, dweight, dbias};
-  bn_reduce4_kernel<1, 2><<<(unsigned)bn_parts(V, C), kT, 0, as_stream(stream)>>>(x, dy, V, C, stats, leak, partial,
-                                                                                 nullptr, 0, fin);
-  return check_launch("msp_bn_bwd_stats_finalize");
 }
 
 int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,

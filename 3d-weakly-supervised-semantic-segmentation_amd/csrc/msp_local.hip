@@ -312,18 +312,26 @@ __global__ __launch_bounds__(256) void split_weights_lane_kernel(const float* __
   split_weights_lane_unit(wt, K, c_out, c_in, NT, img, wlay, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
-// Every image of a step in one launch (msp_split_weight_images): thread g finds its image by a binary search in
-// the units' prefix sums and runs that image's unit.
+// Every image of a step in one launch (msp_split_weight_images): the block's first unit finds its image by one
+// binary search in the units' prefix sums (thread 0; a per-thread search was seven dependent global loads per
+// unit), and each thread steps forward from there to its own image (a block spans one or two images).
 __global__ __launch_bounds__(256) void split_images_kernel(const msp_weight_image* __restrict__ d, int n,
                                                            const int64_t* __restrict__ start, int64_t total) {
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= total) return;
-  int lo = 0, hi = n;  // start[lo] <= g < start[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (start[mid] <= g) lo = mid;
-    else hi = mid;
+  __shared__ int s_lo;
+  const int64_t g0 = (int64_t)blockIdx.x * 256, g = g0 + threadIdx.x;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = n;  // start[lo] <= g0 < start[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (start[mid] <= g0) lo = mid;
+      else hi = mid;
+    }
+    s_lo = lo;
   }
+  __syncthreads();
+  if (g >= total) return;
+  int lo = s_lo;
+  while (lo + 1 < n && start[lo + 1] <= g) ++lo;
   const msp_weight_image e = d[lo];
   const int64_t u = g - start[lo];
   u32x4* img = static_cast<u32x4*>(e.img);

@@ -81,9 +81,6 @@ PROTOTYPES = {
     "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),
-    "msp_bn_stats_finalize": (I, [P, I64, I, P, P, D, D, P, P, P, P, P, P]),
-    "msp_bn_bwd_stats_finalize": (I, [P, P, I64, I, P, F, P, P, P, P, P]),
-    "msp_bn_bwd_apply_sums": (I, [P, P, I64, I, P, P, P, F, I, P, P, P]),
     "msp_join_cols": (I, [P, I, P, I, I64, P, P, P]),
     "msp_split_cols": (I, [P, I64, I, I, P, P, P]),
     "msp_nin_gemm_ok": (I, [I64, I, I]),

@@ -533,22 +533,6 @@ def _bn_partial_buf(V, C, device):
     return torch.empty((P + 1) * 2 * C, dtype=torch.float64, device=device)
 
 
-# One-launch statistics + finalize (msp_bn_stats_finalize / msp_bn_bwd_stats_finalize: the grid's last block
-# finalizes); False = the two-launch forms (bit-identical, tests/test_gpu_ops.py).
-FUSE_FINALIZE = os.environ.get("MSP_FUSE_FINALIZE", "1") != "0"
-_COUNTERS = {}  # (device index, stream) -> uint32 counters of the one-launch forms (zero between launches)
-
-
-def _counter(device, which):
-    """The counter of the one-launch statistics kernels for the current stream (fwd 0, bwd 1): launches on one
-    stream run one after another and each leaves it zero, so concurrent streams each need their own."""
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    t = _COUNTERS.get(key)
-    if t is None:
-        t = _COUNTERS[key] = torch.zeros(2, dtype=torch.int32, device=device)
-    return t[which:]
-
-
 def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial):
     """y, stats of BN + (leaky) ReLU; `partial` = the msp_bn_stats partials of
     x when a residual join already produced them (msp_add_bn_stats), else None."""
@@ -556,20 +540,14 @@ def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, tra
     s = _stream(x)
     stats = torch.empty((5, C), dtype=torch.float32, device=x.device)
     y = torch.empty_like(x)
-    cnt = _counter(x.device, 0) if (FUSE_FINALIZE and partial is None and train) else None
 
     def run(partial=partial):
-        if cnt is not None:
+        if partial is None:
             partial = _bn_partial_buf(V, C, x.device)
-            call("msp_bn_stats_finalize", ptr(x), V, C, ptr(partial), ptr(cnt), float(eps), float(momentum),
-                 ptr(running_mean), ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
-        else:
-            if partial is None:
-                partial = _bn_partial_buf(V, C, x.device)
-                if train:
-                    call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
-            call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
-                 ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
+            if train:
+                call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
+        call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
+             ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
         call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
     # compulsory bytes: statistics pass (read x) unless a join produced them, apply (read x, write y)
     _record(_shape("bn_fwd/hbm", C, C, V), 0, run, 4 * V * C * (3 if (partial is None and train) else 2))
@@ -588,12 +566,6 @@ def _bn_bwd(x, weight, stats, cfg, gy, addend):
     db = torch.empty(C, dtype=torch.float32, device=x.device)
 
     def run():
-        if FUSE_FINALIZE:
-            call("msp_bn_bwd_stats_finalize", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial),
-                 ptr(_counter(x.device, 1)), ptr(dw), ptr(db), s)
-            call("msp_bn_bwd_apply_sums", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats),
-                 ptr(weight) if has_w else None, leak, train, ptr(addend) if addend is not None else None, ptr(dx), s)
-            return
         call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
         call("msp_bn_bwd_apply_add", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats),
              ptr(weight) if has_w else None, leak, train, ptr(addend) if addend is not None else None, ptr(dx),

@@ -300,10 +300,6 @@ def main():
     ap.add_argument("--prefetch-lag", type=int, choices=[1, 2], default=1,
                     help="graph mode: the metadata build of batch i + 1 waits for step i - lag's graph (1: the host "
                          "runs at most one step ahead; 2: two)")
-    ap.add_argument("--prefetch-gate", choices=["prev", "fwd"], default="prev",
-                    help="graph mode: what the metadata build of batch i + 1 waits for on the device -- prev: step "
-                         "i - lag's graph (the build overlaps the start of step i); fwd: an external event the graph "
-                         "of step i records after its forward (the build overlaps step i's backward)")
     ap.add_argument("--prefetch-thread", type=int, choices=[0, 1], default=0,
                     help="graph mode, 1: the metadata of the batch after next is built on a worker thread while the "
                          "next step is captured (two prefetched batches pending; the build waits for the step two "
@@ -498,18 +494,12 @@ def main():
     capture_s = []
     capture_parts = []  # BENCH_HOST_TIMING: (capture_begin, body, capture_end) host seconds
 
-    gate_ev = {}  # --prefetch-gate fwd: step -> the external event its graph records after the forward
-
     def body(i):  # one training step without its prefetch (what a graph captures; N ranks: up to backward)
         x, y, _, text = batches[i % len(batches)]
         if wimg is not None:
             wimg.prepare()
         opt.zero_grad(set_to_none=gsync is None)
         logits, meta = model((x, text), istrain=True)
-        if args.prefetch_gate == "fwd":
-            ev = torch.cuda.Event(external=True)  # an event-record node of the graph, waitable outside it
-            ev.record()
-            gate_ev[i] = ev
         loss = cls_loss(logits, y)
         if contrastive:
             loss = loss + con_loss(*meta)
@@ -612,10 +602,7 @@ def main():
             if worker is None:
                 # batch i + 1 on the side stream, after step i - lag's graph on the device: the build's count reads
                 # pace the host (lag 1: at most one step ahead -- step i is queued while step i + 1 is captured)
-                if args.prefetch_gate == "fwd":
-                    prefetch(i, gate_ev[i])
-                else:
-                    prefetch(i, dones[-args.prefetch_lag] if len(dones) >= args.prefetch_lag else None)
+                prefetch(i, dones[-args.prefetch_lag] if len(dones) >= args.prefetch_lag else None)
                 dones.append(done)
             else:
                 # batch i + 1 was built on the worker during the last capture; batch i + 2 goes there now, after
@@ -777,9 +764,7 @@ def main():
                 "input_pipeline": "none" if args.no_prefetch else
                 "next batch's metadata (voxelisation + rulebooks) built on a side stream during each step "
                 f"(after its {'optimizer' if args.prefetch_at == 'end' else 'forward'} call is queued; host "
-                f"time {1e3 * statistics.median(prefetch_s) if prefetch_s else 0:.1f} ms median"
-                + ("; on the device each build waits for the step before it to end)" if args.prefetch_gate == "prev"
-                   else "; on the device each build waits for the running step's forward to end)"),
+                f"time {1e3 * statistics.median(prefetch_s) if prefetch_s else 0:.1f} ms median)",
                 "launch": (f"every step captured afresh into a HIP graph after its metadata is prefetched and replayed "
                            f"on the compute stream (capture host time {1e3 * statistics.median(capture_s):.1f} ms "
                            "median, overlapped with the previous step's replay)") if use_graph and capture_s else

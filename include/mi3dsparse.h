@@ -345,23 +345,6 @@ int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, cons
                          float* dx, float* dweight, float* dbias, msp_stream_t stream);
 int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,
                      msp_stream_t stream);
-/* One-launch statistics + finalize (ABI 9).  msp_bn_stats_finalize = msp_bn_stats then msp_bn_finalize(train = 1),
- * msp_bn_bwd_stats_finalize = msp_bn_bwd_stats then the backward's channel sums (written to the partial buffer's
- * tail, dweight = sum dz*xhat, dbias = sum dz; either may be NULL), each in ONE launch: the last block of the grid
- * to finish (one atomic increment of *counter after an agent-scope release) sums every block's partials and
- * finalizes -- bit-identical to the two-launch forms (the sums share one fixed order).  counter: a caller-owned
- * uint32 in device memory, zero before the first use; each launch leaves it zero again (it wraps at the grid
- * size), so one counter serves any number of launches ordered on one stream.  msp_bn_bwd_apply_sums is
- * msp_bn_bwd_apply_add without the channel sums (taken from the partial buffer's tail). */
-int msp_bn_stats_finalize(const float* x, int64_t V, int C, double* partial, unsigned* counter, double eps,
-                          double momentum, float* running_mean, float* running_var, const float* weight,
-                          const float* bias, float* stats, msp_stream_t stream);
-int msp_bn_bwd_stats_finalize(const float* x, const float* dy, int64_t V, int C, const float* stats, float leak,
-                              double* partial, unsigned* counter, float* dweight, float* dbias,
-                              msp_stream_t stream);
-int msp_bn_bwd_apply_sums(const float* x, const float* dy, int64_t V, int C, const double* partial,
-                          const float* stats, const float* weight, float leak, int train, const float* addend,
-                          float* dx, msp_stream_t stream);
 /* Channel join (SCN JoinTable, the UNet / FCN skip joins: identity branch first, then the upsampled deeper
  * level): out[v] = [a[v] | b[v]], a [V][ca], b [V][cb], out [V][ca + cb].  With partial
  * non-NULL also the msp_bn_stats partials of out (identical to msp_bn_stats on it), for the BatchNormalization

@@ -903,37 +903,3 @@ def test_sort_pairs_stable(n, end_bit, span):
     _lib.call("msp_sort_pairs", ptr(kin), ptr(kout), ptr(vin), ptr(vout), n, end_bit, ptr(ws), wsb, _lib.stream())
     assert np.array_equal(vout.cpu().numpy(), order.astype(np.int32))
     assert np.array_equal(kout.cpu().numpy().view(np.uint64), keys[order])
-
-
-@pytest.mark.parametrize("V,C", [(3000, 32), (1349716 // 8, 64), (2125, 192), (536, 448), (700, 6)])
-def test_bn_one_launch_finalize_bit_identical(V, C):
-    """msp_bn_stats_finalize / msp_bn_bwd_stats_finalize (the grid's last block finalizes, ABI 9) against the
-    two-launch forms (msp_bn_stats + msp_bn_finalize; msp_bn_bwd_stats + the apply's own channel sums): stats,
-    running statistics, dx, dweight and dbias bit for bit, over repeated launches on ONE counter (each launch must
-    leave it zero) and partial counts from 1 to 1024 blocks; C = 6 takes the two-launch fallback."""
-    from sparseconvnet import ops
-    torch.manual_seed(V + C)
-    x = (torch.randn(V, C, device=DEV) * 3 + torch.linspace(-2, 2, C, device=DEV)).contiguous()
-    gy = torch.randn(V, C, device=DEV)
-    add = torch.randn(V, C, device=DEV)
-    w = torch.linspace(0.5, 1.5, C, device=DEV)
-    b = torch.linspace(-0.2, 0.3, C, device=DEV)
-    outs = {}
-    for fused in (False, True):
-        ops.FUSE_FINALIZE = fused
-        try:
-            rm, rv = torch.linspace(-1, 1, C, device=DEV), torch.linspace(0.5, 2, C, device=DEV)
-            got = []
-            for rep in range(3):  # the same counter reused: a launch that left it non-zero breaks the next
-                xi = x * (1 + 0.1 * rep)
-                y, st = ops._bn_fwd(xi, w, b, rm, rv, 1e-4, 0.9, 0.1, True, None)
-                dx, dw, db = ops._bn_bwd(xi, w, st, (0.1, 1, True, True), gy, add)
-                got += [y, st, dx, dw, db, rm.clone(), rv.clone()]
-            torch.cuda.synchronize()
-            outs[fused] = got
-        finally:
-            ops.FUSE_FINALIZE = True
-    for k, (a, c) in enumerate(zip(outs[False], outs[True])):
-        assert torch.equal(a, c), (k, (a - c).abs().max().item())
-    cnt = ops._counter(x.device, 0)
-    assert int(cnt[0]) == 0 and int(ops._counter(x.device, 1)[0]) == 0
