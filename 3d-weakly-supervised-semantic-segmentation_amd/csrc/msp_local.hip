@@ -65,13 +65,19 @@ __device__ void bitonic_i32(int32_t* a) {
 }
 
 // The tile's distinct input rows, unordered: its K x T neighbour entries (all loads in flight first) go
-// into an open-addressing hash set in LDS (2 N2 int32 slots, load <= 0.42, linear probing by LDS CAS); each
-// first insertion appends the row to uq.  Returns the count.  (Round 2 replaced a bitonic sort of all
-// N2 entries: a tile names 1.6-2 x T distinct rows of 27 T entries, so sorting only those is ~10x less work.)
+// into an open-addressing hash set in LDS (kHashMult N2 int32 slots, linear probing by LDS CAS); each first
+// insertion appends the row to uq.  Returns the count.  (Round 2 replaced a bitonic sort of all N2 entries: a
+// tile names 1.6-2 x T distinct rows of 27 T entries, so sorting only those is ~10x less work.)  Slots: N2 since
+// round 5 (load 0.05-0.1 on surfaces, at most 0.84 for a map whose 27 T entries are all distinct): 32 KB of LDS per
+// block instead of 48, so a build block beside the compute stream's one-block-per-CU weight gradient (125 KB) no
+// longer keeps it off that CU.
+#ifndef MSP_LOCAL_HASH_MULT  // experiments: 2 = the round-2..4 table (2 N2 slots)
+#define MSP_LOCAL_HASH_MULT 1
+#endif
 template <int T, int N2>
 __device__ int tile_distinct(const int32_t* __restrict__ nbr, int K, int64_t n, int64_t t, int32_t* h, int32_t* uq,
                              int* cnt) {
-  constexpr int HS = 2 * N2, HB = __builtin_ctz(HS);
+  constexpr int HS = MSP_LOCAL_HASH_MULT * N2, HB = __builtin_ctz(HS);
   constexpr int PER = N2 / kLT;  // K T <= N2 entries
   for (int i = threadIdx.x; i < HS; i += kLT) h[i] = -1;
   if (threadIdx.x == 0) *cnt = 0;
@@ -129,7 +135,7 @@ template <int T, int N2>
 __global__ __launch_bounds__(kLT) void local_count_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
                                                           int64_t* __restrict__ cnt,
                                                           unsigned long long* __restrict__ mx) {
-  __shared__ int32_t h[2 * N2];
+  __shared__ int32_t h[MSP_LOCAL_HASH_MULT * N2];
   __shared__ int32_t uq[N2];
   __shared__ int c;
   const int64_t t = blockIdx.x;
@@ -250,7 +256,7 @@ __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restri
                                                          int64_t n_pad, const int64_t* __restrict__ u_start,
                                                          int32_t* __restrict__ u_rows, uint16_t* __restrict__ lidx,
                                                          int32_t* __restrict__ perm, uint8_t* __restrict__ wave_off) {
-  __shared__ int32_t h[2 * N2];
+  __shared__ int32_t h[MSP_LOCAL_HASH_MULT * N2];
   __shared__ int32_t uq[N2];
   __shared__ uint32_t msk[T];
   __shared__ uint8_t ord[T];

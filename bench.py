@@ -591,6 +591,7 @@ def main():
     bounds[0].record(cur)
     t0 = time.perf_counter()
     loop_t = []  # graph loop host seconds per step: (replay call incl. an eager exchange, prefetch, capture)
+    mem_t = []  # torch's reserved device memory after each step's capture
     if use_graph:
         inflight, dones = [], []
         for i in range(args.steps):
@@ -622,6 +623,7 @@ def main():
             h3 = time.perf_counter()
             entry = capture(i + 1) if i + 1 < args.steps else None
             loop_t.append((h1 - h0, h2 - h1, time.perf_counter() - h3))
+            mem_t.append(torch.cuda.memory_reserved(dev))
             if host_t is not None:
                 host_t.append((h1 - h0, h2 - h1, h3 - h2, time.perf_counter() - h3))
         if host_t:
@@ -631,6 +633,8 @@ def main():
             cp = [1e3 * statistics.median(c) for c in zip(*capture_parts[-args.steps:])]
             print(f"bench.py capture host ms (median): begin {cp[0]:.2f}  body {cp[1]:.2f}  end {cp[2]:.2f}",
                   file=sys.stderr)
+            print("bench.py reserved device memory after each capture, GB:",
+                  [round(m / 2**30, 1) for m in mem_t], file=sys.stderr)
             print(f"bench.py metadata count reads: {scn_meta.READ_STATS[1]} reads, "
                   f"{1e3 * scn_meta.READ_STATS[0]:.1f} ms of host wait in total", file=sys.stderr)
             host_t.clear()
@@ -758,6 +762,10 @@ def main():
                     if graph_dp else "DDP, 64 MB buckets overlapped with backward"),
                 "comm_backend": dist.get_backend() if dist.is_initialized() else None,
                 "host_threads_per_rank": host_threads if host_threads is not None else torch.get_num_threads(),
+                "device_memory_gb": {"max_allocated": torch.cuda.max_memory_allocated(dev) / 2**30,
+                                     "reserved_first_step": mem_t[0] / 2**30 if mem_t else None,
+                                     "reserved_last_step": mem_t[-1] / 2**30 if mem_t else None,
+                                     "note": "rank 0; torch caching allocator, graph pools included"},
                 "rank_host_ms_per_step": {"replay_call_incl_eager_exchange": rank_host[0],
                                           "prefetch": rank_host[1], "capture": rank_host[2],
                                           "note": "graph loop, median per rank (rank order)"} if loop_t else None,
