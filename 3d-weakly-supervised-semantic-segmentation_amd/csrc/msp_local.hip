@@ -791,11 +791,17 @@ __global__ __launch_bounds__(256) void wgrad_far_kernel(const float* __restrict_
 }
 
 constexpr int kWMaxCh = 216;                   // chunks of one 128-row tile (K <= 27 offsets x 8)
-constexpr int kWXImg = (kWCap + 1) * 32;       // bf16 elements of one x piece image (+ zero row kWCap)
-constexpr int kWDImg = (kWTile + 1) * 32;      // dy piece image (+ zero row 128)
 
 // bf16 element offset of 8-byte unit v (channels 4v .. 4v+3 of the slice) of row j in a piece image
 __device__ __forceinline__ int wimg_off(int j, int v) { return j * 32 + 4 * (v ^ (((j >> 2) & 1) << 2)); }
+// RS (row stride of the piece images, bf16 elements): 32 = the XOR-swizzled layout above; 36 = rows padded to 72
+// bytes, unswizzled, so the 16 rows one transposing read names start at 8-byte granules spread over the banks instead
+// of eight 32-byte windows (experiments: the round-4 PMC put bank conflicts at 0.42 of the kernel's LDS cycles)
+template <int RS>
+__device__ __forceinline__ int wimg_off_rs(int j, int v) {
+  if constexpr (RS == 32) return wimg_off(j, v);
+  return j * RS + 4 * v;
+}
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint2 tr_read(const uint16_t* p) {
@@ -826,7 +832,7 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
 // PW 1 (the product form): the next k-step's rule words are read from LDS at the start of the current one (within
 // an offset), so a k-step no longer opens with an LDS read -> address -> transposing-read chain: 1-6 % faster at
 // levels 0-3 (profiles/r03/kbexp_r03pw.log); PW 0 reads them at the k-step's start.
-template <int NW, int AC = 1, int PW = 1>
+template <int NW, int AC = 1, int PW = 1, int RS = 32>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -837,6 +843,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   constexpr int DI = kWTile * 8 / NTH;                // dy staging items per thread
   constexpr int EI = (kWMaxCh * 16 + NTH - 1) / NTH;  // rule words per thread
   static_assert(DI * NTH == kWTile * 8, "dy staging items must divide evenly");
+  // bf16 elements of one x piece image (+ zero row kWCap) and of one dy piece image (+ zero row 128)
+  constexpr int kWXImg = (kWCap + 1) * RS, kWDImg = (kWTile + 1) * RS;
   __shared__ __attribute__((aligned(16))) uint16_t xim[3 * kWXImg];
   __shared__ __attribute__((aligned(16))) uint16_t dim[3 * kWDImg];
   __shared__ uint32_t ent[(kWMaxCh + 1) * 16];  // + one chunk: the partner read of a last odd chunk stays inside
@@ -862,8 +870,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
 
   // zero rows (never overwritten) and the padding chunk of the rule words
   for (int i = tid; i < 3 * 32; i += NTH) {
-    xim[(i / 32) * kWXImg + kWCap * 32 + (i % 32)] = 0;
-    dim[(i / 32) * kWDImg + kWTile * 32 + (i % 32)] = 0;
+    xim[(i / 32) * kWXImg + kWCap * RS + (i % 32)] = 0;
+    dim[(i / 32) * kWDImg + kWTile * RS + (i % 32)] = 0;
   }
   if (tid < 16) ent[kWMaxCh * 16 + tid] = (uint32_t)kWCap | ((uint32_t)kWTile << 16);
 
@@ -913,7 +921,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
         split4(xv[b], pc);
 #pragma unroll
         for (int pp = 0; pp < 3; ++pp)
-          *reinterpret_cast<uint2*>(xim + pp * kWXImg + wimg_off(it >> 3, it & 7)) = pc[pp];
+          *reinterpret_cast<uint2*>(xim + pp * kWXImg + wimg_off_rs<RS>(it >> 3, it & 7)) = pc[pp];
       }
     }
 #pragma unroll
@@ -923,7 +931,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       split4(dv[b], pc);
 #pragma unroll
       for (int pp = 0; pp < 3; ++pp)
-        *reinterpret_cast<uint2*>(dim + pp * kWDImg + wimg_off(it >> 3, it & 7)) = pc[pp];
+        *reinterpret_cast<uint2*>(dim + pp * kWDImg + wimg_off_rs<RS>(it >> 3, it & 7)) = pc[pp];
     }
 #pragma unroll
     for (int b = 0; b < EI; ++b) {
@@ -967,8 +975,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     rows_from(wd, hasB, xr, dr);
   };
   auto frag = [&](const uint16_t* img, const int (&rr)[2], int v) {
-    const uint2 lo = tr_read(img + wimg_off(rr[0], v));
-    const uint2 hi = tr_read(img + wimg_off(rr[1], v));
+    const uint2 lo = tr_read(img + wimg_off_rs<RS>(rr[0], v));
+    const uint2 hi = tr_read(img + wimg_off_rs<RS>(rr[1], v));
     return u32x4{lo.x, lo.y, hi.x, hi.y};
   };
   uint32_t wcur[2] = {0u, 0u}, wnxt[2] = {0u, 0u};  // PW: this and the next k-step's rule words
@@ -1221,9 +1229,10 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
   hipStream_t s = as_stream(stream);
   const int64_t n_tiles = ceil_div(n_rows, kWTile);
   const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
-  wgrad_x6c_kernel<8><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
-                                                                    chunk_lr, u_start, u_rows, n_rows, n_tiles,
-                                                                    (int)n_ranges, slab);
+  // 72-byte image rows (RS = 36): 9-15 % faster than the swizzled 64-byte rows at every level
+  // (profiles/r05/kbexp_r05m_x6c_row_stride.log)
+  wgrad_x6c_kernel<8, 1, 1, 36><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
+      x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
   wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 16), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
                                                                          (int)n_ranges, n4,
@@ -1387,6 +1396,9 @@ int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, 
   else if (variant == 3)
     wgrad_x6c_kernel<8, 1, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start,
                                                    u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  else if (variant == 43)  // the product form with 72-byte image rows (RS = 36)
+    wgrad_x6c_kernel<8, 1, 1, 36><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr,
+                                                       u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
 
   else {
     set_error("msp_exp_wgrad_chunk: no variant %d", variant);
