@@ -797,6 +797,9 @@ __device__ __forceinline__ int wimg_off(int j, int v) { return j * 32 + 4 * (v ^
 // RS (row stride of the piece images, bf16 elements): 32 = the XOR-swizzled layout above; 36 = rows padded to 72
 // bytes, unswizzled, so the 16 rows one transposing read names start at 8-byte granules spread over the banks instead
 // of eight 32-byte windows (experiments: the round-4 PMC put bank conflicts at 0.42 of the kernel's LDS cycles)
+#ifndef MSP_X6C_RS  // the product's image row stride (experiments: 32 = the round-2..4 swizzled rows)
+#define MSP_X6C_RS 36
+#endif
 template <int RS>
 __device__ __forceinline__ int wimg_off_rs(int j, int v) {
   if constexpr (RS == 32) return wimg_off(j, v);
@@ -1231,7 +1234,7 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
   const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
   // 72-byte image rows (RS = 36): 9-15 % faster than the swizzled 64-byte rows at every level
   // (profiles/r05/kbexp_r05m_x6c_row_stride.log)
-  wgrad_x6c_kernel<8, 1, 1, 36><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
+  wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
       x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
   wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 16), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
