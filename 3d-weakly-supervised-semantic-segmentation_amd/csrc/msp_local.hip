@@ -1142,11 +1142,11 @@ int msp_wgrad_chunk_ok(int64_t n_rows, int K, int c_in, int c_out) {
 // in isolation since the products accumulate straight into the tile sums (0.327 vs 0.347 ms,
 // profiles/r03/kbench_r03y_level0.log) but needs level 0's tile-local rulebook (see msp_conv_local_preferred):
 // 32 output channels stay on the pair lists.
-#ifndef MSP_CHUNK_NARROW  // 1: c_in <= c_out = 32 too (level 0's 32 x 32, over a lists-only tile-local rulebook)
-#define MSP_CHUNK_NARROW 1
+#ifndef MSP_CHUNK_NARROW  // 1: c_out = 32 too (level 0's 32 x 32 and, since round 5's 72-byte image rows, the
+#define MSP_CHUNK_NARROW 1  // decoder's 64 x 32: 0.490 vs 0.517 ms on the pair lists, profiles/r05/kbench_r05p_*)
 #endif
 int msp_wgrad_chunk_preferred(int64_t n_rows, int K, int c_in, int c_out) {
-  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && (c_out >= 64 || (MSP_CHUNK_NARROW && c_in <= c_out)) ? 1
+  return msp_wgrad_chunk_ok(n_rows, K, c_in, c_out) && (c_out >= 64 || (MSP_CHUNK_NARROW && c_out == 32)) ? 1
                                                                                                              : 0;
 }
 
