@@ -689,7 +689,10 @@ __global__ __launch_bounds__(256) void wgrad_ranges_reduce_kernel(const floatx4*
 // w, w + 8, w + 16, w + 24 and keeps their 32 x 32 tiles in registers over the range; the next tile's rows,
 // values and rule words are in flight in registers while the current tile computes.  Per range a slab of
 // partial dW is written and the ranges are added in order (deterministic).
-constexpr int kWCap = 448;     // distinct rows per 128-row tile the weight gradient stages (msp_conv_wgrad_chunk)
+#ifndef MSP_X6C_CAP  // experiments: 384 keeps the block (with 72-byte rows) + one 32 KB build block within a CU's LDS
+#define MSP_X6C_CAP 448
+#endif
+constexpr int kWCap = MSP_X6C_CAP;  // distinct rows per 128-row tile the weight gradient stages (msp_conv_wgrad_chunk)
 constexpr uint32_t kWFar = 0xFFFFu;  // chunk entry whose input row lies past kWCap (never staged)
 
 constexpr int kWTile = 128;

@@ -619,6 +619,8 @@ def main():
             # graphs themselves are kept until the loop has drained: destroying an executable graph here
             # synchronised with the device (measured: 49 ms per step of host wait, the device idle through the
             # next capture)
+            if host_t is not None and i + 1 == args.steps:
+                last_entry = inflight[-1][0]  # BENCH_HOST_TIMING: kept whole for the back-to-back replays below
             inflight[-1] = (inflight[-1][0][0], None, i)
             h3 = time.perf_counter()
             entry = capture(i + 1) if i + 1 < args.steps else None
@@ -649,6 +651,19 @@ def main():
             print("bench.py metadata build done, ms after the previous step's end:",
                   [round(replay_ev[k][1].elapsed_time(build_ev[k + 1]), 2) for k in range(len(replay_ev) - 1)],
                   file=sys.stderr)
+            # the last step's graph replayed three times back to back (its metadata kept alive; nothing queued in
+            # between but the events): the idle before a replay that no host work or stream wait precedes
+            evs = []
+            for _ in range(3):
+                evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                evs[-1][0].record(cur)
+                last_entry[0].replay()
+                evs[-1][1].record(cur)
+            torch.cuda.synchronize()
+            print("bench.py back-to-back replays of one graph, device ms:",
+                  [round(a.elapsed_time(b), 2) for a, b in evs], "idle before each:",
+                  [round(evs[k][1].elapsed_time(evs[k + 1][0]), 3) for k in range(2)], file=sys.stderr)
+            last_entry = None
         if fut is not None:
             fut.result()
         if worker is not None:
