@@ -28,6 +28,7 @@ sample on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -59,6 +60,8 @@ FAMILIES = {"wgrad": "wgrad", "nin_wgrad": "wgrad", "wgrad_strided": "wgrad", "w
             "conv_bwd_data": "pairs", "deconv_fwd": "pairs",
             "nin_fwd": "nin", "nin_bwd_data": "nin", "bn_fwd": "bn", "bn_bwd": "bn", "bn_join": "bn"}
 
+
+_HIP_RT = None  # ctypes handle of the HIP runtime (bench.py --graph-upload)
 
 def family(kind):
     base = kind.split("/")[0]
@@ -307,6 +310,14 @@ def main():
     ap.add_argument("--prefetch-at", choices=["end", "fwd"], default="end",
                     help="when the next batch's metadata is built: after the step's optimizer call is queued (end) "
                          "or right after its forward is queued (fwd: the build's host reads overlap the forward)")
+    ap.add_argument("--meta-release", choices=["done", "stream"], default="done",
+                    help="graph mode: when a replayed step's metadata is freed -- done: once the step's end event has "
+                         "completed (polled on the host, nothing queued on the device); stream: right after the "
+                         "replay is queued, its tensors marked as used by the compute stream (the caching allocator "
+                         "then records one event per freed block on that stream: ~1.1 ms of device idle per step)")
+    ap.add_argument("--graph-upload", type=int, choices=[0, 1], default=0,
+                    help="graph mode, 1: each captured graph is uploaded (hipGraphUpload) on the capture stream right "
+                         "after its capture, while the previous step runs; the replay waits for the upload")
     ap.add_argument("--graph", type=int, choices=[0, 1], default=None,
                     help="1: capture every step afresh into a HIP graph (built after the step's metadata is "
                          "prefetched, replayed on the compute stream while the next step is prefetched and "
@@ -512,6 +523,15 @@ def main():
             gsync.join()  # the exchange's graph nodes rejoin the captured stream
         return loss
 
+    def _hip_runtime():
+        # the HIP runtime torch itself loaded (by soname); only --graph-upload calls into it
+        global _HIP_RT
+        if _HIP_RT is None:
+            _HIP_RT = ctypes.CDLL("libamdhip64.so")
+            _HIP_RT.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            _HIP_RT.hipGraphUpload.restype = ctypes.c_int
+        return _HIP_RT
+
     def capture(i):
         """Graph of step i, whose metadata is the pending prefetch; returns (graph, metadata it reads, the
         metadata's build event).  Nothing executes here: the kernels run at replay."""
@@ -528,6 +548,14 @@ def main():
             c2 = time.perf_counter()
             g.capture_end()
             c3 = time.perf_counter()
+            up = None
+            if args.graph_upload:
+                rc = _hip_runtime().hipGraphUpload(ctypes.c_void_p(g.raw_cuda_graph_exec()),
+                                                   ctypes.c_void_p(cap_stream.cuda_stream))
+                if rc != 0:
+                    raise RuntimeError(f"bench.py --graph-upload: hipGraphUpload returned {rc}")
+                up = torch.cuda.Event()
+                up.record(cap_stream)
         if host_t is not None:
             capture_parts.append((c1 - c0, c2 - c1, c3 - c2))
         keep = scn_meta.captured_metadata()
@@ -536,7 +564,7 @@ def main():
         if not keep:
             raise RuntimeError("bench.py --graph: the captured step did not consume its prefetched metadata")
         capture_s.append(time.perf_counter() - t)
-        return g, keep, ev
+        return g, keep, ev, up
 
     replay_ev = []
     build_ev = []  # BENCH_HOST_TIMING: each replay's metadata build event (when the build finished on the device)
@@ -545,11 +573,14 @@ def main():
         scn_meta.READ_STATS = [0.0, 0]
 
     def replay(entry):
-        g, keep, ev = entry
+        g, keep, ev, up = entry
         cur.wait_event(ev)  # the metadata build (side stream) before the graph reads it
-        for m in keep:
-            for t in m.tensors():
-                t.record_stream(cur)
+        if up is not None:
+            cur.wait_event(up)
+        if args.meta_release == "stream":
+            for m in keep:
+                for t in m.tensors():
+                    t.record_stream(cur)
         if host_t is not None:
             replay_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
             replay_ev[-1][0].record(cur)
@@ -592,6 +623,8 @@ def main():
     t0 = time.perf_counter()
     loop_t = []  # graph loop host seconds per step: (replay call incl. an eager exchange, prefetch, capture)
     mem_t = []  # torch's reserved device memory after each step's capture
+    last_entries = []
+    held = []  # --meta-release done: (metadata, end event) of replayed steps the device may still read
     if use_graph:
         inflight, dones = [], []
         for i in range(args.steps):
@@ -615,12 +648,18 @@ def main():
                 fut = worker.submit(prefetch, i + 1, dones[-2] if len(dones) >= 2 else None) \
                     if i + 2 <= args.steps else None
             h2 = time.perf_counter()
-            # the step's metadata is released now (its tensors were marked as used by the compute stream); the
-            # graphs themselves are kept until the loop has drained: destroying an executable graph here
-            # synchronised with the device (measured: 49 ms per step of host wait, the device idle through the
-            # next capture)
-            if host_t is not None and i + 1 == args.steps:
-                last_entry = inflight[-1][0]  # BENCH_HOST_TIMING: kept whole for the back-to-back replays below
+            # the graphs are kept until the loop has drained: destroying an executable graph here synchronised
+            # with the device (measured: 49 ms per step of host wait, the device idle through the next capture).
+            # The metadata goes as soon as the device is done with it: --meta-release done keeps it until the
+            # step's end event has completed (a host poll; the build's count reads above have waited for step
+            # i - lag, so step i - 1's is normally complete by now) and frees it with no device work; stream frees
+            # it now, its tensors marked as used by the compute stream, and the allocator then records an event on
+            # that stream per freed block -- a few hundred markers queued between this step and the next
+            if host_t is not None and i + 2 >= args.steps:
+                last_entries.append(inflight[-1][0])  # BENCH_HOST_TIMING: kept whole for the replays below
+            if args.meta_release == "done":
+                held.append((inflight[-1][0][1], done))
+                held[:] = [h for h in held if not h[1].query()]
             inflight[-1] = (inflight[-1][0][0], None, i)
             h3 = time.perf_counter()
             entry = capture(i + 1) if i + 1 < args.steps else None
@@ -651,19 +690,48 @@ def main():
             print("bench.py metadata build done, ms after the previous step's end:",
                   [round(replay_ev[k][1].elapsed_time(build_ev[k + 1]), 2) for k in range(len(replay_ev) - 1)],
                   file=sys.stderr)
-            # the last step's graph replayed three times back to back (its metadata kept alive; nothing queued in
-            # between but the events): the idle before a replay that no host work or stream wait precedes
-            evs = []
-            for _ in range(3):
-                evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
-                evs[-1][0].record(cur)
-                last_entry[0].replay()
-                evs[-1][1].record(cur)
-            torch.cuda.synchronize()
-            print("bench.py back-to-back replays of one graph, device ms:",
-                  [round(a.elapsed_time(b), 2) for a, b in evs], "idle before each:",
-                  [round(evs[k][1].elapsed_time(evs[k + 1][0]), 3) for k in range(2)], file=sys.stderr)
-            last_entry = None
+            # the last two steps' graphs replayed back to back (their metadata kept alive; nothing queued in
+            # between but the events): the idle before a replay that no host work precedes -- the same graph
+            # twice, two different graphs, and a graph behind a wait on its (long completed) build event
+            def b2b(seq, wait=False):
+                evs = []
+                for e in seq:
+                    if wait:
+                        cur.wait_event(e[2])
+                    evs.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                    evs[-1][0].record(cur)
+                    e[0].replay()
+                    evs[-1][1].record(cur)
+                torch.cuda.synchronize()
+                return ([round(a.elapsed_time(b), 2) for a, b in evs],
+                        [round(evs[k][1].elapsed_time(evs[k + 1][0]), 3) for k in range(len(evs) - 1)])
+            ea, eb = last_entries[-2], last_entries[-1]
+            for what, seq, wait in (("one graph", [eb, eb, eb], False), ("two graphs", [ea, eb, ea, eb], False),
+                                    ("one graph after its build-event wait", [eb, eb, eb], True),
+                                    ("two graphs after their build-event waits", [ea, eb, ea, eb], True)):
+                ms, idle = b2b(seq, wait)
+                print(f"bench.py back-to-back replays, {what}: device ms {ms} idle before each {idle}",
+                      file=sys.stderr)
+            # freshly captured graphs (their metadata built beforehand), each replayed twice right behind a replay
+            # of an old graph of the same batch (the device busy, not idling through the capture): does a graph's
+            # first replay run slower than its later ones, and does an upload (hipGraphUpload) beforehand help?
+            fresh = []
+            for j, upload in ((0, False), (2, True)):
+                k = args.steps + 1 + j
+                prefetch(k - 1)
+                torch.cuda.synchronize()
+                e = capture(k)
+                if upload:
+                    rc = _hip_runtime().hipGraphUpload(ctypes.c_void_p(e[0].raw_cuda_graph_exec()),
+                                                       ctypes.c_void_p(cap_stream.cuda_stream))
+                    assert rc == 0, rc
+                torch.cuda.synchronize()
+                fresh.append(e)
+            ms, idle = b2b([eb, fresh[0], fresh[0], eb, fresh[1], fresh[1]], True)
+            print(f"bench.py old graph, fresh graph twice, old graph, fresh uploaded graph twice: device ms {ms} "
+                  f"idle {idle}", file=sys.stderr)
+            fresh = None
+            last_entries.clear()
         if fut is not None:
             fut.result()
         if worker is not None:
@@ -679,6 +747,7 @@ def main():
     dt = time.perf_counter() - t0
     step_ms = [a.elapsed_time(b) for a, b in zip(bounds[:-1], bounds[1:])]
     rec.active = False
+    held.clear()  # every step has completed
     if use_graph:
         inflight = entry = None
         _lib.set_recorder(None)
