@@ -76,12 +76,16 @@ __device__ void bitonic_i32(int32_t* a) {
 #endif
 template <int T, int N2>
 __device__ int tile_distinct(const int32_t* __restrict__ nbr, int K, int64_t n, int64_t t, int32_t* h, int32_t* uq,
-                             int* cnt) {
+                             int* cnt, int32_t (&m)[N2 / kLT], uint32_t* msk = nullptr) {
+  // m: this thread's entries (offset i / T, row i % T for i = threadIdx.x + kLT j; -1 absent), kept in registers
+  // for the caller (the fill's local indices).  msk (optional, T words): each row's neighbour mask, set here from
+  // those same entries by LDS OR.
   constexpr int HS = MSP_LOCAL_HASH_MULT * N2, HB = __builtin_ctz(HS);
   constexpr int PER = N2 / kLT;  // K T <= N2 entries
   for (int i = threadIdx.x; i < HS; i += kLT) h[i] = -1;
+  if (msk)
+    for (int i = threadIdx.x; i < T; i += kLT) msk[i] = 0u;
   if (threadIdx.x == 0) *cnt = 0;
-  int32_t m[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int i = threadIdx.x + kLT * j;
@@ -97,6 +101,10 @@ __device__ int tile_distinct(const int32_t* __restrict__ nbr, int K, int64_t n, 
   for (int j = 0; j < PER; ++j) {
     const int32_t v = m[j];
     if (v < 0) continue;
+    if (msk) {
+      const int i = threadIdx.x + kLT * j, o = i / T;
+      atomicOr(&msk[i - o * T], 1u << o);
+    }
     uint32_t sl = ((uint32_t)v * 2654435761u) >> (32 - HB);
     while (true) {
       const int32_t prev = atomicCAS(&h[sl], -1, v);
@@ -110,6 +118,15 @@ __device__ int tile_distinct(const int32_t* __restrict__ nbr, int K, int64_t n, 
   }
   __syncthreads();
   return *cnt;
+}
+
+// The hash slot of v (present in h: inserted by tile_distinct).
+template <int HS>
+__device__ __forceinline__ int hash_slot(const int32_t* h, int32_t v) {
+  constexpr int HB = __builtin_ctz(HS);
+  uint32_t sl = ((uint32_t)v * 2654435761u) >> (32 - HB);
+  while (h[sl] != v) sl = (sl + 1) & (HS - 1);
+  return (int)sl;
 }
 
 // ascending bitonic sort of a[0 .. n2) (n2 a power of two, <= N2)
@@ -139,7 +156,8 @@ __global__ __launch_bounds__(kLT) void local_count_kernel(const int32_t* __restr
   __shared__ int32_t uq[N2];
   __shared__ int c;
   const int64_t t = blockIdx.x;
-  const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c);
+  int32_t m[N2 / kLT];
+  const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c, m);
   if (threadIdx.x == 0) {
     cnt[t] = tot;
     atomicMax(mx, (unsigned long long)tot);
@@ -196,7 +214,11 @@ __device__ void group_rows(const uint32_t* __restrict__ msk, int nv, uint8_t* __
 #pragma unroll
     for (int j = 0; j < RPL; ++j)
       if (p == lane + 64 * j) fr[j] = false;
-    um = (seed ? 0u : um) | msk[p];
+    uint32_t mp = m[0];  // row p's mask from its lane's registers (p is wave-uniform): no LDS round trip
+#pragma unroll
+    for (int j = 1; j < RPL; ++j)
+      if ((p >> 6) == j) mp = m[j];
+    um = (seed ? 0u : um) | (uint32_t)__builtin_amdgcn_readlane((int)mp, p & 63);
     if (lane == 0) ord[pos] = (uint8_t)p;
     if ((pos & 15) == 15 || pos == nv - 1) {
       if (lane == 0) gmask[pos >> 4] = um;
@@ -214,36 +236,51 @@ __device__ void group_rows(const uint32_t* __restrict__ msk, int nv, uint8_t* __
 #ifndef MSP_SHARED_LISTS  // experiments: 1 = both halves walk one list dealt from all 8 groups (their weight loads
 #define MSP_SHARED_LISTS 0  // then coincide, which the vector L1 can serve once)
 #endif
-__device__ void deal_offsets(const uint32_t* __restrict__ gmask, int K, int h, uint8_t* __restrict__ item,
-                             int* __restrict__ cost, uint8_t* __restrict__ wo) {
-  int n = 0;  // item / cost: this half's LDS scratch, the offsets by cost descending (ties: lower offset first)
-  for (int o = 0; o < K; ++o) {
-    int a = 0;
+// One wave deals both halves: lanes 32 h + o hold offset o's cost in half h; each lane ranks its offset (cost
+// descending, then offset ascending: the order an insertion sort by cost gives) with K shuffles, the ranked lists
+// go to LDS, and lanes 0 and 32 deal them out greedily from registers.  (Round 4's form ran the ranking as an
+// insertion sort through LDS on one lane per half: ~K^2 / 2 dependent LDS round trips per tile.)
+__device__ void deal_offsets(const uint32_t* __restrict__ gmask, int K, uint8_t* __restrict__ item,
+                             int* __restrict__ cost, uint8_t* __restrict__ wo2) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, o = lane & 31;
+  int a = 0;  // item / cost: [2][kKMax] LDS scratch; wo2: the tile's two halves' lists (2 x 32 bytes)
+  if (o < K)
     for (int g = MSP_SHARED_LISTS ? 0 : h; g < 8; g += MSP_SHARED_LISTS ? 1 : 2) a += (gmask[g] >> o) & 1u;
-    if (a == 0) continue;
-    int i = n++;
-    while (i > 0 && cost[i - 1] < a) {
-      cost[i] = cost[i - 1];
-      item[i] = item[i - 1];
-      --i;
-    }
-    cost[i] = a;
-    item[i] = (uint8_t)o;
+  int r = 0;
+  for (int q = 0; q < K; ++q) {
+    const int aq = __shfl(a, (h << 5) + q, 64);
+    r += (aq > a || (aq == a && q < o)) ? 1 : 0;
   }
+  const unsigned long long nz = __ballot(a > 0);
+  const int n = __popcll(h ? (nz >> 32) : (nz & 0xFFFFFFFFull));
+  if (a > 0) {
+    item[h * kKMax + r] = (uint8_t)o;
+    cost[h * kKMax + r] = a;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (o != 0) return;
+  int cs[kKMax];
+#pragma unroll
+  for (int i = 0; i < kKMax; ++i) cs[i] = cost[h * kKMax + i];
+  uint8_t* wo = wo2 + h * 32;
   int l0 = 0, l1 = 0, l2 = 0, l3 = 0, n0 = 0, n1 = 0, n2 = 0, n3 = 0;  // load and count per wave
-  for (int i = 0; i < n; ++i) {
+#pragma unroll
+  for (int i = 0; i < kKMax; ++i) {
+    if (i >= n) continue;  // (not break: the loop stays unrolled, cs[] in registers)
     int c = -1, lc = 0;
     if (n0 < 8) c = 0, lc = l0;
     if (n1 < 8 && (c < 0 || l1 < lc)) c = 1, lc = l1;
     if (n2 < 8 && (c < 0 || l2 < lc)) c = 2, lc = l2;
     if (n3 < 8 && (c < 0 || l3 < lc)) c = 3, lc = l3;
-    const int add = 4 * cost[i] + 1;
+    const int add = 4 * cs[i] + 1;
     const int k = c == 0 ? n0++ : c == 1 ? n1++ : c == 2 ? n2++ : n3++;
     if (c == 0) l0 += add;
     else if (c == 1) l1 += add;
     else if (c == 2) l2 += add;
     else l3 += add;
-    wo[c * 8 + k] = item[i];
+    wo[c * 8 + k] = item[h * kKMax + i];
   }
   for (int k = n0; k < 8; ++k) wo[k] = 0xFF;
   for (int k = n1; k < 8; ++k) wo[8 + k] = 0xFF;
@@ -251,21 +288,64 @@ __device__ void deal_offsets(const uint32_t* __restrict__ gmask, int K, int h, u
   for (int k = n3; k < 8; ++k) wo[24 + k] = 0xFF;
 }
 
-template <int T, int N2>
+// conv_x6s's row order and offset lists of the tile-local rulebook (msp_tile_local, before the fill), one wave per
+// tile: the rows' neighbour masks from nbr, group_rows' greedy 16-row groups, deal_offsets' per-wave lists, the
+// order as perm.  group_rows is a serial chain of T wave-wide minima; run inside the fill's 256-thread block, only
+// that block's first wave worked on it while three waited at the barrier, and the fill's LDS allowed four blocks
+// per CU (~460 us over the headline batch's seven levels, scripts/build_bench.py).  Here a CU keeps up to 32
+// tiles' chains in flight.
+template <int T>
+__global__ __launch_bounds__(256) void local_group_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
+                                                          int64_t n_tiles, int32_t* __restrict__ perm,
+                                                          uint8_t* __restrict__ wave_off) {
+  __shared__ uint32_t msk[4][T];
+  __shared__ uint8_t ord[4][T];
+  __shared__ uint32_t gmask[4][T / 16];
+  __shared__ uint8_t ditem[4][2 * kKMax];
+  __shared__ int dcost[4][2 * kKMax];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + w;
+  if (t >= n_tiles) return;  // wave-uniform: nothing below synchronises the block
+  const int nv = (int)(n - t * T < T ? n - t * T : T);
+  for (int p = lane; p < T; p += 64) {  // each lane's own rows (group_rows reads them back on the same lane)
+    uint32_t m = 0;
+    if (p < nv) {
+      const int32_t* col = nbr + t * T + p;
+#pragma unroll 9
+      for (int o = 0; o < K; ++o) m |= (uint32_t)(col[(int64_t)o * n] >= 0) << o;
+    }
+    msk[w][p] = m;
+  }
+  group_rows<T>(msk[w], nv, ord[w], gmask[w]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's ord / gmask stores before the other lanes read
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (T == 128 && wave_off && K <= kKMax) deal_offsets(gmask[w], K, ditem[w], dcost[w], wave_off + t * 64);
+  for (int i = lane; i < T; i += 64) perm[t * T + i] = i < nv ? (int32_t)(t * T + ord[w][i]) : -1;
+}
+
+// MODE 0: the distinct-row lists only (the chunk-local weight gradient needs no row order; the block keeps to the
+// 32 KB of the hash set and the list).  MODE 1: also the row order and offset lists, grouped inside the block by
+// its first wave (few tiles: one kernel's latency), and the local indices.  MODE 2: the local indices in the order
+// local_group_kernel wrote to perm (many tiles: that kernel keeps many tiles' grouping chains in flight).
+template <int T, int N2, int MODE>
 __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
                                                          int64_t n_pad, const int64_t* __restrict__ u_start,
                                                          int32_t* __restrict__ u_rows, uint16_t* __restrict__ lidx,
                                                          int32_t* __restrict__ perm, uint8_t* __restrict__ wave_off) {
-  __shared__ int32_t h[MSP_LOCAL_HASH_MULT * N2];
+  constexpr int HS = MSP_LOCAL_HASH_MULT * N2;
+  __shared__ int32_t h[HS];
   __shared__ int32_t uq[N2];
-  __shared__ uint32_t msk[T];
-  __shared__ uint8_t ord[T];
-  __shared__ uint32_t gmask[T / 16];
-  __shared__ uint8_t ditem[2][kKMax];
-  __shared__ int dcost[2][kKMax];
+  __shared__ uint8_t iord[MODE ? T : 1];  // where tile row p goes in the chosen order
+  __shared__ uint32_t msk[MODE == 1 ? T : 1];
+  __shared__ uint8_t ord[MODE == 1 ? T : 1];
+  __shared__ uint32_t gmask[MODE == 1 ? T / 16 : 1];
+  __shared__ uint8_t ditem[MODE == 1 ? 2 * kKMax : 1];
+  __shared__ int dcost[MODE == 1 ? 2 * kKMax : 1];
   __shared__ int c;
   const int64_t t = blockIdx.x;
-  const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c);
+  int32_t m[N2 / kLT];
+  const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c, m, MODE == 1 ? msk : nullptr);
   // the distinct rows in ascending order
   int n2 = 2;
   while (n2 < tot) n2 <<= 1;
@@ -274,36 +354,54 @@ __global__ __launch_bounds__(kLT) void local_fill_kernel(const int32_t* __restri
   bitonic_i32_n(uq, n2);
   const int64_t u0 = u_start[t];
   for (int i = threadIdx.x; i < tot; i += kLT) u_rows[u0 + i] = uq[i];
-  if (lidx == nullptr) return;  // lists only (the chunk-local weight gradient needs no row order)
-  // rows of the tile grouped by shared offsets (padding rows last)
-  const int nv = (int)(n - t * T < T ? n - t * T : T);
-  for (int p = threadIdx.x; p < T; p += kLT) {
-    uint32_t m = 0;
-    if (p < nv)
-      for (int o = 0; o < K; ++o) m |= (uint32_t)(nbr[(int64_t)o * n + t * T + p] >= 0) << o;
-    msk[p] = m;
+  if constexpr (MODE == 0) return;
+  // each distinct row's slot now holds the row's sorted position (slots found first, then rewritten: a probe
+  // compares uq[h[slot]] with the row from here on)
+  {
+    int sl[N2 / kLT];
+#pragma unroll
+    for (int j = 0; j < N2 / kLT; ++j) {
+      const int i = threadIdx.x + kLT * j;
+      sl[j] = i < tot ? hash_slot<HS>(h, uq[i]) : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < N2 / kLT; ++j)
+      if (sl[j] >= 0) h[sl[j]] = threadIdx.x + kLT * j;
+  }
+  if constexpr (MODE == 1) {  // rows grouped by shared offsets (padding rows last); msk was set by tile_distinct
+    const int nv = (int)(n - t * T < T ? n - t * T : T);
+    if (threadIdx.x < 64) group_rows<T>(msk, nv, ord, gmask);
+    __syncthreads();
+    if (T == 128 && wave_off && K <= kKMax && threadIdx.x < 64) deal_offsets(gmask, K, ditem, dcost, wave_off + t * 64);
+    for (int i = threadIdx.x; i < T; i += kLT) {
+      perm[t * T + i] = i < nv ? (int32_t)(t * T + ord[i]) : -1;
+      iord[ord[i]] = (uint8_t)i;
+    }
+  } else {
+    for (int i = threadIdx.x; i < T; i += kLT) {  // perm: local_group_kernel's row order (padding last, in place)
+      const int32_t r = perm[t * T + i];
+      iord[r >= 0 ? (int)(r - t * T) : i] = (uint8_t)i;
+    }
   }
   __syncthreads();
-  if (threadIdx.x < 64) group_rows<T>(msk, nv, ord, gmask);
-  __syncthreads();
-  if (T == 128 && wave_off && K <= kKMax && threadIdx.x < 2)
-    deal_offsets(gmask, K, threadIdx.x, ditem[threadIdx.x], dcost[threadIdx.x], wave_off + (t * 2 + threadIdx.x) * 32);
-  for (int i = threadIdx.x; i < T; i += kLT) perm[t * T + i] = i < nv ? (int32_t)(t * T + ord[i]) : -1;
-  // local index of every (offset, ordered row): binary search in the distinct list
-  for (int idx = threadIdx.x; idx < K * T; idx += kLT) {
-    const int o = idx / T, i = idx - o * T;
-    const int32_t v = i < nv ? nbr[(int64_t)o * n + t * T + ord[i]] : -1;
-    uint16_t li = kAbsent;
-    if (v >= 0) {
-      int lo = 0, hi = tot;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (uq[mid] < v) lo = mid + 1;
-        else hi = mid;
+  // local index of every (offset, row) entry this thread holds, written at the row's ordered position
+#pragma unroll
+  for (int j = 0; j < N2 / kLT; ++j) {
+    const int i = threadIdx.x + kLT * j;
+    if (i < K * T) {
+      const int o = i / T, p = i - o * T;
+      const int32_t v = m[j];
+      uint16_t li = kAbsent;
+      if (v >= 0) {
+        constexpr int HB = __builtin_ctz(HS);
+        uint32_t q = ((uint32_t)v * 2654435761u) >> (32 - HB);
+        int pos;
+        while (uq[pos = h[q]] != v) q = (q + 1) & (HS - 1);  // the probe path of v holds only inserted rows
+        li = (uint16_t)pos;
       }
-      li = (uint16_t)lo;
+      lidx[(int64_t)o * n_pad + t * T + iord[p]] = li;
     }
-    lidx[(int64_t)o * n_pad + t * T + i] = li;
   }
 }
 
@@ -1093,6 +1191,11 @@ size_t msp_tile_local_workspace_size(int64_t n, int tile_rows) {
   return (size_t)(n_tiles + 1) * sizeof(int64_t) + scan_ws_bytes(n_tiles);
 }
 
+// From this many tiles on, the row grouping runs in its own one-wave-per-tile kernel (MODE 2 above); below, inside
+// the fill (MODE 1).  scripts/build_bench.py, headline batch: L1 (4307 tiles) 284 vs 347 us, L2 (1140) 155 vs 164,
+// L3 (277) 134 vs 109, L4 (66) 132 vs 108 (count + fill + one host read).
+constexpr int64_t kGroupSplitTiles = 1024;
+
 int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t* u_start, int32_t* u_rows,
                    int64_t u_cap, uint16_t* lidx, int32_t* perm, uint8_t* wave_off, void* ws, size_t ws_bytes,
                    msp_stream_t stream) {
@@ -1122,15 +1225,24 @@ int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t*
     if (rc) return rc;
   } else {
     MSP_REQUIRE(u_rows && (lidx == nullptr) == (perm == nullptr), "msp_tile_local: NULL output");
-    if (tile_rows == 64)
-      local_fill_kernel<64, 2048><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm,
-                                                        wave_off);
-    else if (tile_rows == 128)
-      local_fill_kernel<128, 4096><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm,
-                                                        wave_off);
-    else
-      local_fill_kernel<256, 8192><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm,
-                                                        wave_off);
+#define LF(T_, N2_)                                                                                              \
+  if (lidx && n_tiles >= kGroupSplitTiles) {                                                                     \
+    local_group_kernel<T_><<<(unsigned)ceil_div(n_tiles, 4), 256, 0, s>>>(nbr, K, n, n_tiles, perm, wave_off);   \
+    local_fill_kernel<T_, N2_, 2><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm, wave_off);  \
+  } else if (lidx) {                                                                                             \
+    local_fill_kernel<T_, N2_, 1><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, lidx, perm, wave_off);  \
+  } else {                                                                                                       \
+    local_fill_kernel<T_, N2_, 0><<<grid, kLT, 0, s>>>(nbr, K, n, n_pad, u_start, u_rows, nullptr, nullptr,       \
+                                                       nullptr);                                                \
+  }
+    if (tile_rows == 64) {
+      LF(64, 2048)
+    } else if (tile_rows == 128) {
+      LF(128, 4096)
+    } else {
+      LF(256, 8192)
+    }
+#undef LF
   }
   return check_launch("msp_tile_local");
 }
