@@ -97,6 +97,30 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const int64_t*
   }
 }
 
+// n <= kScanTile: the whole scan and its total in one launch (most of a metadata build's scans are this small:
+// per-tile or per-offset counts of the smaller levels; three dependent launches were ~10 us each on the side
+// stream)
+__global__ __launch_bounds__(kScanThreads) void scan_one_kernel(const int64_t* __restrict__ in, int64_t n,
+                                                                int64_t* __restrict__ out, int64_t* __restrict__ total) {
+  int64_t v[kScanItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = (int64_t)threadIdx.x * kScanItems + k;
+    v[k] = (i < n) ? in[i] : 0;
+    s += v[k];
+  }
+  int64_t tot;
+  int64_t ex = block_excl_scan<kScanThreads>(s, &tot);
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int64_t i = (int64_t)threadIdx.x * kScanItems + k;
+    if (i < n) out[i] = ex;
+    ex += v[k];
+  }
+  if (threadIdx.x == 0 && total) *total = tot;
+}
+
 size_t scan_ws_bytes(int64_t n) { return (size_t)(ceil_div(n, kScanTile) + 1) * sizeof(int64_t); }
 
 int scan_exclusive_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* total, void* ws, size_t ws_bytes,
@@ -109,6 +133,10 @@ int scan_exclusive_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tota
   if (nb == 0) {
     if (total) MSP_HIP(hipMemsetAsync(total, 0, sizeof(int64_t), s), "scan: memset");
     return MSP_OK;
+  }
+  if (nb == 1) {
+    scan_one_kernel<<<1, kScanThreads, 0, s>>>(in, n, out, total);
+    return check_launch("scan_exclusive_i64");
   }
   scan_reduce_kernel<<<nb, kScanThreads, 0, s>>>(in, n, sums);
   scan_blocks_kernel<<<1, kScanThreads, 0, s>>>(sums, nb, total);

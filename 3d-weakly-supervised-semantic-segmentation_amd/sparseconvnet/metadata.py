@@ -240,15 +240,25 @@ class PairLists:
         # 16-pair chunks per offset (msp_conv_pairs): the starts computed on the device from off_start (a
         # host-to-device copy from pageable memory would wait for a copy kernel that queues beside the step)
         self.n_chunks = sum((c + CHUNK - 1) // CHUNK for c in self.counts)
+
+    def _chunk_starts(self):
+        """16-pair chunk starts per offset (msp_conv_pairs / the pair-list weight gradient), computed on the
+        device from off_start (a host-to-device copy from pageable memory would wait for a copy kernel that
+        queues beside the step) when the lists are filled -- five small kernels that most levels, whose
+        convolutions and weight gradients take the tile-local and chunk forms, never need."""
         cs = torch.zeros(self.K + 1, dtype=torch.int64, device=self._dev)
         torch.cumsum(torch.div(self.off_start.diff() + (CHUNK - 1), CHUNK, rounding_mode="floor"), 0, out=cs[1:])
         self.chunk_start = cs
+        return cs
 
     def __getattr__(self, name):
         # a count still queued in the replay in progress: read it now
         if name in ("total", "counts", "n_chunks", "chunk_start") and _defer() is not None:
             _defer().flush()
-            return object.__getattribute__(self, name)
+            if name in self.__dict__:
+                return self.__dict__[name]
+        if name == "chunk_start" and "total" in self.__dict__:
+            return self._chunk_starts()
         raise AttributeError(name)
 
     def fill(self):
@@ -264,6 +274,8 @@ class PairLists:
                 call("msp_pair_lists", ptr(self._m), self.K, self._n, ptr(pin), ptr(pout), self.total,
                      ptr(self.off_start), ptr(self._ws), self._ws.numel(), _lib.stream(self._dev))
             self._pin, self._pout = pin, pout
+            if "chunk_start" not in self.__dict__:
+                self._chunk_starts()
         return self
 
     @property
