@@ -101,7 +101,7 @@ __host__ __device__ inline void split_key(uint64_t key, int log2s, int64_t& b, i
   z = (int64_t)compact1by2(mort);
 }
 
-// Open-addressing hash (linear probing) used for neighbour queries.
+// Open-addressing hash (linear probing) of the neighbour queries (msp_meta.hip: block_slot / block_find).
 constexpr uint64_t kEmptyKey = ~0ull;
 __host__ __device__ inline uint64_t hash_key(uint64_t k) {
   k ^= k >> 33;
@@ -110,17 +110,6 @@ __host__ __device__ inline uint64_t hash_key(uint64_t k) {
   k *= 0xc4ceb9fe1a85ec53ull;
   k ^= k >> 33;
   return k;
-}
-
-// Table slots are 16 bytes {key, value}: a probe is one load of one line.
-__device__ inline int32_t hash_find(const uint64_t* __restrict__ table, uint64_t mask, uint64_t key) {
-  uint64_t h = hash_key(key) & mask;
-  for (;;) {
-    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * h);
-    if (e.x == key) return (int32_t)e.y;
-    if (e.x == kEmptyKey) return -1;
-    h = (h + 1) & mask;
-  }
 }
 
 // wave64 helpers

@@ -129,51 +129,86 @@ __global__ __launch_bounds__(kThreads) void seg_apply_kernel(
 }
 
 // ---------------------------------------------------------------- hash grid
+// Block hash of a level's sorted keys (msp_hash_build / msp_subm_map): one slot per occupied block of 32
+// consecutive Morton codes (2 x 4 x 4 sites), {key >> 5, first row << 32 | occupancy mask}.  The keys being
+// sorted, a block's rows are contiguous, so row(key) = first + popc(mask below key's code): one 16-byte load
+// answers every site of the block.  The slot is the block key's low bits (Morton-adjacent blocks share cache
+// lines, a wave's 64 rows look up a handful of lines) plus a mix of the bits above the table size (batch, far
+// regions), so scenes land apart.  Round 1-4 hashed every site with a mixing hash into a table of 2n random
+// slots and wrote the map's mirror half by scatter after a memset of all K n entries.
+constexpr int kBlockBits = 5;
+#ifndef MSP_BLOCK_SLOT_LOCAL  // experiments: 1 = the slot is the block key's low bits (+ a mix of the rest)
+#define MSP_BLOCK_SLOT_LOCAL 0
+#endif
+__device__ __forceinline__ uint64_t block_slot(uint64_t bk, uint64_t mask) {
+  if (MSP_BLOCK_SLOT_LOCAL) return (bk + hash_key(bk >> __popcll(mask))) & mask;
+  return hash_key(bk) & mask;
+}
+
 __global__ __launch_bounds__(kThreads) void hash_build_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                               uint64_t* __restrict__ table, uint64_t mask) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
-  const uint64_t key = keys[i];
-  uint64_t h = hash_key(key) & mask;
+  const uint64_t bk = keys[i] >> kBlockBits;
+  if (i > 0 && (keys[i - 1] >> kBlockBits) == bk) return;  // not the block's first row
+  uint32_t occ = 0;
+#pragma unroll 8
+  for (int k = 0; k < (1 << kBlockBits); ++k) {  // the block's rows are keys[i .. i + 32) with the same block key
+    if (i + k >= n) break;
+    const uint64_t key = keys[i + k];
+    if ((key >> kBlockBits) != bk) break;
+    occ |= 1u << (key & ((1u << kBlockBits) - 1));
+  }
+  uint64_t h = block_slot(bk, mask);
   for (;;) {
     const unsigned long long prev =
-        atomicCAS((unsigned long long*)&table[2 * h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+        atomicCAS((unsigned long long*)&table[2 * h], (unsigned long long)kEmptyKey, (unsigned long long)bk);
     if (prev == kEmptyKey) {
-      table[2 * h + 1] = (uint64_t)i;
+      table[2 * h + 1] = ((uint64_t)i << 32) | occ;
       return;
     }
     h = (h + 1) & mask;
   }
 }
 
-// One thread per (site, offset) of the first half of the filter box plus the
-// centre: the neighbour relation is symmetric (j = nbr[o][i] <=> i =
-// nbr[K-1-o][j]), so each found pair also fills its mirror entry and only
-// half the hash probes are made.  nbr must be pre-filled with -1; every
-// entry is written at most once (no races, deterministic).
+__device__ __forceinline__ int32_t block_find(const uint64_t* __restrict__ table, uint64_t mask, uint64_t key) {
+  const uint64_t bk = key >> kBlockBits;
+  uint64_t h = block_slot(bk, mask);
+  for (;;) {
+    const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * h);
+    if (e.x == bk) {
+      const uint32_t occ = (uint32_t)e.y, c = (uint32_t)(key & ((1u << kBlockBits) - 1));
+      if (!((occ >> c) & 1u)) return -1;
+      return (int32_t)(e.y >> 32) + __popc(occ & ((1u << c) - 1u));
+    }
+    if (e.x == kEmptyKey) return -1;
+    h = (h + 1) & mask;
+  }
+}
+
+// Every entry of nbr[K][n] written (no memset): thread (o, i), i fastest, so a wave's rows are Morton-adjacent
+// and their lookups at one offset share the few block slots they touch.
 __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                             int log2s, int64_t size, int f,
                                                             const uint64_t* __restrict__ table, uint64_t mask,
                                                             int32_t* __restrict__ nbr) {
   const int K = f * f * f, centre = (K - 1) / 2;
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (e >= n * (centre + 1)) return;
+  if (e >= n * K) return;
   const int o = (int)(e / n);
   const int64_t i = e - (int64_t)o * n;
+  int32_t j = -1;
   if (o == centre) {
-    nbr[(int64_t)o * n + i] = (int32_t)i;
-    return;
+    j = (int32_t)i;
+  } else {
+    int64_t b, x, y, z;
+    split_key(keys[i], log2s, b, x, y, z);
+    const int h = f / 2;
+    const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
+    if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size)
+      j = block_find(table, mask, make_key(b, xx, yy, zz, log2s));
   }
-  int64_t b, x, y, z;
-  split_key(keys[i], log2s, b, x, y, z);
-  const int h = f / 2;
-  const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
-  if (xx < 0 || yy < 0 || zz < 0 || xx >= size || yy >= size || zz >= size) return;
-  const int32_t j = hash_find(table, mask, make_key(b, xx, yy, zz, log2s));
-  if (j >= 0) {
-    nbr[(int64_t)o * n + i] = j;
-    nbr[(int64_t)(K - 1 - o) * n + j] = (int32_t)i;
-  }
+  nbr[e] = j;
 }
 
 __global__ __launch_bounds__(kThreads) void down_map_kernel(const uint64_t* __restrict__ keys, int64_t n_fine,
@@ -522,9 +557,8 @@ int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial
   if (n == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
   const int K = filter_size * filter_size * filter_size;
-  MSP_HIP(hipMemsetAsync(nbr, 0xFF, (size_t)K * n * sizeof(int32_t), s), "msp_subm_map");
-  subm_map_kernel<<<grid1(n * ((K - 1) / 2 + 1)), kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size,
-                                                                     table, (uint64_t)(cap - 1), nbr);
+  subm_map_kernel<<<grid1(n * K), kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table,
+                                                    (uint64_t)(cap - 1), nbr);
   return check_launch("msp_subm_map");
 }
 

@@ -94,11 +94,14 @@ int msp_segment(const uint64_t* sorted_keys, int64_t n, int shift, const int32_t
 /* ---------------- metadata: hash grid + rulebooks (replaces SCN Metadata's
  * submanifold / strided rulebooks) ----------------- */
 int64_t msp_hash_capacity(int64_t n);
-/* Open-addressing table of cap 16-byte slots {uint64 key, uint64 value}
- * (table = 2*cap uint64, one probe = one load); it must be pre-filled with
- * 0xFF bytes (empty); keys unique. */
+/* Block hash of a level's keys: open-addressing table of cap 16-byte slots
+ * (table = 2*cap uint64, one probe = one load), one slot per occupied block of
+ * 32 consecutive Morton codes: {key >> 5, (first row << 32) | occupancy mask}.
+ * It must be pre-filled with 0xFF bytes (empty); keys unique and sorted
+ * ascending (a level's keys are), so a block's rows are contiguous. */
 int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap, msp_stream_t stream);
-/* Submanifold neighbour map nbr[K][n], K = filter_size^3 (odd filter_size). */
+/* Submanifold neighbour map nbr[K][n], K = filter_size^3 (odd filter_size),
+ * every entry written (-1: no neighbour); table / cap from msp_hash_build. */
 int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
                  const uint64_t* table, int64_t cap, int32_t* nbr, msp_stream_t stream);
 /* Strided (size == stride == 2^log2_stride) child map: down[K][n_coarse],

@@ -49,6 +49,20 @@ def main():
         rules = lvl.subm_rules(3)
         n = lvl.n
         row = [f"L{L} V={n:8d}"]
+
+        def hash_and_map():
+            lvl._hash = None
+            table, cap = lvl.hash()
+            nbr = torch.empty((27, max(n, 1)), dtype=torch.int32, device=DEV)
+            _lib.call("msp_subm_map", _lib.ptr(lvl.keys), n, lvl.log2, lvl.size, 3, _lib.ptr(table), cap,
+                      _lib.ptr(nbr), s)
+            return nbr
+        ms = timeit(hash_and_map)
+        tot["hash+map"] = tot.get("hash+map", 0.0) + ms
+        nbr = hash_and_map()
+        w = torch.arange(nbr.numel(), device=DEV, dtype=torch.int64) % 1000003 + 1
+        row.append(f"hash+map {1e3 * ms:7.1f}us (map checksum {int((nbr.reshape(-1).long() * w).sum())}, "
+                   f"same as the level's rules: {bool(torch.equal(nbr, rules.nbr))})")
         for name, lists_only in (("local", False), ("lists", True)):
             ms = timeit(lambda: metadata.local_rulebook(rules.nbr, 27, n, rules.nbr.device, s, 128,
                                                         lists_only=lists_only))
