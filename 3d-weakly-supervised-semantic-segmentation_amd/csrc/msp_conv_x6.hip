@@ -1189,10 +1189,17 @@ extern "C" {
 
 // Dense row-group form on the large levels with c_out >= 64 (measured against msp_conv_tile on the headline
 // batch, profiles/r01/kbench_nbr_r01v.log: L0 32->64 -13 %, L1 64->64 -3 %, L2 96->96 -9 %, 192->96 -6 %; the
-// narrow per-wave form stays ahead for c_out = 32 and the shared tile below 10^5 rows).
+// narrow per-wave form stays ahead for c_out = 32 and the shared tile below 10^5 rows).  Off since round 5: its
+// only remaining call (level 0's 32 -> 64 backward-data; levels 1-4 take the tile-local form) needs the map's
+// dense row order, ~0.4 ms of side-stream build per step (a 5-pass radix sort and a permuted copy of the 27 x V
+// map), and the per-wave tiles, whose rulebook level 0 builds anyway, now run the call as fast: 50.35-50.42 vs
+// 50.43-50.52 ms/step (profiles/r05/ab_r05ag_no_nbr.log).  The kernel stays (msp_conv_nbr, tested directly).
+#ifndef MSP_NBR_FORM  // experiments: 1 = the round-1..4 routing above
+#define MSP_NBR_FORM 0
+#endif
 int msp_conv_nbr_preferred(int64_t n_rows, int c_in, int c_out) {
   (void)c_in;
-  return n_rows >= 100000 && c_out >= 64 && c_out % 16 == 0 ? 1 : 0;
+  return MSP_NBR_FORM && n_rows >= 100000 && c_out >= 64 && c_out % 16 == 0 ? 1 : 0;
 }
 
 size_t msp_conv_nbr_workspace_size(int K, int c_in, int c_out) {

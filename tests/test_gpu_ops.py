@@ -415,18 +415,19 @@ def test_conv_nbr_accuracy(cin, cout, flip):
     assert torch.equal(y, yp)
 
 
-def test_subm_conv_large_level_uses_nbr_form():
-    """A level above the dense-form threshold (>= 10^5 rows) with 32 -> 64 channels (level 0's decoder shape,
-    below the tile-local form's 64 input channels) runs the module forward through msp_conv_nbr (the recorded
-    kind says so) and the backward-data 64 -> 32 through the per-wave tiles; output, input gradient and weight
-    gradient match an fp64 evaluation from the neighbour map (1e-5 of scale)."""
-    from sparseconvnet import _lib
+def test_subm_conv_large_level_32_to_64():
+    """A level above 10^5 rows with 32 -> 64 channels (level 0's decoder shape, below the tile-local form's 64 input
+    channels) runs the module forward and the backward-data 64 -> 32 through the tile rulebook (the dense
+    row-group form is off since round 5: msp_conv_nbr_preferred is 0), and msp_conv_nbr called directly on the
+    map's dense row order gives the same output: output, input gradient and weight gradient match an fp64
+    evaluation from the neighbour map (1e-5 of scale)."""
+    from sparseconvnet import _lib, ops
     b = make_batch(1, 50, seed=5)
     coords = torch.from_numpy(b["coords"]).to(DEV)
     feats = torch.from_numpy(b["feats"]).to(DEV)
     t = scn.InputLayer(3, 4096, mode=4)([coords, feats])
     V = t.features.size(0)
-    assert V >= 100000 and int(_lib.query("msp_conv_nbr_preferred", _lib.I64(V), 32, 64))
+    assert V >= 100000 and not int(_lib.query("msp_conv_nbr_preferred", _lib.I64(V), 32, 64))
     assert not int(_lib.query("msp_conv_local_preferred", _lib.I64(V), 32, 64))
     torch.manual_seed(3)
     x = torch.randn(V, 32, device=DEV, requires_grad=True)
@@ -448,8 +449,13 @@ def test_subm_conv_large_level_uses_nbr_form():
         y.backward(gy)
     finally:
         _lib.set_recorder(None)
-    assert "subm_fwd/x6g" in rec.kinds, rec.kinds
-    nb = t.metadata.level(4096).subm_rules(3).nbr.long()
+    # 32 -> 64 on the shared 128-row tiles, 64 -> 32 on the per-wave tiles (msp_conv_tile_form)
+    assert "subm_fwd/x6d" in rec.kinds and "subm_bwd_data/x6r" in rec.kinds, rec.kinds
+    rules = t.metadata.level(4096).subm_rules(3)
+    perm, nbp = rules.dense_order()
+    y_nbr = ops.conv_nbr(x.detach(), conv.weight.detach().reshape(27, 32, 64).contiguous(), 27, 2, 64, nbp, V,
+                         perm=perm)
+    nb = rules.nbr.long()
     w = conv.weight.detach().double().reshape(27, 32, 64)  # [K][c_in][c_out]
     x64 = torch.cat([x.detach().double(), torch.zeros(1, 32, dtype=torch.float64, device=DEV)])
     ref = torch.zeros(V, 64, dtype=torch.float64, device=DEV)
@@ -461,7 +467,8 @@ def test_subm_conv_large_level_uses_nbr_form():
         ref += x64[src] @ w[o]
         dx.index_add_(0, src, g64 @ w[o].t())
         dw[o] = x64[src].t() @ g64
-    close(y, ref, 1e-5, "nbr fwd")
+    close(y, ref, 1e-5, "shared tiles fwd")
+    close(y_nbr, ref, 1e-5, "nbr fwd")
     close(x.grad, dx[:V], 1e-5, "bwd-data")
     close(conv.weight.grad.reshape(27, 32, 64), dw, 1e-5, "dW")
 
