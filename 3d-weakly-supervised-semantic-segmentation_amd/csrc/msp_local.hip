@@ -798,6 +798,94 @@ constexpr int kWTile = 128;
 // Weight-gradient index from the tile-local rulebook (msp_tile_local, 128-row tiles): the tile's sorted
 // distinct input rows are already listed there, so each chunk entry of the 128-row tile rulebook only needs its
 // position in that list (binary search; rows past the list's staged capacity are excluded on the host).
+// The chunk weight gradient's index straight from the full tile-local rulebook (msp_local_chunk_index, round 5):
+// per 128-row tile and offset, the present entries of lidx (in natural row order) compacted into 16-entry
+// chunks, offsets ascending, chunk_lr = local position | natural row << 16, padding slots (position 0, row 128:
+// the zero dy row).  Where a tile-local convolution built that rulebook anyway (levels 1-4), this replaces the
+// 128-row tile rulebook's two passes over the K x n map and msp_wgrad_chunk_index's binary searches.
+constexpr int kLCE = (kKMax * kWTile + kLT - 1) / kLT;  // lidx entries per thread (entry tid + kLT j)
+__global__ __launch_bounds__(kLT) void lchunk_count_kernel(const uint16_t* __restrict__ lidx, int K, int64_t n_pad,
+                                                           int64_t* __restrict__ cnt,
+                                                           unsigned long long* __restrict__ mx) {
+  __shared__ int cs[kKMax];
+  const int64_t t = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid < kKMax) cs[tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kLCE; ++j) {
+    const int e = tid + kLT * j, o = e >> 7;  // a wave's 64 entries share one offset
+    const bool pres = o < K && lidx[(int64_t)o * n_pad + t * kWTile + (e & 127)] != kAbsent;
+    const unsigned long long b = __ballot(pres);
+    if ((tid & 63) == 0 && o < K) atomicAdd(&cs[o], __popcll(b));
+  }
+  __syncthreads();
+  if (tid < 64) {
+    int64_t c = tid < K ? (cs[tid] + MSP_CHUNK - 1) / MSP_CHUNK : 0;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
+    if (tid == 0) {
+      cnt[t] = c;
+      atomicMax(mx, (unsigned long long)c);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kLT) void lchunk_fill_kernel(const uint16_t* __restrict__ lidx,
+                                                          const int32_t* __restrict__ perm, int K, int64_t n_pad,
+                                                          const int64_t* __restrict__ tile_start,
+                                                          uint8_t* __restrict__ chunk_off,
+                                                          uint32_t* __restrict__ chunk_lr) {
+  __shared__ int hc[kKMax][2];  // present entries per (offset, half of the tile's rows)
+  __shared__ int cst[kKMax];    // first chunk of each offset (relative to the tile)
+  __shared__ uint8_t iord[kWTile];  // natural row -> the rulebook's position of it (inverse of perm)
+  const int64_t t = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid < kWTile) {
+    const int32_t r = perm[t * kWTile + tid];
+    iord[r >= 0 ? (int)(r - t * kWTile) : tid] = (uint8_t)tid;
+  }
+  __syncthreads();
+  // entries in natural row order: a chunk's dy rows are then mostly consecutive (the transposing dy reads of
+  // wgrad_x6c; in the rulebook's grouped order they scatter: +0.25 ms/step of wgrad_x6c, ab_r05ak_local_chunk)
+  uint16_t v[kLCE];
+#pragma unroll
+  for (int j = 0; j < kLCE; ++j) {
+    const int e = tid + kLT * j, o = e >> 7;
+    v[j] = o < K ? lidx[(int64_t)o * n_pad + t * kWTile + iord[e & 127]] : kAbsent;
+    const unsigned long long b = __ballot(v[j] != kAbsent);
+    if (lane == 0 && o < K) hc[o][(e >> 6) & 1] = __popcll(b);
+  }
+  __syncthreads();
+  if (tid < 64) {  // chunk starts: exclusive prefix over offsets of ceil(count / 16)
+    const int c = tid < K ? (hc[tid][0] + hc[tid][1] + MSP_CHUNK - 1) / MSP_CHUNK : 0;
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (tid < K) cst[tid] = incl - c;
+  }
+  __syncthreads();
+  const int64_t c0 = tile_start[t];
+#pragma unroll
+  for (int j = 0; j < kLCE; ++j) {
+    const int e = tid + kLT * j, o = e >> 7, i = e & 127;
+    const bool pres = v[j] != kAbsent;
+    const unsigned long long b = __ballot(pres);
+    if (pres) {
+      const int rank = ((e >> 6) & 1 ? hc[o][0] : 0) + __popcll(b & ((1ull << lane) - 1ull));
+      chunk_lr[(c0 + cst[o]) * MSP_CHUNK + rank] = (uint32_t)v[j] | ((uint32_t)i << 16);
+    }
+  }
+  if (tid < K) {  // the offset's chunks: their offset byte and the padding slots of the last one
+    const int c = hc[tid][0] + hc[tid][1], nch = (c + MSP_CHUNK - 1) / MSP_CHUNK;
+    for (int k = 0; k < nch; ++k) chunk_off[c0 + cst[tid] + k] = (uint8_t)tid;
+    for (int r = c; r < nch * MSP_CHUNK; ++r) chunk_lr[(c0 + cst[tid]) * MSP_CHUNK + r] = (uint32_t)kWTile << 16;
+  }
+}
+
 __global__ __launch_bounds__(kLT) void chunk_lidx_kernel(const int64_t* __restrict__ tile_start,
                                                          const int32_t* __restrict__ chunk_src,
                                                          const uint16_t* __restrict__ chunk_row,
@@ -1293,6 +1381,34 @@ int msp_wgrad_chunk_index(const int64_t* tile_start, const int32_t* chunk_src, c
 size_t msp_wgrad_far_workspace_size(int64_t n_far) {
   const int64_t n = n_far > 0 ? n_far : 0;
   return 8 + (size_t)n * 8 + (size_t)((n * 4 + 7) / 8) * 8 + msp_sort_workspace_size(n, kFarShift + 5);
+}
+
+int msp_local_chunk_index(const uint16_t* lidx, const int32_t* perm, int K, int64_t n, int64_t* tile_start,
+                          uint8_t* chunk_off, uint32_t* chunk_lr, int64_t chunk_cap, void* ws, size_t ws_bytes,
+                          msp_stream_t stream) {
+  MSP_REQUIRE(K >= 1 && K <= kKMax && n >= 0 && n < (1ll << 31), "msp_local_chunk_index: K must be in [1, %d]",
+              kKMax);
+  hipStream_t s = as_stream(stream);
+  const int64_t n_tiles = ceil_div(n, kWTile), n_pad = n_tiles * kWTile;
+  const size_t need = msp_tile_local_workspace_size(n, kWTile);
+  MSP_REQUIRE(ws && ws_bytes >= need, "msp_local_chunk_index: workspace too small (%zu < %zu)", ws_bytes, need);
+  if (n_tiles == 0) {
+    if (chunk_cap <= 0) MSP_HIP(hipMemsetAsync(tile_start, 0, 2 * sizeof(int64_t), s), "msp_local_chunk_index");
+    return MSP_OK;
+  }
+  int64_t* cnt = reinterpret_cast<int64_t*>(ws);
+  void* sws = cnt + n_tiles + 1;
+  if (chunk_cap <= 0) {  // counting call: tile_start[0..n_tiles] = exclusive scan, tile_start[n_tiles + 1] = largest
+    MSP_HIP(hipMemsetAsync(tile_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_local_chunk_index");
+    lchunk_count_kernel<<<(unsigned)n_tiles, kLT, 0, s>>>(lidx, K, n_pad, cnt,
+                                                         reinterpret_cast<unsigned long long*>(tile_start + n_tiles + 1));
+    const int rc = scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
+    if (rc) return rc;
+  } else {
+    MSP_REQUIRE(perm && chunk_off && chunk_lr, "msp_local_chunk_index: NULL output");
+    lchunk_fill_kernel<<<(unsigned)n_tiles, kLT, 0, s>>>(lidx, perm, K, n_pad, tile_start, chunk_off, chunk_lr);
+  }
+  return check_launch("msp_local_chunk_index");
 }
 
 int msp_wgrad_far_list(const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,

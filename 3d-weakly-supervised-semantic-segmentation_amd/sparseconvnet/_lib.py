@@ -49,6 +49,7 @@ PROTOTYPES = {
     "msp_wgrad_chunk_ranges": (I64, [I64, I, I]),
     "msp_wgrad_chunk_cap": (I64, []),
     "msp_wgrad_chunk_index": (I, [P, P, P, I64, P, P, P, P, P]),
+    "msp_local_chunk_index": (I, [P, P, I, I64, P, P, P, I64, P, SZ, P]),
     "msp_conv_wgrad_chunk": (I, [P, I, P, I, I, I, P, P, P, P, P, I64, I64, P, P, P]),
     "msp_wgrad_far_workspace_size": (SZ, [I64]),
     "msp_wgrad_far_list": (I, [P, P, P, I64, I64, P, P, P, SZ, P]),

@@ -80,6 +80,11 @@ _TLS = threading.local()  # .defer: this thread's replay in progress (a prefetch
 DEFER_READS = os.environ.get("MSP_DEFER_READS", "1") != "0"
 
 
+# MSP_LOCAL_CHUNK_INDEX=0: the chunk weight gradient's index always from the 128-row tile rulebook (A/B switch;
+# SubmRules._local_chunk_index)
+LOCAL_CHUNK_INDEX = os.environ.get("MSP_LOCAL_CHUNK_INDEX", "1") != "0"
+
+
 # MSP_PINNED_READS=0: count reads as Tensor.cpu() (A/B switch; see _host)
 PINNED_READS = os.environ.get("MSP_PINNED_READS", "1") != "0"
 
@@ -372,6 +377,20 @@ class SubmRules:
                 d.flush()
             if self._wchunk is _PENDING:  # the replay ended without deciding (its flush failed): build it now
                 self._wchunk = None
+        if self._wchunk is None and LOCAL_CHUNK_INDEX:
+            full = self._locals.get(128)
+            if full is not None and "lidx" not in full:  # a replay's counts not read yet: decide once they are
+                self._wchunk = _PENDING
+
+                def decide_full():
+                    self._wchunk = None
+                    self.wgrad_index()
+                _defer().then(decide_full)
+                return self._wchunk
+            if full is not None and full["max_u"] <= int(query("msp_wgrad_chunk_cap")):
+                self._plan.append(("wchunk", self._key))
+                self._wchunk = self._local_chunk_index(full)
+                return self._wchunk
         if self._wchunk is None:
             loc = self.lists()
             tiles = self.tiles_for(128)
@@ -408,6 +427,34 @@ class SubmRules:
                         idx.update(far_key=key, far_tile=tile, far_ws=ws)
                 _later(n_far, far)
         return self._wchunk
+
+    def _local_chunk_index(self, loc):
+        """The chunk weight gradient's index from the full tile-local rulebook (msp_local_chunk_index: count, one
+        host read of the chunk total -- deferred in a replay -- then fill): no 128-row tile rulebook and no
+        binary searches where a tile-local convolution built that rulebook anyway."""
+        dev, s, n = self.nbr.device, _lib.stream(self.nbr.device), self._n
+        n_tiles = (n + 127) // 128
+        tile_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=dev)
+        ws = _ws(query("msp_tile_local_workspace_size", I64(n), 128), dev)
+        call("msp_local_chunk_index", ptr(loc["lidx"]), ptr(loc["perm"]), self.K, n, ptr(tile_start), None, None,
+             0, ptr(ws), ws.numel(), s)
+        tiles = dict(tile_start=tile_start, tile_rows=128)
+        idx = dict(tiles=tiles, u_start=loc["u_start"], u_rows=loc["u_rows"], n_far=0, ws=ws)
+
+        def fill(counts):
+            n_chunks, max_chunks = counts
+            chunk_off = torch.empty(max(n_chunks, 1), dtype=torch.uint8, device=dev)
+            lr = torch.empty(max(n_chunks, 1) * CHUNK, dtype=torch.int32, device=dev)
+            if n_chunks:
+                call("msp_local_chunk_index", ptr(loc["lidx"]), ptr(loc["perm"]), self.K, n, ptr(tile_start),
+                     ptr(chunk_off), ptr(lr), n_chunks, ptr(ws), ws.numel(), s)
+            tiles.update(chunk_off=chunk_off, n_chunks=n_chunks, max_chunks=max_chunks)
+            idx["chunk_lr"] = lr
+        if n_tiles:
+            _later(tile_start[n_tiles:], fill)
+        else:
+            fill((0, 0))
+        return idx
 
     def note_use(self, purpose, c_in, c_out):
         """Record in the plan that a convolution / weight gradient with these channel counts runs over these

@@ -243,6 +243,16 @@ int64_t msp_wgrad_chunk_ranges(int64_t n_rows, int c_in, int c_out);
 int msp_wgrad_chunk_index(const int64_t* tile_start, const int32_t* chunk_src, const uint16_t* chunk_row,
                           int64_t n_rows, const int64_t* u_start, const int32_t* u_rows, uint32_t* chunk_lr,
                           int64_t* n_far, msp_stream_t stream);
+/* The same index (tile_start[n_tiles + 2], chunk_off, chunk_lr as above, tiles of 128 rows) built from a FULL
+ * tile-local rulebook of the map (msp_tile_local with lidx / perm, tile_rows = 128) instead of the tile rulebook:
+ * per tile and offset the present lidx entries, in natural row order, in 16-entry chunks, offsets
+ * ascending; padding slots are (0 | 128 << 16).  Count-then-fill like msp_tile_rulebook (chunk_cap = 0: count,
+ * tile_start[n_tiles] = total chunks, tile_start[n_tiles + 1] = the largest tile's; then fill with chunk_cap >=
+ * total and the same workspace, msp_tile_local_workspace_size(n, 128) bytes).  Every position must be within
+ * msp_wgrad_chunk_cap() (u_start[n_tiles + 1] <= cap): no far rules. */
+int msp_local_chunk_index(const uint16_t* lidx, const int32_t* perm, int K, int64_t n, int64_t* tile_start,
+                          uint8_t* chunk_off, uint32_t* chunk_lr, int64_t chunk_cap, void* ws, size_t ws_bytes,
+                          msp_stream_t stream);
 int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, int K, int tile_rows,
                          const int64_t* tile_start, const uint8_t* chunk_off, const uint32_t* chunk_lr,
                          const int64_t* u_start, const int32_t* u_rows, int64_t n_rows, int64_t n_ranges,

@@ -830,6 +830,45 @@ def test_conv_wgrad_chunk_accuracy(cin, cout):
     assert (dw - dwp).abs().max().item() / scale < 2e-6
 
 
+@pytest.mark.parametrize("cin,cout", [(64, 64), (96, 192)])
+def test_conv_wgrad_chunk_from_local_index(cin, cout):
+    """The chunk weight gradient's index built from the full tile-local rulebook (msp_local_chunk_index: what
+    levels 1-4, whose convolutions take the tile-local form, use since round 5) gives dW within 1e-6 of fp64 and
+    of the index built from the 128-row tile rulebook (msp_wgrad_chunk_index), and no tile rulebook is built."""
+    from sparseconvnet import metadata, ops
+    torch.manual_seed(cin + 7 * cout)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    rules = t.metadata.level(64).subm_rules(3)
+    V = t.metadata.level(64).n
+    rules.local()
+    assert metadata.LOCAL_CHUNK_INDEX
+    idx = rules.wgrad_index(wait=True)
+    assert "chunk_src" not in idx["tiles"] and 128 not in rules._tiles and idx["n_far"] == 0
+    x = torch.randn(V, cin, device=DEV)
+    dy = torch.randn(V, cout, device=DEV)
+    dw = ops.conv_wgrad_chunk(x, dy, rules, 27)
+    nb = rules.nbr.long()
+    ref = torch.empty(27, cin, cout, dtype=torch.float64, device=DEV)
+    for o in range(27):
+        m = nb[o] >= 0
+        ref[o] = x[nb[o][m]].double().t() @ dy[m].double()
+    scale = ref.abs().max().item()
+    err = (dw.double() - ref).abs().max().item() / scale
+    print(f"wgrad_chunk from the local index {cin}x{cout}: max err {err:.2e} of the dW scale")
+    assert err < 1e-6
+    metadata.LOCAL_CHUNK_INDEX = False
+    try:
+        rules._wchunk = None
+        idx_t = rules.wgrad_index(wait=True)
+        assert "chunk_src" in idx_t["tiles"]
+        dw_t = ops.conv_wgrad_chunk(x, dy, rules, 27)
+    finally:
+        metadata.LOCAL_CHUNK_INDEX = True
+    assert idx_t["tiles"]["n_chunks"] == idx["tiles"]["n_chunks"]
+    assert (dw - dw_t).abs().max().item() / scale < 2e-6
+
+
 def test_conv_wgrad_chunk_over_cap_far_rules():
     """A map whose 128-row tiles name more distinct input rows than the chunk weight gradient stages
     (msp_wgrad_chunk_cap, 448): msp_wgrad_chunk_index counts the rules whose row lies past the cap (n_far, ADVICE
