@@ -268,14 +268,24 @@ int msp_conv_tile_rows(int64_t n_rows, int c_in, int c_out) {
   return 128;
 }
 
+// Per-wave tiles (x6r) for narrow outputs, and since round 5 for level 0's 32 -> 64 too (two 32-column passes
+// over the gathers, n_y = 2) instead of the shared tiles (x6d: mfma_busy 0.15 there, 0.83 ms per call): 49.73-49.81
+// vs 50.07-50.11 ms/step (profiles/r05/ab_r05am_x6r_wide.log).  MSP_X6R_WIDE 0: the round-4 choice.
+#ifndef MSP_X6R_WIDE
+#define MSP_X6R_WIDE 1
+#endif
+static bool use_x6r(int64_t n_rows, int c_in, int c_out) {
+  return (c_out <= 32 && c_in <= 64) || (MSP_X6R_WIDE && c_out == 64 && c_in <= 32 && n_rows >= 100000);
+}
+
 int msp_conv_tile_form(int64_t n_rows, int c_in, int c_out, int tile_rows) {
   if (n_rows <= 0 || c_in <= 0 || c_out <= 0 || tile_rows != 128) return 0;
-  return (c_out <= 32 && c_in <= 64) ? 1 : 2;
+  return use_x6r(n_rows, c_in, c_out) ? 1 : 2;
 }
 
 size_t msp_conv_tile_workspace_size(int64_t n_rows, int K, int c_in, int c_out, int tile_rows) {
   if (tile_rows != 128 || n_rows <= 0 || c_out <= 0 || K <= 0) return 0;
-  if (c_out <= 32 && c_in <= 64) return x6p_ws_bytes(K, c_in, c_out);
+  if (use_x6r(n_rows, c_in, c_out)) return x6p_ws_bytes(K, c_in, c_out);
   return x6_ws_bytes(n_rows, K, c_in, c_out, plan_x6(n_rows, c_out));
 }
 
@@ -291,7 +301,7 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
   const int64_t n_tiles = ceil_div(n_rows, tile_rows);
   if (n_tiles == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
-  if (c_out <= 32 && c_in <= 64) {
+  if (use_x6r(n_rows, c_in, c_out)) {
     // narrow outputs: per-wave 128-row tiles, no barriers (msp_conv_x6.hip)
     const size_t need = x6p_ws_bytes(K, c_in, c_out);
     MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_tile: workspace too small (%zu < %zu)", ws_bytes, need);

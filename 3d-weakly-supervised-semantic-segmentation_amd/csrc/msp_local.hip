@@ -1493,7 +1493,7 @@ int msp_conv_weight_image(int entry, int64_t n_rows, int K, int c_in, int c_out,
   d->kind = 1;
   d->units = (int64_t)K * c_out * nks * 12;
   if (entry == 0) {  // msp_conv_tile, 128-row tiles
-    if (c_out <= 32 && c_in <= 64) {
+    if (msp_conv_tile_form(n_rows, c_in, c_out, 128) == 1) {  // per-wave tiles (launch_x6r's NT)
       d->p = 16 * (c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1);
     } else {
       d->p = 16 * plan_x6(n_rows, c_out).nt;
