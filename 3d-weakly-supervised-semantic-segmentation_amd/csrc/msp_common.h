@@ -153,8 +153,9 @@ __device__ inline T block_excl_scan(T v, T* total) {
 
 // Exclusive scan over int64 in device memory, used by every compaction.
 // Workspace: msp_scan_workspace_size(n) bytes.
+// max_out (optional): the largest input (the count passes' largest tile).
 int scan_exclusive_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* total, void* ws, size_t ws_bytes,
-                       hipStream_t s);
+                       hipStream_t s, int64_t* max_out = nullptr);
 size_t scan_ws_bytes(int64_t n);
 // Exclusive scan of a short array in place with one block; total -> *total.
 int scan_small_inplace(int64_t* data, int64_t n, int64_t* total, hipStream_t s);

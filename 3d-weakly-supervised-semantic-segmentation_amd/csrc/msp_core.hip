@@ -45,33 +45,68 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = 8;  // items per thread
 constexpr int kScanTile = kScanThreads * kScanItems;
 
+// Largest value over the block (every thread gets it): wave maxima by shuffles, then the four waves' in LDS.
+__device__ int64_t block_max_i64(int64_t v) {
+  __shared__ int64_t wm[kScanThreads / 64];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const int64_t o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int64_t m = wm[0];
+#pragma unroll
+  for (int w = 1; w < kScanThreads / 64; ++w) m = wm[w] > m ? wm[w] : m;
+  __syncthreads();
+  return m;
+}
+
+// block_max (optional): the block's largest input, for the scan's max_out (round 5: the count passes' largest
+// tile used to need a memset and an atomicMax of their own, ~8 us of side-stream latency per count)
 __global__ __launch_bounds__(kScanThreads) void scan_reduce_kernel(const int64_t* __restrict__ in, int64_t n,
-                                                                   int64_t* __restrict__ block_sums) {
+                                                                   int64_t* __restrict__ block_sums,
+                                                                   int64_t* __restrict__ block_max) {
   const int64_t base = (int64_t)blockIdx.x * kScanTile;
-  int64_t s = 0;
+  int64_t s = 0, mx = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     int64_t i = base + (int64_t)k * kScanThreads + threadIdx.x;
-    if (i < n) s += in[i];
+    if (i < n) {
+      s += in[i];
+      mx = in[i] > mx ? in[i] : mx;
+    }
   }
   int64_t tot;
   block_excl_scan<kScanThreads>(s, &tot);
-  if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+  if (block_max) mx = block_max_i64(mx);
+  if (threadIdx.x == 0) {
+    block_sums[blockIdx.x] = tot;
+    if (block_max) block_max[blockIdx.x] = mx;
+  }
 }
 
-// single block: exclusive scan of the block sums in place, total -> *total
+// single block: exclusive scan of the block sums in place, total -> *total; max_out (optional) = the largest of
+// block_max[0 .. nb)
 __global__ __launch_bounds__(kScanThreads) void scan_blocks_kernel(int64_t* __restrict__ sums, int64_t nb,
-                                                                   int64_t* __restrict__ total) {
-  int64_t carry = 0;
+                                                                   int64_t* __restrict__ total,
+                                                                   const int64_t* __restrict__ block_max,
+                                                                   int64_t* __restrict__ max_out) {
+  int64_t carry = 0, mx = 0;
   for (int64_t base = 0; base < nb; base += kScanThreads) {
     int64_t i = base + threadIdx.x;
     int64_t v = (i < nb) ? sums[i] : 0;
+    if (block_max && i < nb) mx = block_max[i] > mx ? block_max[i] : mx;
     int64_t tot;
     int64_t ex = block_excl_scan<kScanThreads>(v, &tot);
     if (i < nb) sums[i] = carry + ex;
     carry += tot;
   }
-  if (threadIdx.x == 0 && total) *total = carry;
+  if (max_out) mx = block_max_i64(mx);
+  if (threadIdx.x == 0) {
+    if (total) *total = carry;
+    if (max_out) *max_out = mx;
+  }
 }
 
 __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const int64_t* __restrict__ in, int64_t n,
@@ -101,14 +136,20 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const int64_t*
 // per-tile or per-offset counts of the smaller levels; three dependent launches were ~10 us each on the side
 // stream)
 __global__ __launch_bounds__(kScanThreads) void scan_one_kernel(const int64_t* __restrict__ in, int64_t n,
-                                                                int64_t* __restrict__ out, int64_t* __restrict__ total) {
+                                                                int64_t* __restrict__ out, int64_t* __restrict__ total,
+                                                                int64_t* __restrict__ max_out) {
   int64_t v[kScanItems];
-  int64_t s = 0;
+  int64_t s = 0, mx = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     const int64_t i = (int64_t)threadIdx.x * kScanItems + k;
     v[k] = (i < n) ? in[i] : 0;
     s += v[k];
+    mx = v[k] > mx ? v[k] : mx;
+  }
+  if (max_out) {
+    mx = block_max_i64(mx);
+    if (threadIdx.x == 0) *max_out = mx;  // (before the in-place writes below: max_out may alias nothing read)
   }
   int64_t tot;
   int64_t ex = block_excl_scan<kScanThreads>(s, &tot);
@@ -121,31 +162,33 @@ __global__ __launch_bounds__(kScanThreads) void scan_one_kernel(const int64_t* _
   if (threadIdx.x == 0 && total) *total = tot;
 }
 
-size_t scan_ws_bytes(int64_t n) { return (size_t)(ceil_div(n, kScanTile) + 1) * sizeof(int64_t); }
+size_t scan_ws_bytes(int64_t n) { return (size_t)(2 * (ceil_div(n, kScanTile) + 1)) * sizeof(int64_t); }
 
 int scan_exclusive_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* total, void* ws, size_t ws_bytes,
-                       hipStream_t s) {
+                       hipStream_t s, int64_t* max_out) {
   MSP_REQUIRE(n >= 0, "scan: n < 0");
   MSP_REQUIRE(ws_bytes >= scan_ws_bytes(n), "scan: workspace too small (%zu < %zu)", ws_bytes,
               scan_ws_bytes(n));
   const int64_t nb = ceil_div(n, kScanTile);
   int64_t* sums = reinterpret_cast<int64_t*>(ws);
+  int64_t* bmax = max_out ? sums + nb + 1 : nullptr;
   if (nb == 0) {
     if (total) MSP_HIP(hipMemsetAsync(total, 0, sizeof(int64_t), s), "scan: memset");
+    if (max_out) MSP_HIP(hipMemsetAsync(max_out, 0, sizeof(int64_t), s), "scan: memset");
     return MSP_OK;
   }
   if (nb == 1) {
-    scan_one_kernel<<<1, kScanThreads, 0, s>>>(in, n, out, total);
+    scan_one_kernel<<<1, kScanThreads, 0, s>>>(in, n, out, total, max_out);
     return check_launch("scan_exclusive_i64");
   }
-  scan_reduce_kernel<<<nb, kScanThreads, 0, s>>>(in, n, sums);
-  scan_blocks_kernel<<<1, kScanThreads, 0, s>>>(sums, nb, total);
+  scan_reduce_kernel<<<nb, kScanThreads, 0, s>>>(in, n, sums, bmax);
+  scan_blocks_kernel<<<1, kScanThreads, 0, s>>>(sums, nb, total, bmax, max_out);
   scan_apply_kernel<<<nb, kScanThreads, 0, s>>>(in, n, sums, out);
   return check_launch("scan_exclusive_i64");
 }
 
 int scan_small_inplace(int64_t* data, int64_t n, int64_t* total, hipStream_t s) {
-  scan_blocks_kernel<<<1, kScanThreads, 0, s>>>(data, n, total);
+  scan_blocks_kernel<<<1, kScanThreads, 0, s>>>(data, n, total, nullptr, nullptr);
   return check_launch("scan_small_inplace");
 }
 

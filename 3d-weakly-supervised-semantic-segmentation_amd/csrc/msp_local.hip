@@ -150,18 +150,14 @@ __device__ void bitonic_i32_n(int32_t* a, int n2) {
 
 template <int T, int N2>
 __global__ __launch_bounds__(kLT) void local_count_kernel(const int32_t* __restrict__ nbr, int K, int64_t n,
-                                                          int64_t* __restrict__ cnt,
-                                                          unsigned long long* __restrict__ mx) {
+                                                          int64_t* __restrict__ cnt) {
   __shared__ int32_t h[MSP_LOCAL_HASH_MULT * N2];
   __shared__ int32_t uq[N2];
   __shared__ int c;
   const int64_t t = blockIdx.x;
   int32_t m[N2 / kLT];
   const int tot = tile_distinct<T, N2>(nbr, K, n, t, h, uq, &c, m);
-  if (threadIdx.x == 0) {
-    cnt[t] = tot;
-    atomicMax(mx, (unsigned long long)tot);
-  }
+  if (threadIdx.x == 0) cnt[t] = tot;  // (the largest count: the scan's max_out)
 }
 
 // Rows of a tile into 16-row groups that share filter offsets (one wave, T / 64 rows per lane): each group is
@@ -805,8 +801,7 @@ constexpr int kWTile = 128;
 // 128-row tile rulebook's two passes over the K x n map and msp_wgrad_chunk_index's binary searches.
 constexpr int kLCE = (kKMax * kWTile + kLT - 1) / kLT;  // lidx entries per thread (entry tid + kLT j)
 __global__ __launch_bounds__(kLT) void lchunk_count_kernel(const uint16_t* __restrict__ lidx, int K, int64_t n_pad,
-                                                           int64_t* __restrict__ cnt,
-                                                           unsigned long long* __restrict__ mx) {
+                                                           int64_t* __restrict__ cnt) {
   __shared__ int cs[kKMax];
   const int64_t t = blockIdx.x;
   const int tid = threadIdx.x;
@@ -824,10 +819,7 @@ __global__ __launch_bounds__(kLT) void lchunk_count_kernel(const uint16_t* __res
     int64_t c = tid < K ? (cs[tid] + MSP_CHUNK - 1) / MSP_CHUNK : 0;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d, 64);
-    if (tid == 0) {
-      cnt[t] = c;
-      atomicMax(mx, (unsigned long long)c);
-    }
+    if (tid == 0) cnt[t] = c;
   }
 }
 
@@ -1304,12 +1296,11 @@ int msp_tile_local(const int32_t* nbr, int K, int64_t n, int tile_rows, int64_t*
   void* sws = cnt + n_tiles + 1;
   const unsigned grid = (unsigned)n_tiles;
   if (u_cap <= 0) {  // counting call: u_start[0..n_tiles] = exclusive scan, u_start[n_tiles + 1] = largest tile
-    MSP_HIP(hipMemsetAsync(u_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_tile_local");
-    auto* mx = reinterpret_cast<unsigned long long*>(u_start + n_tiles + 1);
-    if (tile_rows == 64) local_count_kernel<64, 2048><<<grid, kLT, 0, s>>>(nbr, K, n, cnt, mx);
-    else if (tile_rows == 128) local_count_kernel<128, 4096><<<grid, kLT, 0, s>>>(nbr, K, n, cnt, mx);
-    else local_count_kernel<256, 8192><<<grid, kLT, 0, s>>>(nbr, K, n, cnt, mx);
-    const int rc = scan_exclusive_i64(cnt, u_start, n_tiles, u_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
+    if (tile_rows == 64) local_count_kernel<64, 2048><<<grid, kLT, 0, s>>>(nbr, K, n, cnt);
+    else if (tile_rows == 128) local_count_kernel<128, 4096><<<grid, kLT, 0, s>>>(nbr, K, n, cnt);
+    else local_count_kernel<256, 8192><<<grid, kLT, 0, s>>>(nbr, K, n, cnt);
+    const int rc = scan_exclusive_i64(cnt, u_start, n_tiles, u_start + n_tiles, sws, scan_ws_bytes(n_tiles), s,
+                                      u_start + n_tiles + 1);
     if (rc) return rc;
   } else {
     MSP_REQUIRE(u_rows && (lidx == nullptr) == (perm == nullptr), "msp_tile_local: NULL output");
@@ -1399,10 +1390,9 @@ int msp_local_chunk_index(const uint16_t* lidx, const int32_t* perm, int K, int6
   int64_t* cnt = reinterpret_cast<int64_t*>(ws);
   void* sws = cnt + n_tiles + 1;
   if (chunk_cap <= 0) {  // counting call: tile_start[0..n_tiles] = exclusive scan, tile_start[n_tiles + 1] = largest
-    MSP_HIP(hipMemsetAsync(tile_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_local_chunk_index");
-    lchunk_count_kernel<<<(unsigned)n_tiles, kLT, 0, s>>>(lidx, K, n_pad, cnt,
-                                                         reinterpret_cast<unsigned long long*>(tile_start + n_tiles + 1));
-    const int rc = scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
+    lchunk_count_kernel<<<(unsigned)n_tiles, kLT, 0, s>>>(lidx, K, n_pad, cnt);
+    const int rc = scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s,
+                                      tile_start + n_tiles + 1);
     if (rc) return rc;
   } else {
     MSP_REQUIRE(perm && chunk_off && chunk_lr, "msp_local_chunk_index: NULL output");

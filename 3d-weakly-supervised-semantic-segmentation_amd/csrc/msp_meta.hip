@@ -129,6 +129,26 @@ __global__ __launch_bounds__(kThreads) void seg_apply_kernel(
 }
 
 // ---------------------------------------------------------------- hash grid
+// Byte fill with 16-byte stores over a grid sized to the chip (hipMemsetAsync's fill of a 64 MB table or a
+// 17 MB map ran at ~0.8 TB/s on the side stream, profiles/r05/prof_r05final).
+__global__ __launch_bounds__(kThreads) void fill16_kernel(uint4* __restrict__ p, int64_t n16, uint4 v) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kThreads) p[i] = v;
+}
+
+static int fill_bytes(void* p, uint8_t value, size_t bytes, hipStream_t s, const char* what) {
+  if (bytes == 0) return MSP_OK;
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0 && (bytes & 15) == 0) {
+    const uint32_t w = 0x01010101u * value;
+    const int64_t n16 = (int64_t)(bytes / 16);
+    const int64_t blocks = ceil_div(n16, kThreads);
+    fill16_kernel<<<(unsigned)(blocks < 4096 ? blocks : 4096), kThreads, 0, s>>>(static_cast<uint4*>(p), n16,
+                                                                                  make_uint4(w, w, w, w));
+    return check_launch(what);
+  }
+  MSP_HIP(hipMemsetAsync(p, value, bytes, s), what);
+  return MSP_OK;
+}
+
 // Block hash of a level's sorted keys (msp_hash_build / msp_subm_map): one slot per occupied block of 32
 // consecutive Morton codes (2 x 4 x 4 sites), {key >> 5, first row << 32 | occupancy mask}.  The keys being
 // sorted, a block's rows are contiguous, so row(key) = first + popc(mask below key's code): one 16-byte load
@@ -290,8 +310,7 @@ constexpr int kChunk = MSP_CHUNK;
 // one barrier; then per-tile sums over the TW waves.  K <= 255.
 template <int TW>
 __global__ __launch_bounds__(kThreads) void tile_count_kernel(const int32_t* __restrict__ map, int K, int64_t n,
-                                                              int64_t n_tiles, int64_t* __restrict__ cnt,
-                                                              int64_t* __restrict__ max_cnt) {
+                                                              int64_t n_tiles, int64_t* __restrict__ cnt) {
   __shared__ uint8_t pc_s[kThreads / 64][256];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = wave % TW;
   const int64_t t = (int64_t)blockIdx.x * (kThreads / 64 / TW) + wave / TW;
@@ -313,10 +332,7 @@ __global__ __launch_bounds__(kThreads) void tile_count_kernel(const int32_t* __r
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) nch += __shfl_xor(nch, d, 64);
-  if (lane == 0) {
-    cnt[t] = nch;
-    atomicMax(reinterpret_cast<unsigned long long*>(max_cnt), (unsigned long long)nch);
-  }
+  if (lane == 0) cnt[t] = nch;  // (the largest: the scan's max_out)
 }
 
 template <int TW>
@@ -544,8 +560,10 @@ int64_t msp_hash_capacity(int64_t n) {
 
 int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap, msp_stream_t stream) {
   MSP_REQUIRE(cap >= 2 * n && (cap & (cap - 1)) == 0, "msp_hash_build: capacity must be a power of 2 >= 2n");
-  if (n == 0) return MSP_OK;
-  hash_build_kernel<<<grid1(n), kThreads, 0, as_stream(stream)>>>(keys, n, table, (uint64_t)(cap - 1));
+  hipStream_t s = as_stream(stream);
+  const int rc = fill_bytes(table, 0xFF, (size_t)cap * 16, s, "msp_hash_build");  // every slot empty
+  if (rc || n == 0) return rc;
+  hash_build_kernel<<<grid1(n), kThreads, 0, s>>>(keys, n, table, (uint64_t)(cap - 1));
   return check_launch("msp_hash_build");
 }
 
@@ -567,7 +585,8 @@ int msp_down_map(const uint64_t* fine_keys, int64_t n_fine, const int32_t* paren
   MSP_REQUIRE(log2_stride >= 1 && log2_stride <= 2, "msp_down_map: stride must be 2 or 4");
   const int K = 1 << (3 * log2_stride);
   hipStream_t s = as_stream(stream);
-  MSP_HIP(hipMemsetAsync(down, 0xFF, (size_t)K * n_coarse * sizeof(int32_t), s), "msp_down_map");
+  const int rc = fill_bytes(down, 0xFF, (size_t)K * n_coarse * sizeof(int32_t), s, "msp_down_map");
+  if (rc) return rc;
   if (n_fine == 0) return MSP_OK;
   down_map_kernel<<<grid1(n_fine), kThreads, 0, s>>>(fine_keys, n_fine, parent_of, log2_size_fine,
                                                      log2_stride, down, n_coarse);
@@ -618,15 +637,13 @@ int msp_tile_rulebook(const int32_t* map, int K, int64_t n, int tile_rows, int64
   const int tw = tile_rows / 64;
   const unsigned g = (unsigned)ceil_div(n_tiles, kThreads / 64 / tw);
   if (chunk_cap <= 0) {  // counting call; the filling call reuses its tile_start
-    MSP_HIP(hipMemsetAsync(tile_start + n_tiles + 1, 0, sizeof(int64_t), s), "msp_tile_rulebook");
-    int64_t* mx = tile_start + n_tiles + 1;
     switch (tw) {
-      case 1: tile_count_kernel<1><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, mx); break;
-      case 2: tile_count_kernel<2><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, mx); break;
-      default: tile_count_kernel<4><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt, mx); break;
+      case 1: tile_count_kernel<1><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt); break;
+      case 2: tile_count_kernel<2><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt); break;
+      default: tile_count_kernel<4><<<g, kThreads, 0, s>>>(map, K, n, n_tiles, cnt); break;
     }
-    const int rc =
-        scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles), s);
+    const int rc = scan_exclusive_i64(cnt, tile_start, n_tiles, tile_start + n_tiles, sws, scan_ws_bytes(n_tiles),
+                                      s, tile_start + n_tiles + 1);
     if (rc) return rc;
   } else {
     switch (tw) {

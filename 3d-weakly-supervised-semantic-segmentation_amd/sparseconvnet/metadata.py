@@ -508,9 +508,8 @@ class Level:
     def hash(self):
         if self._hash is None:
             cap = int(query("msp_hash_capacity", I64(self.n)))
-            table = torch.full((2 * cap,), -1, dtype=torch.int64, device=self.device)  # {key, value} slots
-            if self.n:
-                call("msp_hash_build", ptr(self.keys), self.n, ptr(table), cap, _lib.stream(self.device))
+            table = torch.empty((2 * cap,), dtype=torch.int64, device=self.device)  # {key, value} slots
+            call("msp_hash_build", ptr(self.keys), self.n, ptr(table), cap, _lib.stream(self.device))  # (empties it)
             self._hash = (table, cap)
         return self._hash
 
@@ -584,7 +583,7 @@ class Metadata:
         n_batch = int(max_b) + 1 if n else 0
         monotonic = n_desc == 0
         # one read-back: [voxel count, scene starts of a non-decreasing batch column (msp_batch_starts)]
-        tail = torch.zeros(2 + (n_batch if monotonic else 0), dtype=torch.int64, device=dev)
+        tail = torch.empty(2 + (n_batch if monotonic else 0), dtype=torch.int64, device=dev)  # (all read are written)
         ws = _ws(((n + 2047) // 2048 + 1) * 8, dev)
         call("msp_segment", ptr(skeys), n, 0, ptr(perm), ptr(seg_of), ptr(p2v), ptr(uniq), ptr(vstart), ptr(tail),
              ptr(ws), ws.numel(), s)
@@ -628,7 +627,7 @@ class Metadata:
         parent = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         uniq = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         cstart = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        nu = torch.zeros(1, dtype=torch.int64, device=dev)
+        nu = torch.empty(1, dtype=torch.int64, device=dev)  # (msp_segment writes it)
         ws = _ws(((n + 2047) // 2048 + 1) * 8, dev)
         call("msp_segment", ptr(fine.keys), n, 3 * k, None, ptr(parent), None, ptr(uniq), ptr(cstart), ptr(nu),
              ptr(ws), ws.numel(), s)

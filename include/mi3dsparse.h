@@ -97,8 +97,8 @@ int64_t msp_hash_capacity(int64_t n);
 /* Block hash of a level's keys: open-addressing table of cap 16-byte slots
  * (table = 2*cap uint64, one probe = one load), one slot per occupied block of
  * 32 consecutive Morton codes: {key >> 5, (first row << 32) | occupancy mask}.
- * It must be pre-filled with 0xFF bytes (empty); keys unique and sorted
- * ascending (a level's keys are), so a block's rows are contiguous. */
+ * msp_hash_build empties every slot first (0xFF bytes); keys unique and
+ * sorted ascending (a level's keys are), so a block's rows are contiguous. */
 int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap, msp_stream_t stream);
 /* Submanifold neighbour map nbr[K][n], K = filter_size^3 (odd filter_size),
  * every entry written (-1: no neighbour); table / cap from msp_hash_build. */

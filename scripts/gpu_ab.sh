@@ -3,7 +3,8 @@
 # (B, scripts/build_exp.sh with EXP_FLAGS), ROUNDS times each, alternating; one JSON line per run in
 # gpurun_out/ab_$TAG.log (prefixed A / B).  B_ENV="VAR=value ..." sets environment variables for the B runs
 # only; B_LIB=0 keeps B on the product library (an environment-only A/B); B_ARGS: extra bench.py arguments
-# for the B runs.
+# for the B runs; B_ROOT: run B from another tree (e.g. a previous commit's build staged under ab_prev/, when
+# the change spans the library and its Python side).
 set -o pipefail
 TAG=${TAG:-ab}
 ROUNDS=${ROUNDS:-2}
@@ -18,7 +19,10 @@ for i in $(seq 1 $ROUNDS); do
     envs=""
     extra=""
     [ $v = B ] && envs="${B_ENV:-}" && extra="${B_ARGS:-}"
-    env $envs timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 15 --warmup 5} $extra > gpurun_out/ab_${TAG}_$v$i.log 2>&1 || exit $?
+    root=.
+    [ $v = B ] && [ -n "${B_ROOT:-}" ] && root=$B_ROOT && unset MI3DSPARSE_LIB
+    (cd $root && env $envs timeout -k 10 300 python -u bench.py ${BENCH_ARGS:---steps 15 --warmup 5} $extra) \
+      > gpurun_out/ab_${TAG}_$v$i.log 2>&1 || exit $?
     echo "$v $(grep '^{"metric"' gpurun_out/ab_${TAG}_$v$i.log)" >> gpurun_out/ab_$TAG.log
     python - "$v" gpurun_out/ab_${TAG}_$v$i.log <<'PY'
 import json, sys
