@@ -207,28 +207,60 @@ __device__ __forceinline__ int32_t block_find(const uint64_t* __restrict__ table
 }
 
 // Every entry of nbr[K][n] written (no memset): thread (o, i), i fastest, so a wave's rows are Morton-adjacent
-// and their lookups at one offset share the few block slots they touch.
+// and their lookups at one offset share the few block slots they touch.  part (nullable): the block's count of
+// present entries (msp_subm_map_counted: the rule total without a separate pass over the map).
 __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                             int log2s, int64_t size, int f,
                                                             const uint64_t* __restrict__ table, uint64_t mask,
-                                                            int32_t* __restrict__ nbr) {
+                                                            int32_t* __restrict__ nbr, int32_t* __restrict__ part) {
   const int K = f * f * f, centre = (K - 1) / 2;
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (e >= n * K) return;
-  const int o = (int)(e / n);
-  const int64_t i = e - (int64_t)o * n;
   int32_t j = -1;
-  if (o == centre) {
-    j = (int32_t)i;
-  } else {
-    int64_t b, x, y, z;
-    split_key(keys[i], log2s, b, x, y, z);
-    const int h = f / 2;
-    const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
-    if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size)
-      j = block_find(table, mask, make_key(b, xx, yy, zz, log2s));
+  if (e < n * K) {
+    const int o = (int)(e / n);
+    const int64_t i = e - (int64_t)o * n;
+    if (o == centre) {
+      j = (int32_t)i;
+    } else {
+      int64_t b, x, y, z;
+      split_key(keys[i], log2s, b, x, y, z);
+      const int h = f / 2;
+      const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
+      if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size)
+        j = block_find(table, mask, make_key(b, xx, yy, zz, log2s));
+    }
+    nbr[e] = j;
   }
-  nbr[e] = j;
+  if (part) {
+    __shared__ int wc[kThreads / 64];
+    const int c = __popcll(__ballot(j >= 0));
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+#pragma unroll
+      for (int w = 0; w < kThreads / 64; ++w) t += wc[w];
+      part[blockIdx.x] = t;
+    }
+  }
+}
+
+// *total = the sum of part[0 .. nb) (one block; int64, so the order does not matter)
+__global__ __launch_bounds__(kThreads) void sum_parts_kernel(const int32_t* __restrict__ part, int64_t nb,
+                                                             int64_t* __restrict__ total) {
+  __shared__ int64_t ws[kThreads / 64];
+  int64_t t = 0;
+  for (int64_t i = threadIdx.x; i < nb; i += kThreads) t += part[i];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) s += ws[w];
+    *total = s;
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void down_map_kernel(const uint64_t* __restrict__ keys, int64_t n_fine,
@@ -567,6 +599,33 @@ int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap
   return check_launch("msp_hash_build");
 }
 
+size_t msp_subm_map_workspace_size(int64_t n, int filter_size) {
+  const int64_t K = (int64_t)filter_size * filter_size * filter_size;
+  return (size_t)(ceil_div(n > 0 ? n * K : 1, kThreads)) * sizeof(int32_t);
+}
+
+int msp_subm_map_counted(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
+                         const uint64_t* table, int64_t cap, int32_t* nbr, int64_t* n_rules, void* ws,
+                         size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(filter_size >= 1 && (filter_size & 1) == 1 && filter_size <= 5,
+              "msp_subm_map_counted: filter_size must be odd and <= 5 (got %d)", filter_size);
+  MSP_REQUIRE((cap & (cap - 1)) == 0, "msp_subm_map_counted: bad capacity");
+  MSP_REQUIRE(n_rules && ws && ws_bytes >= msp_subm_map_workspace_size(n, filter_size),
+              "msp_subm_map_counted: NULL count or workspace too small");
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {
+    MSP_HIP(hipMemsetAsync(n_rules, 0, sizeof(int64_t), s), "msp_subm_map_counted");
+    return MSP_OK;
+  }
+  const int K = filter_size * filter_size * filter_size;
+  const unsigned nb = grid1(n * K);
+  int32_t* part = static_cast<int32_t*>(ws);
+  subm_map_kernel<<<nb, kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table, (uint64_t)(cap - 1),
+                                          nbr, part);
+  sum_parts_kernel<<<1, kThreads, 0, s>>>(part, nb, n_rules);
+  return check_launch("msp_subm_map_counted");
+}
+
 int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
                  const uint64_t* table, int64_t cap, int32_t* nbr, msp_stream_t stream) {
   MSP_REQUIRE(filter_size >= 1 && (filter_size & 1) == 1 && filter_size <= 5,
@@ -576,7 +635,7 @@ int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial
   hipStream_t s = as_stream(stream);
   const int K = filter_size * filter_size * filter_size;
   subm_map_kernel<<<grid1(n * K), kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table,
-                                                    (uint64_t)(cap - 1), nbr);
+                                                    (uint64_t)(cap - 1), nbr, nullptr);
   return check_launch("msp_subm_map");
 }
 

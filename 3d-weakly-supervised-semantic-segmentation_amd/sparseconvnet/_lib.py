@@ -37,6 +37,8 @@ PROTOTYPES = {
     "msp_hash_capacity": (I64, [I64]),
     "msp_hash_build": (I, [P, I64, P, I64, P]),
     "msp_subm_map": (I, [P, I64, I, I64, I, P, I64, P, P]),
+    "msp_subm_map_workspace_size": (SZ, [I64, I]),
+    "msp_subm_map_counted": (I, [P, I64, I, I64, I, P, I64, P, P, P, SZ, P]),
     "msp_down_map": (I, [P, I64, P, I, I, P, I64, P]),
     "msp_pair_lists": (I, [P, I, I64, P, P, I64, P, P, SZ, P]),
     "msp_tile_rulebook": (I, [P, I, I64, I, P, P, P, P, I64, P, SZ, P]),

@@ -304,19 +304,37 @@ class SubmRules:
         V = level.n
         table, cap = level.hash()
         self.nbr = torch.empty((K, max(V, 1)), dtype=torch.int32, device=dev)
-        if V:
-            call("msp_subm_map", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(table), cap,
-                 ptr(self.nbr), s)
+        # the rulebook size counted as the map is written (round 5; the pair lists' count pass over the map ran
+        # for every level, though most never fill the lists)
+        self._nr = torch.empty(1, dtype=torch.int64, device=dev)
+        ws = _ws(query("msp_subm_map_workspace_size", I64(V), filter_size), dev)
+        call("msp_subm_map_counted", ptr(level.keys), V, level.log2, level.size, filter_size, ptr(table), cap,
+             ptr(self.nbr), ptr(self._nr), ptr(ws), ws.numel(), s)
         self._tiles = {}
         self._locals = {}
         self._wchunk = None
         self._dense = None
         self._map, self._n = self.nbr, V
-        self.pairs = PairLists(self.nbr, K, V, dev, s, self._plan, self._key)
+        self._pairs = None
+        _later(self._nr, self._counted)
+
+    def _counted(self, vals):
+        self._n_rules = vals[0]
 
     @property
     def n_rules(self):
-        return self.pairs.total  # = SCN rulebook size (centre included)
+        """SCN's rulebook size (centre included); a count still queued in the replay in progress is read now."""
+        if "_n_rules" not in self.__dict__ and _defer() is not None:
+            _defer().flush()
+        return self._n_rules
+
+    @property
+    def pairs(self):
+        """Per-offset pair lists of the map (the pair-list weight gradient), counted on first use."""
+        if self._pairs is None:
+            self._pairs = PairLists(self.nbr, self.K, self._n, self.nbr.device, _lib.stream(self.nbr.device),
+                                    self._plan, self._key)
+        return self._pairs
 
     def dense_order(self):
         """(perm, permuted neighbour map) for the dense row-group convolution

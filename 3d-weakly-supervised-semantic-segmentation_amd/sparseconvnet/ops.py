@@ -318,15 +318,16 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         dx = dw = None
         join = None
         if ctx.needs_input_grad[1]:
-            p = rules.pairs
             V = xp.size(0)
             dwp = None
             rules.note_use("wgrad", cin_p, cout_p)
+            flops = 2.0 * rules.n_rules * cin * cout
             if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(V), K, cin_p, cout_p)) and \
                     rules.wgrad_index(wait=True) is not None:
-                dwp, join = _on_side(xp, V, lambda: conv_wgrad_chunk(xp, g, rules, K, flops=2.0 * p.total * cin * cout))
+                dwp, join = _on_side(xp, V, lambda: conv_wgrad_chunk(xp, g, rules, K, flops=flops))
             if dwp is None:  # pair lists (beside the backward-data on small levels or when WGRAD_CONCURRENT)
-                dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout)
+                p = rules.pairs  # (built by the prefetch when this batch's sizes select them: ops.prepare)
+                dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, flops)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             dxp = conv_tile(g, wp, K, 1, cin_p, rules, xp.size(0), "subm_bwd_data",

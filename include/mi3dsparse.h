@@ -104,6 +104,13 @@ int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap
  * every entry written (-1: no neighbour); table / cap from msp_hash_build. */
 int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
                  const uint64_t* table, int64_t cap, int32_t* nbr, msp_stream_t stream);
+/* msp_subm_map + the number of present entries (the rulebook size, centre
+ * included) into n_rules (device int64), counted as the map is written;
+ * workspace msp_subm_map_workspace_size(n, filter_size) bytes. */
+size_t msp_subm_map_workspace_size(int64_t n, int filter_size);
+int msp_subm_map_counted(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
+                         const uint64_t* table, int64_t cap, int32_t* nbr, int64_t* n_rules, void* ws,
+                         size_t ws_bytes, msp_stream_t stream);
 /* Strided (size == stride == 2^log2_stride) child map: down[K][n_coarse],
  * K = 8^log2_stride, down[o][parent_of[i]] = i for every fine row i. */
 int msp_down_map(const uint64_t* fine_keys, int64_t n_fine, const int32_t* parent_of, int log2_size_fine,

@@ -886,7 +886,8 @@ def test_conv_wgrad_chunk_over_cap_far_rules():
     r.nbr[13] = torch.arange(V, dtype=torch.int32, device=DEV)  # the centre offset
     r._tiles, r._locals, r._wchunk, r._dense = {}, {}, None, None
     r._map, r._n = r.nbr, V
-    r.pairs = metadata.PairLists(r.nbr, K, V, DEV, _lib.stream(), r._plan, r._key)
+    r._pairs = metadata.PairLists(r.nbr, K, V, DEV, _lib.stream(), r._plan, r._key)
+    r._n_rules = int((r.nbr >= 0).sum())
     loc = r.local()
     cap = int(_lib.query("msp_wgrad_chunk_cap"))
     assert loc["max_u"] > cap  # random rows: ~27 x 0.8 x 128 per tile
