@@ -157,6 +157,7 @@ static int fill_bytes(void* p, uint8_t value, size_t bytes, hipStream_t s, const
 // regions), so scenes land apart.  Round 1-4 hashed every site with a mixing hash into a table of 2n random
 // slots and wrote the map's mirror half by scatter after a memset of all K n entries.
 constexpr int kBlockBits = 5;
+constexpr unsigned kMapBlocks = 4096;  // grid cap of the counted submanifold map
 #ifndef MSP_BLOCK_SLOT_LOCAL  // experiments: 1 = the slot is the block key's low bits (+ a mix of the rest)
 #define MSP_BLOCK_SLOT_LOCAL 0
 #endif
@@ -214,26 +215,30 @@ __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __re
                                                             const uint64_t* __restrict__ table, uint64_t mask,
                                                             int32_t* __restrict__ nbr, int32_t* __restrict__ part) {
   const int K = f * f * f, centre = (K - 1) / 2;
-  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  int32_t j = -1;
-  if (e < n * K) {
-    const int o = (int)(e / n);
-    const int64_t i = e - (int64_t)o * n;
-    if (o == centre) {
-      j = (int32_t)i;
-    } else {
-      int64_t b, x, y, z;
-      split_key(keys[i], log2s, b, x, y, z);
-      const int h = f / 2;
-      const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
-      if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size)
-        j = block_find(table, mask, make_key(b, xx, yy, zz, log2s));
+  int c = 0;  // present entries this wave wrote (lane 0's count; part only)
+  // grid-stride (at most kMapBlocks blocks), so the per-block counts stay few enough for one summing block
+  for (int64_t e0 = (int64_t)blockIdx.x * kThreads; e0 < n * K; e0 += (int64_t)gridDim.x * kThreads) {
+    const int64_t e = e0 + threadIdx.x;
+    int32_t j = -1;
+    if (e < n * K) {
+      const int o = (int)(e / n);
+      const int64_t i = e - (int64_t)o * n;
+      if (o == centre) {
+        j = (int32_t)i;
+      } else {
+        int64_t b, x, y, z;
+        split_key(keys[i], log2s, b, x, y, z);
+        const int h = f / 2;
+        const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
+        if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size)
+          j = block_find(table, mask, make_key(b, xx, yy, zz, log2s));
+      }
+      nbr[e] = j;
     }
-    nbr[e] = j;
+    if (part) c += __popcll(__ballot(j >= 0));
   }
   if (part) {
     __shared__ int wc[kThreads / 64];
-    const int c = __popcll(__ballot(j >= 0));
     if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -245,7 +250,8 @@ __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __re
   }
 }
 
-// *total = the sum of part[0 .. nb) (one block; int64, so the order does not matter)
+// *total = the sum of part[0 .. nb) (one block, nb <= kMapBlocks: 16 loads per thread; int64, so the order does not
+// matter).  Over one count per 256-entry block -- 137 k at level 0 -- this one block took 142 us.
 __global__ __launch_bounds__(kThreads) void sum_parts_kernel(const int32_t* __restrict__ part, int64_t nb,
                                                              int64_t* __restrict__ total) {
   __shared__ int64_t ws[kThreads / 64];
@@ -618,7 +624,7 @@ int msp_subm_map_counted(const uint64_t* keys, int64_t n, int log2_size, int64_t
     return MSP_OK;
   }
   const int K = filter_size * filter_size * filter_size;
-  const unsigned nb = grid1(n * K);
+  const unsigned nb = std::min<unsigned>(grid1(n * K), kMapBlocks);
   int32_t* part = static_cast<int32_t*>(ws);
   subm_map_kernel<<<nb, kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table, (uint64_t)(cap - 1),
                                           nbr, part);

@@ -717,6 +717,8 @@ def test_tile_local_rulebook():
     loc = metadata.local_rulebook(rules.nbr, 27, lvl.n, rules.nbr.device, _lib.stream(), 128)
     assert lvl.n % 128 != 0
     _check_local_rulebook(rules.nbr, loc, lvl.n)
+    # the rulebook size msp_subm_map_counted wrote beside the map, and the pair lists' count of the same map
+    assert rules.n_rules == int((rules.nbr >= 0).sum()) == rules.pairs.total
 
 
 @pytest.mark.parametrize("mode", ["random", "dup", "distinct"])
