@@ -207,35 +207,53 @@ __device__ __forceinline__ int32_t block_find(const uint64_t* __restrict__ table
   }
 }
 
-// Every entry of nbr[K][n] written (no memset): thread (o, i), i fastest, so a wave's rows are Morton-adjacent
-// and their lookups at one offset share the few block slots they touch.  part (nullable): the block's count of
-// present entries (msp_subm_map_counted: the rule total without a separate pass over the map).
+// Every entry of nbr[K][n] written (no memset).  A block covers 1024 consecutive rows of one offset, each thread
+// four rows 256 apart: the four key loads and the four slot probes are independent, so a wave has four chains of
+// (key -> probe) in flight instead of one (one row per thread was latency-bound: 247 us at level 0,
+// profiles/r05/prof_r05final2).  Within each of the four steps a wave's 64 rows are consecutive (coalesced
+// stores; their lookups at one offset share a few block slots).  Grid-stride over (offset, row block) with at
+// most kMapBlocks blocks; part (nullable): each block's count of present entries (msp_subm_map_counted).
+constexpr int kMapRows = 4;
 __global__ __launch_bounds__(kThreads) void subm_map_kernel(const uint64_t* __restrict__ keys, int64_t n,
                                                             int log2s, int64_t size, int f,
                                                             const uint64_t* __restrict__ table, uint64_t mask,
                                                             int32_t* __restrict__ nbr, int32_t* __restrict__ part) {
-  const int K = f * f * f, centre = (K - 1) / 2;
-  int c = 0;  // present entries this wave wrote (lane 0's count; part only)
-  // grid-stride (at most kMapBlocks blocks), so the per-block counts stay few enough for one summing block
-  for (int64_t e0 = (int64_t)blockIdx.x * kThreads; e0 < n * K; e0 += (int64_t)gridDim.x * kThreads) {
-    const int64_t e = e0 + threadIdx.x;
-    int32_t j = -1;
-    if (e < n * K) {
-      const int o = (int)(e / n);
-      const int64_t i = e - (int64_t)o * n;
-      if (o == centre) {
-        j = (int32_t)i;
-      } else {
-        int64_t b, x, y, z;
-        split_key(keys[i], log2s, b, x, y, z);
-        const int h = f / 2;
-        const int64_t xx = x + o / (f * f) - h, yy = y + (o / f) % f - h, zz = z + o % f - h;
-        if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size)
-          j = block_find(table, mask, make_key(b, xx, yy, zz, log2s));
-      }
-      nbr[e] = j;
+  const int K = f * f * f, centre = (K - 1) / 2, h = f / 2;
+  const int64_t nrb = (n + (int64_t)kThreads * kMapRows - 1) / ((int64_t)kThreads * kMapRows);
+  int c = 0;  // present entries this wave wrote (part only)
+  for (int64_t bi = blockIdx.x; bi < nrb * K; bi += gridDim.x) {
+    const int o = (int)(bi / nrb);
+    const int64_t i0 = (bi - (int64_t)o * nrb) * kThreads * kMapRows + threadIdx.x;
+    const int dx = o / (f * f) - h, dy = (o / f) % f - h, dz = o % f - h;
+    uint64_t key[kMapRows];
+#pragma unroll
+    for (int k = 0; k < kMapRows; ++k) {
+      const int64_t i = i0 + (int64_t)k * kThreads;
+      key[k] = (o != centre && i < n) ? keys[i] : 0;
     }
-    if (part) c += __popcll(__ballot(j >= 0));
+    int32_t j[kMapRows];
+#pragma unroll
+    for (int k = 0; k < kMapRows; ++k) {
+      const int64_t i = i0 + (int64_t)k * kThreads;
+      j[k] = -1;
+      if (i < n) {
+        if (o == centre) {
+          j[k] = (int32_t)i;
+        } else {
+          int64_t b, x, y, z;
+          split_key(key[k], log2s, b, x, y, z);
+          const int64_t xx = x + dx, yy = y + dy, zz = z + dz;
+          if (xx >= 0 && yy >= 0 && zz >= 0 && xx < size && yy < size && zz < size)
+            j[k] = block_find(table, mask, make_key(b, xx, yy, zz, log2s));
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kMapRows; ++k) {
+      const int64_t i = i0 + (int64_t)k * kThreads;
+      if (i < n) nbr[(int64_t)o * n + i] = j[k];
+      if (part) c += __popcll(__ballot(j[k] >= 0));
+    }
   }
   if (part) {
     __shared__ int wc[kThreads / 64];
@@ -624,7 +642,7 @@ int msp_subm_map_counted(const uint64_t* keys, int64_t n, int log2_size, int64_t
     return MSP_OK;
   }
   const int K = filter_size * filter_size * filter_size;
-  const unsigned nb = std::min<unsigned>(grid1(n * K), kMapBlocks);
+  const unsigned nb = (unsigned)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * kMapRows) * K, kMapBlocks);
   int32_t* part = static_cast<int32_t*>(ws);
   subm_map_kernel<<<nb, kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table, (uint64_t)(cap - 1),
                                           nbr, part);
@@ -640,8 +658,9 @@ int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial
   if (n == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
   const int K = filter_size * filter_size * filter_size;
-  subm_map_kernel<<<grid1(n * K), kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table,
-                                                    (uint64_t)(cap - 1), nbr, nullptr);
+  const unsigned nb = (unsigned)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * kMapRows) * K, kMapBlocks);
+  subm_map_kernel<<<nb, kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table, (uint64_t)(cap - 1),
+                                          nbr, nullptr);
   return check_launch("msp_subm_map");
 }
 
