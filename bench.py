@@ -532,6 +532,11 @@ def main():
             _HIP_RT.hipGraphUpload.restype = ctypes.c_int
         return _HIP_RT
 
+    cprof = None
+    if os.environ.get("BENCH_CPROFILE"):  # diagnostic: host profile of the captures and prefetches in the loop
+        import cProfile
+        cprof = cProfile.Profile()
+
     def capture(i):
         """Graph of step i, whose metadata is the pending prefetch; returns (graph, metadata it reads, the
         metadata's build event).  Nothing executes here: the kernels run at replay."""
@@ -662,7 +667,11 @@ def main():
                 held[:] = [h for h in held if not h[1].query()]
             inflight[-1] = (inflight[-1][0][0], None, i)
             h3 = time.perf_counter()
+            if cprof is not None:
+                cprof.enable()
             entry = capture(i + 1) if i + 1 < args.steps else None
+            if cprof is not None:
+                cprof.disable()
             loop_t.append((h1 - h0, h2 - h1, time.perf_counter() - h3))
             mem_t.append(torch.cuda.memory_reserved(dev))
             if host_t is not None:
@@ -745,6 +754,12 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if cprof is not None and rank == 0:
+        import io
+        import pstats
+        out = io.StringIO()
+        pstats.Stats(cprof, stream=out).sort_stats("tottime").print_stats(35)
+        print(out.getvalue(), file=sys.stderr)
     step_ms = [a.elapsed_time(b) for a, b in zip(bounds[:-1], bounds[1:])]
     rec.active = False
     held.clear()  # every step has completed
