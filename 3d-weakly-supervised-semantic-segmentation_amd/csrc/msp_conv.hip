@@ -76,6 +76,198 @@ __global__ __launch_bounds__(kThreads) void conv_pairs_kernel(
   }
 }
 
+// Runs of chunks (MSP_PAIRS_RUN): one wave takes `run` consecutive chunks.  The chunks are offset-major, so a run
+// stays in one offset except where it crosses into the next; the offset's weight block (c_in / 16 <= KMAX k-steps
+// of NT 16-column groups) is loaded into registers once per run and reloaded only at such a crossing, instead of
+// once per 16 pairs (conv_pairs_kernel reads 2x the bytes of the x rows it multiplies in weights at level 0).
+// The next chunk's pair indices are loaded while the current chunk's x rows are in flight.  Per chunk the
+// arithmetic is conv_pairs_kernel's, in the same order: the outputs are bit-identical.
+template <int NT, int KMAX>
+__global__ __launch_bounds__(kThreads) void conv_pairs_run_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int c_out,
+    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
+    const int64_t* __restrict__ chunk_start, int64_t n_chunks, int run, float* __restrict__ out) {
+  constexpr int NC = 16 * NT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t ch0 = ((int64_t)blockIdx.x * kWaves + wave) * run;
+  if (ch0 >= n_chunks) return;
+  const int64_t ch1 = ch0 + run < n_chunks ? ch0 + run : n_chunks;
+  const int c0 = blockIdx.y * NC;
+  const int r = lane & 15, q = lane >> 4;
+  const int kcn = c_in >> 4;
+  // offset walk of the index loads (wave-uniform; empty offsets have equal chunk starts)
+  int oi = find_offset(chunk_start, K, ch0);
+  int64_t oi_first = chunk_start[oi], oi_end = chunk_start[oi + 1], pb = off_start[oi], pe = off_start[oi + 1];
+  auto indices = [&](int64_t ch, int& src, int (&dst)[4], int& o_of) {
+    if (ch >= oi_end) {
+      do {
+        ++oi;
+        oi_end = chunk_start[oi + 1];
+      } while (ch >= oi_end);
+      oi_first = chunk_start[oi];
+      pb = off_start[oi];
+      pe = off_start[oi + 1];
+    }
+    const int64_t p0 = pb + (ch - oi_first) * MSP_CHUNK;
+    src = p0 + r < pe ? pin[p0 + r] : -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j] = p0 + 4 * q + j < pe ? pout[p0 + 4 * q + j] : -1;
+    o_of = oi;
+  };
+  floatx4 b[KMAX][NT];
+  int ow = -1;  // the offset whose weights are in b
+  int src, dst[4], o;
+  indices(ch0, src, dst, o);
+  for (int64_t ch = ch0; ch < ch1; ++ch) {
+    if (o != ow) {
+      ow = o;
+      const float* wb = wt + ((int64_t)o * c_out + c0 + r) * c_in + 4 * q;
+#pragma unroll
+      for (int kc = 0; kc < KMAX; ++kc)
+        if (kc < kcn) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            b[kc][t] = *reinterpret_cast<const floatx4*>(wb + (int64_t)t * 16 * c_in + kc * 16);
+        }
+    }
+    const float* xs = x + (int64_t)(src < 0 ? 0 : src) * c_in + 4 * q;
+    floatx4 a[KMAX];
+#pragma unroll
+    for (int kc = 0; kc < KMAX; ++kc)
+      if (kc < kcn) {
+        a[kc] = *reinterpret_cast<const floatx4*>(xs + kc * 16);
+        if (src < 0) a[kc] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    int dcur[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dcur[j] = dst[j];
+    if (ch + 1 < ch1) indices(ch + 1, src, dst, o);
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KMAX; ++kc)
+      if (kc < kcn) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[kc][s], b[kc][t][s], acc[t]);
+        }
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (dcur[j] >= 0) {
+        float* d = out + (int64_t)dcur[j] * c_out + c0 + r;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) d[t * 16] = acc[t][j];
+      }
+    }
+  }
+}
+
+// MSP_PAIRS_DEPTH 2: conv_pairs_run_kernel with the next chunk's x rows loaded as well (and the indices two chunks
+// ahead) while the current chunk's MFMAs and stores run.
+template <int NT, int KMAX>
+__global__ __launch_bounds__(kThreads) void conv_pairs_pipe_kernel(
+    const float* __restrict__ x, int c_in, const float* __restrict__ wt, int K, int c_out,
+    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
+    const int64_t* __restrict__ chunk_start, int64_t n_chunks, int run, float* __restrict__ out) {
+  constexpr int NC = 16 * NT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t ch0 = ((int64_t)blockIdx.x * kWaves + wave) * run;
+  if (ch0 >= n_chunks) return;
+  const int64_t ch1 = ch0 + run < n_chunks ? ch0 + run : n_chunks;
+  const int c0 = blockIdx.y * NC;
+  const int r = lane & 15, q = lane >> 4;
+  const int kcn = c_in >> 4;
+  int oi = find_offset(chunk_start, K, ch0);
+  int64_t oi_first = chunk_start[oi], oi_end = chunk_start[oi + 1], pb = off_start[oi], pe = off_start[oi + 1];
+  auto indices = [&](int64_t ch, int& src, int (&dst)[4], int& o_of) {
+    if (ch >= oi_end) {
+      do {
+        ++oi;
+        oi_end = chunk_start[oi + 1];
+      } while (ch >= oi_end);
+      oi_first = chunk_start[oi];
+      pb = off_start[oi];
+      pe = off_start[oi + 1];
+    }
+    const int64_t p0 = pb + (ch - oi_first) * MSP_CHUNK;
+    src = p0 + r < pe ? pin[p0 + r] : -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j] = p0 + 4 * q + j < pe ? pout[p0 + 4 * q + j] : -1;
+    o_of = oi;
+  };
+  auto load_x = [&](int src, floatx4 (&a)[KMAX]) {
+    const float* xs = x + (int64_t)(src < 0 ? 0 : src) * c_in + 4 * q;
+#pragma unroll
+    for (int kc = 0; kc < KMAX; ++kc)
+      if (kc < kcn) a[kc] = *reinterpret_cast<const floatx4*>(xs + kc * 16);
+  };
+  floatx4 b[KMAX][NT];
+  int ow = -1;
+  // chunk ch: a / s_c / d_c / o_c; chunk ch + 1: indices s_n / d_n / o_n (its x rows are loaded in the body)
+  int s_c, d_c[4], o_c, s_n = -1, d_n[4] = {-1, -1, -1, -1}, o_n = 0;
+  floatx4 a[KMAX];
+  indices(ch0, s_c, d_c, o_c);
+  load_x(s_c, a);
+  if (ch0 + 1 < ch1) indices(ch0 + 1, s_n, d_n, o_n);
+  for (int64_t ch = ch0; ch < ch1; ++ch) {
+    if (o_c != ow) {
+      ow = o_c;
+      const float* wb = wt + ((int64_t)o_c * c_out + c0 + r) * c_in + 4 * q;
+#pragma unroll
+      for (int kc = 0; kc < KMAX; ++kc)
+        if (kc < kcn) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            b[kc][t] = *reinterpret_cast<const floatx4*>(wb + (int64_t)t * 16 * c_in + kc * 16);
+        }
+    }
+    const bool more = ch + 1 < ch1;
+    floatx4 an[KMAX];
+    if (more) load_x(s_n, an);
+    int s2 = -1, d2[4] = {-1, -1, -1, -1}, o2 = o_n;
+    if (ch + 2 < ch1) indices(ch + 2, s2, d2, o2);
+    if (s_c < 0) {
+#pragma unroll
+      for (int kc = 0; kc < KMAX; ++kc) a[kc] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < KMAX; ++kc)
+      if (kc < kcn) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[kc][s], b[kc][t][s], acc[t]);
+        }
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (d_c[j] >= 0) {
+        float* d = out + (int64_t)d_c[j] * c_out + c0 + r;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) d[t * 16] = acc[t][j];
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int kc = 0; kc < KMAX; ++kc) a[kc] = an[kc];
+      s_c = s_n;
+      o_c = o_n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d_c[j] = d_n[j];
+      s_n = s2;
+      o_n = o2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d_n[j] = d2[j];
+    }
+  }
+}
+
 // dw[o][e] = sum over pieces j of slab[j][o][e]: block = 64 elements x 4
 // contiguous piece segments; the segment sums are added in segment order
 // (fixed order, deterministic).
@@ -318,16 +510,58 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
   return rc ? rc : check_launch("msp_conv_tile");
 }
 
+// Runs of chunks with the weights in registers where c_in <= 64; MSP_PAIRS_RUN 0: one chunk per wave, weights
+// re-read per chunk (the round-4 form).  Level 0 of the headline batch (64 -> 32, 1.30 M pairs): 148.8 us in the
+// one-chunk form, 137.6 with runs (MSP_PAIRS_DEPTH 1: indices one chunk ahead), 123.5 with the x rows one chunk
+// ahead as well (MSP_PAIRS_DEPTH 2); 4096 waves instead of 8192: 133.1 (profiles/r05/kb_pairs_r05b.log).  Without
+// any prefetch the runs were slower than the one-chunk form (163 vs 150 us).
+#ifndef MSP_PAIRS_RUN
+#define MSP_PAIRS_RUN 1
+#endif
+#ifndef MSP_PAIRS_WAVES
+#define MSP_PAIRS_WAVES 8192
+#endif
+#ifndef MSP_PAIRS_DEPTH
+#define MSP_PAIRS_DEPTH 2
+#endif
+
 int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, const int32_t* pair_in,
                    const int32_t* pair_out, const int64_t* off_start, const int64_t* chunk_start,
                    int64_t n_chunks, float* out, msp_stream_t stream) {
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_pairs: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   if (n_chunks == 0) return MSP_OK;
-  const int NT = pick_tile(c_out / 16);
-  dim3 grid((unsigned)ceil_div(n_chunks, kWaves), (unsigned)(c_out / (16 * NT)));
   hipStream_t s = as_stream(stream);
-#define LAUNCH(N)                                                                                       \
+  const int kcn = c_in / 16, n16 = c_out / 16;
+  if (MSP_PAIRS_RUN && kcn <= 4) {
+    // weights in registers (c_in <= 64); wider inputs keep the one-chunk form, which measured faster there (the
+    // weight registers cost occupancy and narrower column groups re-read x: profiles/r05/kb_pairs_r05*.log)
+    const int NT = pick_tile(n16), ny = n16 / NT;
+    // about MSP_PAIRS_WAVES waves over the grid: runs long enough to amortise the weights, enough waves to fill
+    // the chip
+    int64_t run = n_chunks * ny / MSP_PAIRS_WAVES;
+    run = run < 1 ? 1 : run > 16 ? 16 : run;
+    const int64_t waves = ceil_div(n_chunks, run);
+    dim3 grid((unsigned)ceil_div(waves, kWaves), (unsigned)ny);
+#define LAUNCH_RUN(N)                                                                                          \
+  if (MSP_PAIRS_DEPTH == 2)                                                                                    \
+    conv_pairs_pipe_kernel<N, 4><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, c_out, pair_in, pair_out, off_start, \
+                                                           chunk_start, n_chunks, (int)run, out);              \
+  else                                                                                                         \
+    conv_pairs_run_kernel<N, 4><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, c_out, pair_in, pair_out, off_start,  \
+                                                          chunk_start, n_chunks, (int)run, out)
+    switch (NT) {
+      case 1: LAUNCH_RUN(1); break;
+      case 2: LAUNCH_RUN(2); break;
+      case 3: LAUNCH_RUN(3); break;
+      default: LAUNCH_RUN(4); break;
+    }
+#undef LAUNCH_RUN
+    return check_launch("msp_conv_pairs");
+  }
+  const int NT = pick_tile(n16);
+  dim3 grid((unsigned)ceil_div(n_chunks, kWaves), (unsigned)(c_out / (16 * NT)));
+#define LAUNCH(N)                                                                                     \
   case N:                                                                                               \
     conv_pairs_kernel<N><<<grid, kThreads, 0, s>>>(x, c_in, wt, K, c_out, pair_in, pair_out, off_start, \
                                                    chunk_start, n_chunks, out);                        \

@@ -148,6 +148,43 @@ def test_strided_conv_deconv_unpool(stride, cin, cout):
     close(dg.weight.grad, do.weight.grad, 1e-5, "deconv dW")
 
 
+@pytest.mark.parametrize("cin,cout", [(64, 32), (96, 64), (48, 16), (160, 32)])
+def test_conv_pairs_runs_cross_offsets(cin, cout):
+    """msp_conv_pairs at a size where a wave takes a run of chunks with the weights in registers (c_in <= 64),
+    runs crossing from one offset into the next and over an empty offset, against fp64: every output row has one
+    contribution, W[o]^T x[pin], as the deconvolution forward and the strided backward-data have.  c_in = 96 and
+    160 take the one-chunk form.  The library's f32 MFMA products are exact, so 1e-5 is the fp32 accumulation."""
+    from sparseconvnet import _lib
+    g = torch.Generator().manual_seed(cin + cout)
+    K, n_out, n_in = 8, 300_000, 50_000
+    counts = torch.multinomial(torch.ones(K), n_out, replacement=True, generator=g).bincount(minlength=K)
+    counts[3] = 0   # an empty offset
+    counts[0] += n_out - int(counts.sum())
+    starts = torch.zeros(K + 1, dtype=torch.int64)
+    starts[1:] = counts.cumsum(0)
+    pout = torch.randperm(n_out, generator=g).int()
+    pin = torch.randint(0, n_in, (n_out,), generator=g).int()
+    for o in range(K):  # sorted by source row within an offset, as the pair lists are
+        a, b = int(starts[o]), int(starts[o + 1])
+        pin[a:b] = pin[a:b].sort().values
+    chunk_start = torch.zeros(K + 1, dtype=torch.int64)
+    chunk_start[1:] = ((counts + 15) // 16).cumsum(0)
+    n_chunks = int(chunk_start[-1])
+    x = torch.randn(n_in, cin, generator=g)
+    wt = torch.randn(K, cout, cin, generator=g)   # [K][c_out][c_in]
+    dx, dwt, dpin, dpout = x.to(DEV), wt.to(DEV), pin.to(DEV), pout.to(DEV)
+    dst, dcs = starts.to(DEV), chunk_start.to(DEV)
+    out = torch.full((n_out, cout), float("nan"), device=DEV)
+    _lib.call("msp_conv_pairs", dx.data_ptr(), cin, dwt.data_ptr(), K, cout, dpin.data_ptr(), dpout.data_ptr(),
+              dst.data_ptr(), dcs.data_ptr(), n_chunks, out.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    ref = torch.empty(n_out, cout, dtype=torch.float64)
+    for o in range(K):
+        a, b = int(starts[o]), int(starts[o + 1])
+        ref[pout[a:b].long()] = x[pin[a:b].long()].double() @ wt[o].double().t()
+    close(out, ref, 1e-5, f"conv_pairs {cin}->{cout}")
+
+
 @pytest.mark.parametrize("C,leak,train,mu,sd", [(32, 0.0, True, 1.5, 3.0), (48, 0.333, True, 1.5, 3.0),
                                                 (896, 0.0, True, 1.5, 3.0), (16, 0.0, False, 1.5, 3.0),
                                                 (32, 0.0, True, 10.0, 0.01)])
