@@ -623,9 +623,15 @@ int msp_hash_build(const uint64_t* keys, int64_t n, uint64_t* table, int64_t cap
   return check_launch("msp_hash_build");
 }
 
-size_t msp_subm_map_workspace_size(int64_t n, int filter_size) {
+// the counted map's grid (one partial count per block, written by every block)
+static unsigned subm_map_blocks(int64_t n, int filter_size) {
   const int64_t K = (int64_t)filter_size * filter_size * filter_size;
-  return (size_t)(ceil_div(n > 0 ? n * K : 1, kThreads)) * sizeof(int32_t);
+  return (unsigned)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * kMapRows) * K, kMapBlocks);
+}
+
+size_t msp_subm_map_workspace_size(int64_t n, int filter_size) {
+  const unsigned nb = n > 0 ? subm_map_blocks(n, filter_size) : 1u;
+  return (size_t)(nb > 0 ? nb : 1u) * sizeof(int32_t);
 }
 
 int msp_subm_map_counted(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial_size, int filter_size,
@@ -641,8 +647,7 @@ int msp_subm_map_counted(const uint64_t* keys, int64_t n, int log2_size, int64_t
     MSP_HIP(hipMemsetAsync(n_rules, 0, sizeof(int64_t), s), "msp_subm_map_counted");
     return MSP_OK;
   }
-  const int K = filter_size * filter_size * filter_size;
-  const unsigned nb = (unsigned)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * kMapRows) * K, kMapBlocks);
+  const unsigned nb = subm_map_blocks(n, filter_size);
   int32_t* part = static_cast<int32_t*>(ws);
   subm_map_kernel<<<nb, kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table, (uint64_t)(cap - 1),
                                           nbr, part);
@@ -657,8 +662,7 @@ int msp_subm_map(const uint64_t* keys, int64_t n, int log2_size, int64_t spatial
   MSP_REQUIRE((cap & (cap - 1)) == 0, "msp_subm_map: bad capacity");
   if (n == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
-  const int K = filter_size * filter_size * filter_size;
-  const unsigned nb = (unsigned)std::min<int64_t>(ceil_div(n, (int64_t)kThreads * kMapRows) * K, kMapBlocks);
+  const unsigned nb = subm_map_blocks(n, filter_size);
   subm_map_kernel<<<nb, kThreads, 0, s>>>(keys, n, log2_size, spatial_size, filter_size, table, (uint64_t)(cap - 1),
                                           nbr, nullptr);
   return check_launch("msp_subm_map");

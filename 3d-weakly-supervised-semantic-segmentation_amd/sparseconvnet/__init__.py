@@ -15,6 +15,7 @@ from .networkArchitectures import FullyConvolutionalNet, FullyConvolutionalNetEn
 from .utils import checkpoint_restore, checkpoint_save, is_power2
 from . import _lib
 from . import weight_images
+from . import graphs
 
 # SCN's global work counters (train.py:50-51,86-87): multiply-adds of every
 # convolution (rules * nIn * nOut) and output elements of every convolution.
@@ -27,5 +28,5 @@ __all__ = [
     "BatchNormLeakyReLU", "Sequential", "ConcatTable", "AddTable", "JoinTable", "Identity", "SparseToDense",
     "UNet", "FullyConvolutionalNet", "FullyConvolutionalNetEncoder", "checkpoint_save", "checkpoint_restore",
     "is_power2", "forward_pass_multiplyAdd_count", "forward_pass_hidden_states", "prefetch_metadata",
-    "weight_images",
+    "weight_images", "graphs",
 ]

@@ -326,6 +326,8 @@ class SubmRules:
         """SCN's rulebook size (centre included); a count still queued in the replay in progress is read now."""
         if "_n_rules" not in self.__dict__ and _defer() is not None:
             _defer().flush()
+        if "_n_rules" not in self.__dict__:  # a replay whose flush failed left the count unread: read it now
+            self._n_rules = int(_host(self._nr)[0])
         return self._n_rules
 
     @property
@@ -387,13 +389,15 @@ class SubmRules:
         Inside a replay whose counts are not read yet this returns the _PENDING sentinel (the index is built when
         the replay flushes its reads); wait=True (every consumer of the index) flushes them first, so the caller
         always gets the index itself."""
-        if self._wchunk is _PENDING:
+        if self._wchunk is _PENDING or (isinstance(self._wchunk, dict) and "chunk_lr" not in self._wchunk):
             if not wait:
                 return self._wchunk
             d = _defer()
             if d is not None:
                 d.flush()
-            if self._wchunk is _PENDING:  # the replay ended without deciding (its flush failed): build it now
+            # the replay ended without deciding or without filling the index (its flush failed): build it now
+            w = self._wchunk
+            if w is _PENDING or (isinstance(w, dict) and "chunk_lr" not in w):
                 self._wchunk = None
         if self._wchunk is None and LOCAL_CHUNK_INDEX:
             full = self._locals.get(128)
@@ -696,10 +700,12 @@ class Metadata:
             _TLS.defer.flush()
         finally:
             _TLS.defer = outer
-            # a flush that raised leaves weight-gradient indices undecided: forget them (built again on use)
+            # a flush that raised leaves weight-gradient indices undecided or half-built (no chunk words yet):
+            # forget them (built again on use); the rulebook sizes are read on use (SubmRules.n_rules)
             for lvl in self.levels.values():
                 for r in getattr(lvl, "subm", {}).values():
-                    if getattr(r, "_wchunk", None) is _PENDING:
+                    w = getattr(r, "_wchunk", None)
+                    if w is _PENDING or (isinstance(w, dict) and "chunk_lr" not in w):
                         r._wchunk = None
 
     def _replay(self, plan):

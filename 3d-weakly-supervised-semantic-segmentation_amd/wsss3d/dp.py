@@ -208,6 +208,15 @@ class GradSync:
             torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
         self._pending = None
 
+    def abort(self):
+        """A capture of the step failed inside backward (sparseconvnet.graphs.capture's on_abort): the exchange
+        stream rejoins the capturing stream (a stream that joined a capture and did not rejoin it keeps the
+        capture from ending) and the bucket counts are dropped; the next step's begin() starts afresh."""
+        if self._pending is not None and self._side is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
+        self._pending = None
+        self._next = 0
+
     def average(self):
         if dist.is_initialized():
             dist.all_reduce(self.flat)

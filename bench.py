@@ -549,7 +549,13 @@ def main():
             c0 = time.perf_counter()
             g.capture_begin(pool=graph_pool, capture_error_mode="relaxed")
             c1 = time.perf_counter()
-            body(i)
+            try:
+                body(i)
+            except BaseException:
+                # end the capture and discard the graph before the error propagates (an open capture makes
+                # ~CUDAGraph terminate the process); sparseconvnet.graphs.capture is the same path
+                scn.graphs.abort(g, gsync.abort if gsync is not None else None)
+                raise
             c2 = time.perf_counter()
             g.capture_end()
             c3 = time.perf_counter()

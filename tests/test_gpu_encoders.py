@@ -376,6 +376,80 @@ def test_graph_captured_step_matches_eager():
             assert torch.equal(sa[k], sb[k])
 
 
+@pytest.mark.parametrize("where", ["forward", "backward"])
+def test_capture_error_is_a_clean_error(where):
+    """An error raised inside a captured step (a module whose forward raises; a gradient hook that raises in
+    backward) comes out of sparseconvnet.graphs.capture as that RuntimeError, with the capture ended and the
+    graph discarded -- not an abort of the process (round-5 verdict: ~CUDAGraph on an open capture called
+    std::terminate).  The process then runs an eager step, and a captured + replayed step, bit-identical to a
+    twin model that never saw the failed capture (weight images on, so the discarded prepare() must not be
+    trusted)."""
+    import copy
+    import torch.nn.functional as F
+    from sparseconvnet import metadata as md
+    model, xs, ys = _prefetch_model()
+    twin = copy.deepcopy(model)
+    opts = [torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=True) for m in (model, twin)]
+    wimg = scn.weight_images.enable(twin, DEV, optimizer=opts[1])
+    fail = [False]
+
+    def boom(*_):
+        if fail[0]:
+            raise RuntimeError("injected failure inside the capture")
+
+    enc = twin.pc_encoder.encoder
+    hook = list(enc)[2].register_forward_hook(boom) if where == "forward" else None
+
+    def body(m, opt, k, images=None):
+        if images is not None:
+            images.prepare()
+        opt.zero_grad(set_to_none=True)
+        logits, _ = m((xs[k], None), istrain=True)
+        if where == "backward" and m is twin:
+            logits.register_hook(lambda g: boom() or g)
+        F.multilabel_soft_margin_loss(logits, ys[k]).backward()
+        opt.step()
+
+    try:
+        for m, opt in zip((model, twin), opts):   # plan, optimizer state and image descriptors, eagerly
+            body(m, opt, 0, wimg if m is twin else None)
+        wimg.build()
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream()
+        scn.prefetch_metadata(twin, xs[1].coords, wait_for_producer=False)
+        fail[0] = True
+        with pytest.raises(RuntimeError, match="injected failure"):
+            scn.graphs.capture(lambda: body(twin, opts[1], 1, wimg), side)
+        fail[0] = False
+        assert not torch.cuda.is_current_stream_capturing()
+        assert md.captured_metadata() == [] and md.pending_count() == 0
+        assert not wimg.valid  # the discarded capture's prepare() is not trusted
+        # an eager step on both, then a captured + replayed step on the twin against an eager one
+        body(model, opts[0], 1)
+        body(twin, opts[1], 1, wimg)
+        scn.prefetch_metadata(model, xs[0].coords, wait_for_producer=False)
+        body(model, opts[0], 0)
+        wimg.build()
+        scn.prefetch_metadata(twin, xs[0].coords, wait_for_producer=False)
+        ev = md.prefetch_event(DEV)
+        g, _ = scn.graphs.capture(lambda: body(twin, opts[1], 0, wimg), side)
+        keep = md.captured_metadata()
+        assert len(keep) == 1
+        torch.cuda.current_stream().wait_event(ev)
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        scn.weight_images.disable()
+        if hook is not None:
+            hook.remove()
+    for (na, a), (nb, b) in zip(model.named_parameters(), twin.named_parameters()):
+        assert torch.equal(a, b), na
+        assert torch.equal(a.grad, b.grad), na
+    for sa, sb in zip(opts[0].state.values(), opts[1].state.values()):
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(sa[k], sb[k])
+
+
 def test_graph_capture_beside_worker_prefetch():
     """bench.py --prefetch-thread: each step is captured while a worker thread builds the metadata of the next
     batch on the side stream (two prefetched batches pending, PREFETCH_DEPTH = 2); three captured and replayed

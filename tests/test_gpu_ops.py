@@ -561,11 +561,15 @@ def test_residual_join_stats(V, C):
 
 
 @pytest.mark.parametrize("C,leak,nin", [(32, 0.0, False), (64, 0.333, True), (6, 0.0, False)])
-def test_residual_block_fused_matches_unfused(C, leak, nin):
+def test_residual_block_fused_matches_unfused(C, leak, nin, monkeypatch):
     """ConcatTable(shortcut, BN-SubM-BN-SubM) + AddTable + BN with the fork /
     join fusions against the same modules run one by one with torch adds
     (the unfused composition): outputs, input gradient and every parameter
-    gradient bit-equal, running statistics equal."""
+    gradient bit-equal, running statistics equal.  (The BatchNorm statistics
+    epilogues change the fp64 summation order, so they are off here; their own
+    comparison is tests/test_gpu_bn_epilogue.py.)"""
+    from sparseconvnet import ops
+    monkeypatch.setattr(ops, "FUSE_BN_STATS", False)
     torch.manual_seed(C)
     coords, feats = _inputs(3000, 24, n_feat=C)
     g, _ = _pair(coords, feats)
