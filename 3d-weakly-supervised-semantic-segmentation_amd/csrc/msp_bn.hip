@@ -261,6 +261,31 @@ __device__ inline void sum_partials(const double* __restrict__ partial, int64_t 
   out2[1] = red[1][0];
 }
 
+// The same over a channel-major buffer partial[2][C][P] (msp_bn_epilogue): a channel's P slots are contiguous,
+// so the block's loads are coalesced however many tiles wrote them.
+__device__ inline void sum_partials_cm(const double* __restrict__ partial, int64_t P, int C, int c, double* out2) {
+  __shared__ double red[2][kT];
+  double a = 0.0, b = 0.0;
+  const double* p0 = partial + (int64_t)c * P;
+  const double* p1 = partial + ((int64_t)C + c) * P;
+  for (int64_t p = threadIdx.x; p < P; p += kT) {
+    a += p0[p];
+    b += p1[p];
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int w = kT / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  out2[0] = red[0][0];
+  out2[1] = red[1][0];
+}
+
 // one block per channel
 __global__ __launch_bounds__(kT) void bn_finalize_kernel(const double* __restrict__ partial, int64_t P, int C,
                                                          int64_t V, double eps, double momentum, int train,
@@ -334,6 +359,52 @@ __global__ __launch_bounds__(kT) void bn_apply4_kernel(const float* __restrict__
     const float4 a = x4[v * C4 + c4];
     y4[v * C4 + c4] = make_float4(f(a.x, 0), f(a.y, 1), f(a.z, 2), f(a.w, 3));
   }
+}
+
+// one block per channel, channel-major partials (msp_bn_finalize_cm)
+__global__ __launch_bounds__(kT) void bn_finalize_cm_kernel(const double* __restrict__ partial, int64_t P, int C,
+                                                            int64_t V, double eps, double momentum, int train,
+                                                            float* __restrict__ rmean, float* __restrict__ rvar,
+                                                            const float* __restrict__ weight,
+                                                            const float* __restrict__ bias, float* __restrict__ stats) {
+  const int c = blockIdx.x;
+  double sums[2] = {0.0, 0.0};
+  if (train) sum_partials_cm(partial, P, C, c, sums);
+  if (threadIdx.x != 0) return;
+  double mu, var;
+  if (train) {
+    mu = V > 0 ? sums[0] / (double)V : 0.0;
+    var = V > 0 ? sums[1] / (double)V - mu * mu : 0.0;
+    if (var < 0.0) var = 0.0;
+    const double unb = V > 1 ? var * (double)V / (double)(V - 1) : var;
+    rmean[c] = (float)(momentum * rmean[c] + (1.0 - momentum) * mu);
+    rvar[c] = (float)(momentum * rvar[c] + (1.0 - momentum) * unb);
+  } else {
+    mu = rmean[c];
+    var = rvar[c];
+  }
+  const double is = 1.0 / sqrt(var + eps);
+  const double w = weight ? weight[c] : 1.0, b = bias ? bias[c] : 0.0;
+  const float hi = (float)mu;
+  stats[c] = hi;
+  stats[C + c] = (float)(mu - (double)hi);
+  stats[2 * C + c] = (float)is;
+  stats[3 * C + c] = (float)(w * is);
+  stats[4 * C + c] = (float)b;
+}
+
+// one block per channel, channel-major partials (msp_bn_bwd_apply_cm)
+__global__ __launch_bounds__(kT) void bn_bwd_finalize_cm_kernel(const double* __restrict__ partial, int64_t P, int C,
+                                                                float* __restrict__ dweight,
+                                                                float* __restrict__ dbias, double* __restrict__ sums) {
+  const int c = blockIdx.x;
+  double s2[2];
+  sum_partials_cm(partial, P, C, c, s2);
+  if (threadIdx.x != 0) return;
+  sums[c] = s2[0];
+  sums[C + c] = s2[1];
+  if (dbias) dbias[c] = (float)s2[0];
+  if (dweight) dweight[c] = (float)s2[1];
 }
 
 // one block per channel
@@ -518,6 +589,16 @@ int msp_bn_finalize(const double* partial, int64_t V, int C, double eps, double 
   return check_launch("msp_bn_finalize");
 }
 
+int msp_bn_finalize_cm(const double* partial, int64_t P, int64_t V, int C, double eps, double momentum, int train,
+                       float* running_mean, float* running_var, const float* weight, const float* bias, float* stats,
+                       msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && P >= 0 && (partial || !train), "msp_bn_finalize_cm: bad shape (C=%d P=%lld)", C,
+              (long long)P);
+  bn_finalize_cm_kernel<<<(unsigned)C, kT, 0, as_stream(stream)>>>(partial, P, C, V, eps, momentum, train,
+                                                                   running_mean, running_var, weight, bias, stats);
+  return check_launch("msp_bn_finalize_cm");
+}
+
 int msp_bn_apply(const float* x, int64_t V, int C, const float* stats, float leak, float* y, msp_stream_t stream) {
   const int64_t n = V * C;
   if (n == 0) return MSP_OK;
@@ -538,6 +619,11 @@ int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const fl
   return check_launch("msp_bn_bwd_stats");
 }
 
+// dx from the per-channel totals `sums` [2][C] (the finalize before it wrote them)
+static int bn_bwd_apply_sums(const float* x, const float* dy, int64_t V, int C, const double* sums,
+                             const float* stats, const float* weight, float leak, int train, const float* addend,
+                             float* dx, hipStream_t s);
+
 int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, const double* partial,
                          const float* stats, const float* weight, float leak, int train, const float* addend,
                          float* dx, float* dweight, float* dbias, msp_stream_t stream) {
@@ -547,6 +633,23 @@ int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, cons
   // the partial buffer (it holds (P + 1) * 2 * C doubles, see the header).
   double* sums = const_cast<double*>(partial) + bn_parts(V, C) * 2 * C;
   bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V, C), C, dweight, dbias, sums);
+  return bn_bwd_apply_sums(x, dy, V, C, sums, stats, weight, leak, train, addend, dx, s);
+}
+
+int msp_bn_bwd_apply_cm(const float* x, const float* dy, int64_t V, int C, const double* partial, int64_t P,
+                        const float* stats, const float* weight, float leak, int train, const float* addend,
+                        float* dx, float* dweight, float* dbias, msp_stream_t stream) {
+  MSP_REQUIRE(addend == nullptr || addend != dx || V * C == 0, "msp_bn_bwd_apply_cm: addend must not alias dx");
+  MSP_REQUIRE(C > 0 && P >= 0 && partial, "msp_bn_bwd_apply_cm: bad shape (C=%d P=%lld)", C, (long long)P);
+  hipStream_t s = as_stream(stream);
+  double* sums = const_cast<double*>(partial) + P * 2 * C;  // the [2][C] tail
+  bn_bwd_finalize_cm_kernel<<<(unsigned)C, kT, 0, s>>>(partial, P, C, dweight, dbias, sums);
+  return bn_bwd_apply_sums(x, dy, V, C, sums, stats, weight, leak, train, addend, dx, s);
+}
+
+static int bn_bwd_apply_sums(const float* x, const float* dy, int64_t V, int C, const double* sums,
+                             const float* stats, const float* weight, float leak, int train, const float* addend,
+                             float* dx, hipStream_t s) {
   const int64_t n = V * C;
   if (n > 0) {
     if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx) &&

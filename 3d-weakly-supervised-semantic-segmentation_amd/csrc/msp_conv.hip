@@ -485,6 +485,20 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
                   const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                   const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
                   msp_stream_t stream) {
+  return msp_conv_tile_bn(x, c_in, wt, K, flip, c_out, tile_rows, tile_start, chunk_off, chunk_src, chunk_row,
+                          n_rows, out, ws, ws_bytes, nullptr, stream);
+}
+
+int64_t msp_conv_bn_parts(int64_t n_rows) { return n_rows > 0 ? ceil_div(n_rows, 128) : 0; }
+
+int msp_conv_tile_bn(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                     const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                     const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                     const msp_bn_epilogue* epi, msp_stream_t stream) {
+  MSP_REQUIRE(epi == nullptr || (epi->partial != nullptr && (epi->x == nullptr || epi->stats != nullptr)),
+              "msp_conv_tile_bn: epilogue without a partial buffer (or a backward one without stats)");
+  MSP_REQUIRE(epi == nullptr || n_rows <= 0 || msp_conv_tile_form(n_rows, c_in, c_out, tile_rows) == 1,
+              "msp_conv_tile_bn: the BatchNorm epilogue needs the per-wave form (msp_conv_tile_form 1)");
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_tile: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= 128, "msp_conv_tile: K must be in [1, 128] (got %d)", K);
@@ -498,7 +512,7 @@ int msp_conv_tile(const float* x, int c_in, const float* wt, int K, int flip, in
     const size_t need = x6p_ws_bytes(K, c_in, c_out);
     MSP_REQUIRE(ws && ws_bytes >= need, "msp_conv_tile: workspace too small (%zu < %zu)", ws_bytes, need);
     const int rc = launch_x6r(x, c_in, wt, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows, out,
-                              ws, s);
+                              ws, s, epi);
     return rc ? rc : check_launch("msp_conv_tile");
   }
   // shared 128-row tiles on bf16 MFMA with exact operand splits (msp_conv_x6.hip)

@@ -73,7 +73,7 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
 // Per-wave split-bf16 form for narrow outputs (c_out <= 32, c_in <= 64), 128-row tiles.
 int launch_x6r(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
                const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
-               float* out, void* ws, hipStream_t s);
+               float* out, void* ws, hipStream_t s, const msp_bn_epilogue* epi = nullptr);
 size_t x6p_ws_bytes(int K, int c_in, int c_out);
 
 // Dense row-group split-bf16 form over the neighbour map (submanifold convs).

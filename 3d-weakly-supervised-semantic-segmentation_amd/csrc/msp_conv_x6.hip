@@ -32,6 +32,7 @@
 // B = X^T[k 8q .. 8q+7][chunk row r]; D[out 16t + 4q + j][chunk row r] lands in
 // register j, the accumulator layout of the f32 kernels.
 #include "msp_x6.h"
+#include "msp_bn_epi.h"
 
 namespace msp {
 
@@ -398,12 +399,14 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
 // PS 1 (experiments build only; measured slower): x is the exact split image of the input rows (split_rows_kernel: per row and 32-channel slice, 3 pieces x 4
 // k-octets of 16 bytes, row stride 6 c_in bytes), so the chunk loop loads the pieces instead of splitting every
 // gathered row per rule.
-template <int NT, int NKK, int D, int NW, int TR = 128, int PS = 0>
+// EPI (msp_bn_epilogue, round 6): the BatchNorm sums of the rows written; its own instantiation, so the plain form
+// compiles exactly as before.
+template <int NT, int NKK, int D, int NW, int TR = 128, int PS = 0, bool EPI = false>
 __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const int32_t* __restrict__ chunk_src, const uint16_t* __restrict__ chunk_row, int64_t n_rows,
-    int64_t n_tiles, int n_y, float* __restrict__ out) {
+    int64_t n_tiles, int n_y, float* __restrict__ out, BnEpi epi) {
   constexpr int NC = 16 * NT;
   constexpr int WU = 3 * 4 * NC;  // 16-byte units of one (offset, k-slice) image
   __shared__ floatx4 lds4[kWaves][TR * NC / 4];
@@ -562,10 +565,48 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
   const int nr = (int)((n_rows - row0) < TR ? (n_rows - row0) : TR);
   constexpr int V4 = NC / 4;
   const int c0 = cy * NC;
-  for (int i = lane; i < nr * V4; i += 64) {
-    const int rr = i / V4, g = i % V4;
-    *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
-        *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
+  // msp_bn_epilogue (uniform): the BatchNorm sums of the tile's rows, per lane for its column quad lane % V4,
+  // then over the wave's lanes into this tile's slot (TR = 128: one slot per tile)
+  if constexpr (!EPI) {
+    for (int i = lane; i < nr * V4; i += 64) {
+      const int rr = i / V4, g = i % V4;
+      *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) =
+          *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
+    }
+    return;
+  }
+  BnEpiAcc ea;
+  ea.init(epi, c0 + 4 * (lane % V4));
+  // backward: the BN input quads in batches of four loads in flight (16 serial latencies per tile otherwise)
+  constexpr int EI = TR * V4 / 64, EB = 4;  // output quads per lane, batch
+  static_assert(EI * 64 == TR * V4 && EI % EB == 0, "whole batches of quads per lane");
+#pragma unroll
+  for (int e0 = 0; e0 < EI; e0 += EB) {
+    floatx4 xq[EB];
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int i = lane + 64 * (e0 + e);
+      xq[e] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (epi.x != nullptr && i < nr * V4)
+        xq[e] = *reinterpret_cast<const floatx4*>(epi.x + (row0 + i / V4) * epi.C + c0 + 4 * (i % V4));
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int i = lane + 64 * (e0 + e);
+      if (i < nr * V4) {
+        const int rr = i / V4, g = i % V4;
+        const floatx4 v = *reinterpret_cast<const floatx4*>(acc_s + acc_pos<NC>(rr, g));
+        *reinterpret_cast<floatx4*>(out + (row0 + rr) * c_out + c0 + 4 * g) = v;
+        ea.add_x(epi, v, epi.x != nullptr ? xq[e] : v);
+      }
+    }
+  }
+  {
+    static_assert(TR == 128 && 64 % V4 == 0, "one epilogue slot per 128-row tile");
+    ea.wave_reduce<V4>();
+    if (lane < V4)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) *bn_epi_slot(epi, k >> 2, c0 + 4 * lane + (k & 3), tile) = ea.s[k];
   }
 }
 
@@ -573,7 +614,8 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
 // offset run, chunk values three deep (profiles/r01/kbench_x6r_r01u.log).
 int launch_x6r(const float* x, int c_in, const float* wt, int K, int flip, int c_out, const int64_t* tile_start,
                const uint8_t* chunk_off, const int32_t* chunk_src, const uint16_t* chunk_row, int64_t n_rows,
-               float* out, void* ws, hipStream_t s) {
+               float* out, void* ws, hipStream_t s, const msp_bn_epilogue* epi) {
+  const BnEpi be = bn_epi_of(epi, c_out, n_rows);
   const int NT = c_out / 16 >= 2 && (c_out / 16) % 2 == 0 ? 2 : 1;
   const int NKK = (c_in + 31) / 32;
   const int n_y = c_out / (16 * NT);
@@ -587,8 +629,12 @@ int launch_x6r(const float* x, int c_in, const float* wt, int K, int flip, int c
   const unsigned grid = (unsigned)(ceil_div(n_tiles, kWaves) * n_y);
 #define LR(N, C)                                                                                               \
   if (NT == N && NKK == C) {                                                                                   \
-    conv_x6r_kernel<N, C, 3, 2><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start, chunk_off, \
-                                                          chunk_src, chunk_row, n_rows, n_tiles, n_y, out);    \
+    if (epi)                                                                                                   \
+      conv_x6r_kernel<N, C, 3, 2, 128, 0, true><<<grid, kThreads, 0, s>>>(                                     \
+          x, c_in, wimg, K, flip, c_out, tile_start, chunk_off, chunk_src, chunk_row, n_rows, n_tiles, n_y, out, be); \
+    else                                                                                                       \
+      conv_x6r_kernel<N, C, 3, 2><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start, chunk_off, \
+                                                            chunk_src, chunk_row, n_rows, n_tiles, n_y, out, be); \
     return MSP_OK;                                                                                             \
   }
   LR(2, 1) LR(2, 2) LR(1, 1) LR(1, 2)
@@ -635,11 +681,12 @@ int launch_x6r_exp(int variant, const float* x, int c_in, const float* wt, int K
     if (ps)                                                                                                    \
       conv_x6r_kernel<N, C, DD, 2, TT, 1><<<grid, kThreads, 0, s>>>(xin, c_in, wimg, K, flip, c_out,           \
                                                                     tile_start, chunk_off, chunk_src,          \
-                                                                    chunk_row, n_rows, n_tiles, n_y, out);     \
+                                                                    chunk_row, n_rows, n_tiles, n_y, out,      \
+                                                                    BnEpi{});                                  \
     else                                                                                                       \
       conv_x6r_kernel<N, C, DD, 2, TT><<<grid, kThreads, 0, s>>>(x, c_in, wimg, K, flip, c_out, tile_start,    \
                                                                  chunk_off, chunk_src, chunk_row, n_rows,      \
-                                                                 n_tiles, n_y, out);                           \
+                                                                 n_tiles, n_y, out, BnEpi{});                  \
     return MSP_OK;                                                                                             \
   }
   LE(2, 1, 3, 128) LE(2, 1, 3, 64) LE(2, 1, 2, 128) LE(2, 1, 2, 64)

@@ -34,6 +34,7 @@
 #include <type_traits>
 
 #include "msp_x6.h"
+#include "msp_bn_epi.h"
 
 namespace msp {
 
@@ -471,12 +472,14 @@ __device__ __forceinline__ int xs_unit(int j, int p, int qq) { return j * kXU + 
 // WB (weight fragment register sets): 1 = one set, the next step's fragments loaded after the step's MFMAs (their
 // latency exposed at the next step's start); 2 = two sets alternating, the next step's fragments loaded before the
 // step's MFMAs, so a whole step hides their latency (the first step of each slice loads after the staging).
-template <int NT, int AB = 0, int AC = 1, int WB = 1>
+// EPI (msp_bn_epilogue, round 6): the BatchNorm sums of the rows written; its own instantiation, so the plain form
+// compiles exactly as before (the epilogue's registers and loads never touch it).
+template <int NT, int AB = 0, int AC = 1, int WB = 1, bool EPI = false>
 __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int flip, int c_out,
     const uint16_t* __restrict__ lidx, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
     const int32_t* __restrict__ perm, const uint8_t* __restrict__ wave_off, int64_t n_pad, int n_y,
-    float* __restrict__ out) {
+    float* __restrict__ out, BnEpi epi) {
   constexpr int T = 128, NTH = 512, G = 4;
   constexpr int NC = 16 * NT;
   static_assert(4 * T * NC * 4 <= kXR * kXU * 16, "partial sums must fit the staging area");
@@ -674,6 +677,25 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
     }
   };
 
+  // msp_bn_epilogue, backward: the BN input rows the epilogue reads (its output rows' quads), loaded at the start of
+  // the last k-slice so their latency hides under that slice's MFMAs instead of ending the block
+  constexpr int QPR = NC / 4;  // float4 quads per output row
+  constexpr int EPR = T * QPR / NTH;
+  static_assert(EPR * NTH == T * QPR && 64 % QPR == 0, "a thread keeps one column quad in the epilogue");
+  floatx4 epx[EPR];
+  int32_t epd[EPR];
+  auto epi_prefetch = [&]() {
+    if constexpr (!EPI) return;
+#pragma unroll
+    for (int e = 0; e < EPR; ++e) {
+      const int i = tid + NTH * e, row = i / QPR, cq = i - row * QPR;
+      epd[e] = perm[tile * T + row];
+      epx[e] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (epi.x != nullptr && epd[e] >= 0)
+        epx[e] = *reinterpret_cast<const floatx4*>(epi.x + (int64_t)epd[e] * epi.C + cy * NC + 4 * cq);
+    }
+  };
+
   using Far = std::true_type;
   using Near = std::false_type;
   if (WB == 2 && U <= kUCap) {  // block-uniform: every listed row is staged (all but 0-0.09 % of tiles)
@@ -692,6 +714,7 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       if (ks) __syncthreads();  // previous slice's readers done
       stage(ks);
       __syncthreads();
+      if (ks == nks - 1) epi_prefetch();
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
         ld_next(ks, j, wb);
@@ -707,6 +730,7 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       if (ks) __syncthreads();  // previous slice's readers done
       stage(ks);
       __syncthreads();
+      if (ks == nks - 1) epi_prefetch();
       for (int j = 0; j < n_j; ++j) {
         run(ks, off_of(j), wf, Far{});
         if constexpr (!(AB & 4)) ld_w(ks * n_j + j + 1, wf);
@@ -723,15 +747,50 @@ __global__ __launch_bounds__(512, 4) void conv_x6s_kernel(
       *reinterpret_cast<floatx4*>(red + ((int64_t)(wc * T + 16 * (2 * g + rp) + r)) * NC + 16 * t + 4 * q) =
           acc[g][t];
   __syncthreads();
-  constexpr int QPR = NC / 4;  // float4 quads per row
-  for (int i = tid; i < T * QPR; i += NTH) {
-    const int row = i / QPR, cq = i - row * QPR;
+  // msp_bn_epilogue (block-uniform): the BatchNorm sums of the rows written, per thread for its column quad
+  // tid % QPR, then over the wave's lanes and the 8 waves in order into this tile's slot
+  if constexpr (!EPI) {
+    for (int i = tid; i < T * QPR; i += NTH) {
+      const int row = i / QPR, cq = i - row * QPR;
+      const float* pr = red + row * NC + 4 * cq;
+      floatx4 v = *reinterpret_cast<const floatx4*>(pr);
+#pragma unroll
+      for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const floatx4*>(pr + w * T * NC);
+      const int32_t dst = perm[tile * T + row];
+      if (dst >= 0) *reinterpret_cast<floatx4*>(out + (int64_t)dst * c_out + cy * NC + 4 * cq) = v;
+    }
+    return;
+  }
+  BnEpiAcc ea;
+  ea.init(epi, cy * NC + 4 * (tid % QPR));
+#pragma unroll
+  for (int e = 0; e < EPR; ++e) {
+    const int i = tid + NTH * e, row = i / QPR, cq = i - row * QPR;
     const float* pr = red + row * NC + 4 * cq;
     floatx4 v = *reinterpret_cast<const floatx4*>(pr);
 #pragma unroll
     for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const floatx4*>(pr + w * T * NC);
-    const int32_t dst = perm[tile * T + row];
-    if (dst >= 0) *reinterpret_cast<floatx4*>(out + (int64_t)dst * c_out + cy * NC + 4 * cq) = v;
+    const int32_t dst = epd[e];
+    if (dst >= 0) {
+      *reinterpret_cast<floatx4*>(out + (int64_t)dst * c_out + cy * NC + 4 * cq) = v;
+      ea.add_x(epi, v, epx[e]);
+    }
+  }
+  {
+    ea.wave_reduce<QPR>();
+    double* scr = reinterpret_cast<double*>(ls);  // the index tile is no longer read: NTH / 64 x QPR x 8 doubles
+    static_assert((NTH / 64) * QPR * 8 * 8 <= (int)sizeof(ls), "epilogue scratch must fit the index tile");
+    if (lane < QPR)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) scr[(wave * QPR + lane) * 8 + k] = ea.s[k];
+    __syncthreads();
+    if (tid < QPR * 8) {
+      const int cq = tid >> 3, k = tid & 7;
+      double a = 0.0;
+#pragma unroll
+      for (int w = 0; w < NTH / 64; ++w) a += scr[(w * QPR + cq) * 8 + k];
+      *bn_epi_slot(epi, k >> 2, cy * NC + 4 * cq + (k & 3), tile) = a;
+    }
   }
 }
 
@@ -1535,6 +1594,17 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
                    const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
                    const uint8_t* wave_off, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
                    msp_stream_t stream) {
+  return msp_conv_local_bn(x, c_in, wt, K, flip, c_out, tile_rows, lidx, u_start, u_rows, perm, wave_off, n_rows,
+                           out, ws, ws_bytes, nullptr, stream);
+}
+
+int msp_conv_local_bn(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                      const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
+                      const uint8_t* wave_off, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                      const msp_bn_epilogue* epi, msp_stream_t stream) {
+  MSP_REQUIRE(epi == nullptr || epi->partial != nullptr, "msp_conv_local_bn: epilogue without a partial buffer");
+  MSP_REQUIRE(epi == nullptr || epi->x == nullptr || epi->stats != nullptr,
+              "msp_conv_local_bn: backward epilogue needs the BatchNorm's stats");
   MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0,
               "msp_conv_local: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
   MSP_REQUIRE(K >= 1 && K <= kKMax, "msp_conv_local: K must be in [1, %d] (got %d)", kKMax, K);
@@ -1554,12 +1624,18 @@ int msp_conv_local(const float* x, int c_in, const float* wt, int K, int flip, i
                                                                              (flip >> 1) & 1);
   const int64_t n_pad = n_tiles * tile_rows;
   const unsigned grid = (unsigned)(n_tiles * n_y);
-  if (NT == 2)
-    conv_x6s_kernel<2><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, wave_off,
-                                         n_pad, n_y, out);
-  else
-    conv_x6s_kernel<1><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, wave_off,
-                                         n_pad, n_y, out);
+  const BnEpi be = bn_epi_of(epi, c_out, n_rows);
+#define X6S(N, E)                                                                                                \
+  conv_x6s_kernel<N, 0, 1, 1, E><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows, perm, \
+                                                     wave_off, n_pad, n_y, out, be)
+  if (NT == 2) {
+    if (epi) X6S(2, true);
+    else X6S(2, false);
+  } else {
+    if (epi) X6S(1, true);
+    else X6S(1, false);
+  }
+#undef X6S
   return check_launch("msp_conv_local");
 }
 
@@ -1590,7 +1666,7 @@ int msp_exp_conv_local(int variant, const float* x, int c_in, const float* wt, i
 #define EV(A, C, W)                                                                                            \
   if (wbv == W && variant / 100 == A && (variant / 10) % 10 == C) {                                            \
     conv_x6s_kernel<2, A, C, W><<<grid, 512, 0, s>>>(x, c_in, img, K, flip & 1, c_out, lidx, u_start, u_rows,  \
-                                                     perm, wo, n_pad, n_y, out);                               \
+                                                     perm, wo, n_pad, n_y, out, BnEpi{});                      \
     return check_launch("msp_exp_conv_local");                                                                 \
   }
   EV(0, 0, 1) EV(0, 1, 1) EV(1, 0, 1) EV(1, 1, 1) EV(4, 0, 1) EV(5, 0, 1) EV(8, 1, 1) EV(0, 1, 2)

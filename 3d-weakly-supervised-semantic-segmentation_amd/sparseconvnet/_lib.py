@@ -24,6 +24,11 @@ class WeightImage(ctypes.Structure):
                 ("K", ctypes.c_int32), ("c_in", ctypes.c_int32), ("c_out", ctypes.c_int32), ("p", ctypes.c_int32),
                 ("wlay", ctypes.c_int32)]
 
+class BnEpilogue(ctypes.Structure):
+    """msp_bn_epilogue (include/mi3dsparse.h)."""
+    _fields_ = [("partial", c_void_p), ("x", c_void_p), ("stats", c_void_p), ("leak", c_float)]
+
+
 # name -> (restype, argtypes); mirrors include/mi3dsparse.h one to one
 PROTOTYPES = {
     "msp_abi_version": (I, []),
@@ -84,6 +89,11 @@ PROTOTYPES = {
     "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),
+    "msp_conv_bn_parts": (I64, [I64]),
+    "msp_conv_local_bn": (I, [P, I, P, I, I, I, I, P, P, P, P, P, I64, P, P, SZ, P, P]),
+    "msp_conv_tile_bn": (I, [P, I, P, I, I, I, I, P, P, P, P, I64, P, P, SZ, P, P]),
+    "msp_bn_finalize_cm": (I, [P, I64, I64, I, D, D, I, P, P, P, P, P, P]),
+    "msp_bn_bwd_apply_cm": (I, [P, P, I64, I, P, I64, P, P, F, I, P, P, P, P, P]),
     "msp_join_cols": (I, [P, I, P, I, I64, P, P, P]),
     "msp_split_cols": (I, [P, I64, I, I, P, P, P]),
     "msp_nin_gemm_ok": (I, [I64, I, I]),

@@ -128,10 +128,21 @@ class SubmanifoldConvolution(_ConvBase):
     def forward(self, input):
         size = input.size_int
         rules = input.metadata.level(size).subm_rules(int(self.filter_size[0]))
-        f = ops.SubmanifoldConvFunction.apply(input.features, self.weight, rules)
+        # BatchNorm epilogues (ops.FUSE_BN_STATS): the BN whose output this is gets its backward sums from this
+        # convolution's backward-data; a training-mode BN right after it (Sequential sets _bn_next) its forward
+        # sums from this forward
+        bl = getattr(input, "_bn_link", None)
+        link = bl[1] if (bl is not None and bl[0] is input.features) else None
+        parts = None
+        if self.__dict__.get("_bn_next") and self.bias is None and input.features.is_cuda:
+            parts = ops.BnParts(self.nOut, input.features.size(0), input.features.device)
+        f = ops.SubmanifoldConvFunction.apply(input.features, self.weight, rules, link, parts)
         f = self._bias(f)
         _count(rules.n_rules * self.nIn * self.nOut, f)
-        return SparseConvNetTensor(f, input.metadata, input.spatial_size)
+        out = SparseConvNetTensor(f, input.metadata, input.spatial_size)
+        if parts is not None and parts.written:
+            out._bn_partial = (f, parts)
+        return out
 
 
 class Convolution(_ConvBase):
@@ -144,11 +155,17 @@ class Convolution(_ConvBase):
     def forward(self, input):
         stride = int(self.filter_stride[0])
         coarse, rules = input.metadata.downsample(input.size_int, stride)
-        f = ops.ConvolutionFunction.apply(input.features, self.weight, rules, coarse.n)
+        parts = None
+        if self.__dict__.get("_bn_next") and self.bias is None and input.features.is_cuda:
+            parts = ops.BnParts(self.nOut, coarse.n, input.features.device)
+        f = ops.ConvolutionFunction.apply(input.features, self.weight, rules, coarse.n, parts)
         f = self._bias(f)
         _count(input.features.size(0) * self.nIn * self.nOut, f)
         size = (input.spatial_size - self.filter_size) // self.filter_stride + 1
-        return SparseConvNetTensor(f, input.metadata, size)
+        out = SparseConvNetTensor(f, input.metadata, size)
+        if parts is not None and parts.written:
+            out._bn_partial = (f, parts)
+        return out
 
 
 class Deconvolution(_ConvBase):
@@ -161,7 +178,9 @@ class Deconvolution(_ConvBase):
     def forward(self, input):
         stride = int(self.filter_stride[0])
         fine, rules = input.metadata.upsample_rules(input.size_int, stride)
-        f = ops.DeconvolutionFunction.apply(input.features, self.weight, rules, fine.n)
+        bl = getattr(input, "_bn_link", None)
+        link = bl[1] if (bl is not None and bl[0] is input.features) else None
+        f = ops.DeconvolutionFunction.apply(input.features, self.weight, rules, fine.n, link)
         f = self._bias(f)
         _count(fine.n * self.nIn * self.nOut, f)
         size = (input.spatial_size - 1) * self.filter_stride + self.filter_size
@@ -237,8 +256,12 @@ class BatchNormalization(nn.Module):
     def forward(self, input):
         if input.features.size(1) != self.nPlanes:
             raise ValueError(f"BatchNormalization({self.nPlanes}) got {input.features.size(1)} channels")
+        # a training-mode BN hands its consumer a link: a submanifold convolution's backward-data then leaves
+        # this BN's backward sums (ops.BnLink)
+        link = ops.BnLink(self.leakiness) if (ops.FUSE_BN_STATS and self.training and input.features.is_cuda) \
+            else None
         args = (self.weight, self.bias, self.running_mean, self.running_var, self.eps, self.momentum,
-                float(self.leakiness), self.training, self._joined_partial(input))
+                float(self.leakiness), self.training, self._joined_partial(input), link)
         if self.__dict__.pop("_fork", False):
             # residual fork requested by ConcatTable: x is handed on to the shortcut through the Function so
             # the shortcut's gradient of x is added inside the BN backward (ops.BatchNormForkFunction)
@@ -246,7 +269,10 @@ class BatchNormalization(nn.Module):
             self._fork_shortcut = SparseConvNetTensor(xs, input.metadata, input.spatial_size)
         else:
             f = ops.BatchNormFunction.apply(input.features, *args)
-        return SparseConvNetTensor(f, input.metadata, input.spatial_size)
+        out = SparseConvNetTensor(f, input.metadata, input.spatial_size)
+        if link is not None:
+            out._bn_link = (f, link)
+        return out
 
     def _joined_partial(self, input):
         """Batch-statistic partials a residual join left on its output (AddTable), if they are for exactly
@@ -279,10 +305,51 @@ class BatchNormLeakyReLU(BatchNormalization):
 
 
 # ------------------------------------------------------------------ containers
+def _leading_bn(m):
+    """The BatchNormalization that consumes a module's input first: m itself, the first child of a Sequential, or
+    the BN of a residual fork (ConcatTable(shortcut, Sequential(BN, ...)), which runs its BN first), recursively;
+    None otherwise."""
+    while True:
+        if isinstance(m, Sequential) and len(m) > 0:
+            m = m[0]
+        elif isinstance(m, ConcatTable) and _fork_bn(list(m._modules.values())) is not None:
+            m = _fork_bn(list(m._modules.values()))
+        else:
+            return m if isinstance(m, BatchNormalization) else None
+
+
+def _fork_bn(mods):
+    """The BN of a residual fork (shortcut, Sequential(BatchNorm, ...)) that ConcatTable runs fused, or None."""
+    if FUSE_RESIDUAL and len(mods) == 2 and isinstance(mods[1], nn.Sequential) and len(mods[1]) > 0 \
+            and type(mods[1][0]).forward is BatchNormalization.forward:
+        return mods[1][0]
+    return None
+
+
 class Sequential(nn.Sequential):
     def add(self, module):
         self._modules[str(len(self._modules))] = module
         return self
+
+    def forward(self, input):
+        return _chain(list(self._modules.values()), input)
+
+
+def _chain(mods, input):
+    """Run mods in order (Sequential); a SubmanifoldConvolution followed by a training-mode BatchNorm leaves that
+    BN's forward sums in its epilogue (_bn_next, ops.FUSE_BN_STATS)."""
+    for i, m in enumerate(mods):
+        if ops.FUSE_BN_STATS and type(m) in (SubmanifoldConvolution, Convolution) and i + 1 < len(mods):
+            bn = _leading_bn(mods[i + 1])
+            if bn is not None and bn.training:
+                m._bn_next = True
+                try:
+                    input = m(input)
+                finally:
+                    m.__dict__.pop("_bn_next", None)
+                continue
+        input = m(input)
+    return input
 
 
 # Residual fork / join fusions (ops.BatchNormForkFunction, ops.ResidualJoinFunction); False = SCN's
@@ -304,13 +371,10 @@ class ConcatTable(nn.Module):
         mods = list(self._modules.values())
         # residual fork (shortcut, Sequential(BatchNorm..., ...)): the BN runs first and hands x on to the
         # shortcut, so x's two gradients are summed inside the BN backward (ops.BatchNormForkFunction)
-        if FUSE_RESIDUAL and len(mods) == 2 and isinstance(mods[1], nn.Sequential) and len(mods[1]) > 0 \
-                and type(mods[1][0]).forward is BatchNormalization.forward and input.features.is_cuda:
+        if _fork_bn(mods) is not None and input.features.is_cuda:
             y, xs = mods[1][0].forward_fork(input)
             out = mods[0](xs)
-            for m in list(mods[1])[1:]:
-                y = m(y)
-            return [out, y]
+            return [out, _chain(list(mods[1])[1:], y)]
         return [m(input) for m in mods]
 
 

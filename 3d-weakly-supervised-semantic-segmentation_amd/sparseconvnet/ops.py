@@ -8,6 +8,7 @@ are zero-padded to the MFMA chunk width here and sliced back.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -110,15 +111,73 @@ def prepare(rules, purpose, c_in, c_out):
         rules.pairs.fill()
 
 
-def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
+# ------------------------------------------------------------------ BatchNorm statistics in convolution epilogues
+# The BN -> SubM -> BN -> SubM chains of the residual blocks (models/SparseConvNet.py:63-69): the submanifold
+# convolution that feeds a training-mode BatchNorm leaves that BN's forward sums in its epilogue, and the
+# backward-data of the convolution a BatchNorm feeds leaves that BN's backward sums (msp_bn_epilogue), so the BN
+# skips its own statistics pass over the rows.  Off by default (MI3DSPARSE_BN_EPILOGUE=1 turns it
+# on): the BN family drops from 9.0 to 7.5 ms/step but the convolutions' epilogues cost more than that -- 50.08-50.20
+# vs 49.80-49.89 ms/step, interleaved on one box (profiles/r06/ab_r06g_bnepi_on_off.txt).
+FUSE_BN_STATS = os.environ.get("MI3DSPARSE_BN_EPILOGUE", "0") == "1"
+
+
+class BnParts:
+    """Channel-major BatchNorm partial sums [2][C][P] (+ the [2][C] tail msp_bn_bwd_apply_cm writes) that a
+    convolution epilogue fills, one slot per 128-row tile; `written` once a call filled them."""
+    __slots__ = ("buf", "P", "C", "written")
+
+    def __init__(self, C, n_rows, device):
+        self.C = int(C)
+        self.P = int(_lib.query("msp_conv_bn_parts", _lib.I64(n_rows)))
+        self.buf = torch.empty(max(2 * self.C * (self.P + 1), 1), dtype=torch.float64, device=device)
+        self.written = False
+
+
+class BnLink:
+    """A training-mode BatchNorm-ReLU whose output a submanifold convolution consumes: the BN's forward fills
+    x / stats; the convolution's backward-data, when its form has the epilogue, leaves the BN's backward sums in
+    `bwd` = (the gradient tensor it returned, BnParts); the BN's backward uses them when the gradient it receives
+    is that very tensor (one consumer)."""
+    __slots__ = ("leak", "x", "stats", "bwd")
+
+    def __init__(self, leak):
+        self.leak = float(leak)
+        self.x = self.stats = self.bwd = None
+
+
+def bn_epi_ok(rules, n_rows, c_in, c_out, K):
+    """Whether the convolution over `rules` for these sizes runs a form with the BatchNorm epilogue (the
+    tile-local form, or the per-wave tiles of msp_conv_tile)."""
+    if not n_rows:
+        return False
+    f = conv_form(rules, n_rows, c_in, c_out, K)
+    if f == "local":
+        return True
+    if f == "nbr":
+        return False
+    return int(_lib.query("msp_conv_tile_form", _lib.I64(n_rows), c_in, c_out, f)) == 1
+
+
+def _epi_arg(epi):
+    """ctypes pointer to an msp_bn_epilogue for epi = (BnParts, BN input x or None, BN stats or None, leak)."""
+    parts, xb, stats, leak = epi
+    e = _lib.BnEpilogue(parts.buf.data_ptr(), xb.data_ptr() if xb is not None else None,
+                        stats.data_ptr() if stats is not None else None, float(leak))
+    return ctypes.byref(e)  # keeps e alive with the pointer
+
+
+def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0, epi=None):
     """Output-stationary convolution over the rulebook's tile form; the tile
     height (and so which rulebook) is the library's choice for these channel
-    counts (msp_conv_tile_rows)."""
+    counts (msp_conv_tile_rows).  epi: the BatchNorm epilogue (bn_epi_ok must hold)."""
     c_in = x.size(1)
     rules.note_use("conv", c_in, c_out)
     f = conv_form(rules, n_rows, c_in, c_out, K)
     if f == "local":
-        return conv_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops)
+        return conv_local(x, wt, K, flip, c_out, rules, n_rows, kind, flops, epi)
+    if epi is not None and (f == "nbr" or not n_rows or
+                            int(_lib.query("msp_conv_tile_form", _lib.I64(n_rows), c_in, c_out, f)) != 1):
+        raise RuntimeError("conv_tile: the BatchNorm epilogue needs the tile-local or per-wave form (bn_epi_ok)")
     if f == "nbr":
         perm, nbr_p = rules.dense_order()
         return conv_nbr(x, wt, K, flip, c_out, nbr_p, n_rows, kind, flops, perm)
@@ -136,16 +195,24 @@ def conv_tile(x, wt, K, flip, c_out, rules, n_rows, kind="conv_tile", flops=0):
         # offsets, 16 x (int32 src + uint16 row) per chunk, tile starts)
         nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
             tiles["n_chunks"] * (1 + 16 * 6) + 8 * (tiles["tile_start"].numel())
-        _record(kind, flops, lambda: call(
-            "msp_conv_tile", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tr, ptr(tiles["tile_start"]),
-            ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), n_rows, ptr(out),
-            ptr(ws), wsb, _stream(x)), nbytes)
+        if epi is None:
+            _record(kind, flops, lambda: call(
+                "msp_conv_tile", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tr, ptr(tiles["tile_start"]),
+                ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), n_rows, ptr(out),
+                ptr(ws), wsb, _stream(x)), nbytes)
+        else:  # + the epilogue's read of the BN input rows (backward)
+            ea = _epi_arg(epi)
+            _record(kind, flops, lambda: call(
+                "msp_conv_tile_bn", ptr(x), c_in, ptr(wt), K, int(flip), c_out, tr, ptr(tiles["tile_start"]),
+                ptr(tiles["chunk_off"]), ptr(tiles["chunk_src"]), ptr(tiles["chunk_row"]), n_rows, ptr(out),
+                ptr(ws), wsb, ea, _stream(x)), nbytes + (4 * n_rows * c_out if epi[1] is not None else 0))
+            epi[0].written = True
     return out[:n_rows]
 
 
-def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0):
+def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0, epi=None):
     """Submanifold convolution over the tile-local rulebook (SubmRules.local): each 128-row tile's distinct
-    input rows staged in LDS and split once (msp_conv_local)."""
+    input rows staged in LDS and split once (msp_conv_local); epi: the BatchNorm epilogue (msp_conv_local_bn)."""
     c_in = x.size(1)
     loc = rules.local()
     out = torch.empty((max(n_rows, 1), c_out), dtype=torch.float32, device=x.device)
@@ -154,11 +221,20 @@ def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0)
     # compulsory bytes: input rows, output rows, weights, the tile-local rulebook
     nbytes = 4 * (x.size(0) * c_in + n_rows * c_out + K * c_in * c_out) + \
         4 * loc["total"] + 2 * K * loc["n_tiles"] * loc["tile_rows"] + 4 * loc["n_tiles"] * loc["tile_rows"]
-    _record(_shape(kind + "/x6s", c_in, c_out, n_rows), flops, lambda: call(
-        "msp_conv_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
-        ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), ptr(loc.get("wave_off")), n_rows, ptr(out),
-        ptr(ws), wsb, _stream(x)),
-        nbytes)
+    if epi is None:
+        _record(_shape(kind + "/x6s", c_in, c_out, n_rows), flops, lambda: call(
+            "msp_conv_local", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
+            ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), ptr(loc.get("wave_off")), n_rows, ptr(out),
+            ptr(ws), wsb, _stream(x)),
+            nbytes)
+    elif n_rows:  # + the epilogue's read of the BN input rows (backward)
+        ea = _epi_arg(epi)
+        _record(_shape(kind + "/x6s", c_in, c_out, n_rows), flops, lambda: call(
+            "msp_conv_local_bn", ptr(x), c_in, ptr(wt), K, int(flip), c_out, loc["tile_rows"], ptr(loc["lidx"]),
+            ptr(loc["u_start"]), ptr(loc["u_rows"]), ptr(loc["perm"]), ptr(loc.get("wave_off")), n_rows, ptr(out),
+            ptr(ws), wsb, ea, _stream(x)),
+            nbytes + (4 * n_rows * c_out if epi[1] is not None else 0))
+        epi[0].written = True
     return out[:n_rows]
 
 
@@ -281,10 +357,14 @@ class SubmanifoldConvFunction(torch.autograd.Function):
     """out[i] = sum_o W[o]^T x[nbr(i, o)] over the active set."""
 
     @staticmethod
-    def forward(ctx, x, weight, rules):
+    def forward(ctx, x, weight, rules, link=None, parts=None):
+        """link: BnLink of the BatchNorm whose output x is (its backward sums from this convolution's
+        backward-data); parts: BnParts for the forward sums of the output, for the BatchNorm it feeds (filled
+        when the form has the epilogue: parts.written)."""
         _check_feats(x)
         K, _, cin, cout = weight.shape
         V = x.size(0)
+        ctx.link = None
         nbr = getattr(rules, "nbr", None)
         if nbr is not None and int(_lib.query("msp_conv_narrow_in_ok", K, cin, cout)):
             # the colour input layer (c_in <= 4): straight from the neighbour map, no channel padding
@@ -301,10 +381,15 @@ class SubmanifoldConvFunction(torch.autograd.Function):
         xp = _pad_cols(x.contiguous(), cin_p)
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
         # flip bit 1: the weights in their own [K][c_in][c_out] layout (no transposed copy)
+        epi = None
+        if parts is not None and cout_p == cout and parts.C == cout and bn_epi_ok(rules, V, cin_p, cout_p, K):
+            epi = (parts, None, None, 0.0)
         out = conv_tile(xp, wp, K, 2, cout_p, rules, V, "subm_fwd",
-                        2.0 * rules.n_rules * cin * cout)
+                        2.0 * rules.n_rules * cin * cout, epi=epi)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims, ctx.narrow = rules, (cin, cout), False
+        if link is not None and cin_p == cin:
+            ctx.link = link
         return out if cout_p == cout else out[:, :cout].contiguous()
 
     @staticmethod
@@ -330,12 +415,20 @@ class SubmanifoldConvFunction(torch.autograd.Function):
                 dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, flops)
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
-            dxp = conv_tile(g, wp, K, 1, cin_p, rules, xp.size(0), "subm_bwd_data",
-                            2.0 * rules.n_rules * cin * cout)
+            V = xp.size(0)
+            link, epi = ctx.link, None
+            if link is not None and link.x is not None and bn_epi_ok(rules, V, cout_p, cin_p, K):
+                # the BatchNorm that produced x gets its backward sums from this call's epilogue
+                epi = (BnParts(cin_p, V, g.device), link.x, link.stats, link.leak)
+            dxp = conv_tile(g, wp, K, 1, cin_p, rules, V, "subm_bwd_data",
+                            2.0 * rules.n_rules * cin * cout, epi=epi)
+            if epi is not None:
+                link.bwd = (dxp, epi[0])
             dx = dxp if cin_p == cin else dxp[:, :cin]
         if join is not None:
             join()
-        return dx, dw, None
+        ctx.link = None
+        return dx, dw, None, None, None
 
     @staticmethod
     def _backward_narrow(ctx, gout):
@@ -359,7 +452,7 @@ class SubmanifoldConvFunction(torch.autograd.Function):
             dxp = conv_tile(_pad_cols(g, cout_p), wp, K, 1, cin_p, rules, V, "subm_bwd_data",
                             2.0 * rules.n_rules * cin * cout)
             dx = dxp[:, :cin]
-        return dx, dw, None
+        return dx, dw, None, None, None
 
 
 # ------------------------------------------------------------------ strided convolution
@@ -367,13 +460,18 @@ class ConvolutionFunction(torch.autograd.Function):
     """Strided conv, filter_size == stride: out[p] = sum_o W[o]^T x[child(p, o)] (§8(a) a7)."""
 
     @staticmethod
-    def forward(ctx, x, weight, rules, n_coarse):
+    def forward(ctx, x, weight, rules, n_coarse, parts=None):
+        """parts: BnParts for the forward sums of the output, for the BatchNorm it feeds (SubmanifoldConvFunction)."""
         _check_feats(x)
         K, _, cin, cout = weight.shape
         cin_p, cout_p = _pad16(cin), _pad16(cout)
         xp = _pad_cols(x.contiguous(), cin_p)
         wp = _pad_weight(weight.reshape(K, cin, cout), cin_p, cout_p)
-        out = conv_tile(xp, wp, K, 2, cout_p, rules, n_coarse, "conv_fwd", 2.0 * x.size(0) * cin * cout)
+        epi = None
+        if parts is not None and cout_p == cout and parts.C == cout and \
+                bn_epi_ok(rules, n_coarse, cin_p, cout_p, K):
+            epi = (parts, None, None, 0.0)
+        out = conv_tile(xp, wp, K, 2, cout_p, rules, n_coarse, "conv_fwd", 2.0 * x.size(0) * cin * cout, epi=epi)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims = rules, (cin, cout)
         return out if cout_p == cout else out[:, :cout].contiguous()
@@ -398,7 +496,7 @@ class ConvolutionFunction(torch.autograd.Function):
             dx = dxp if cin_p == cin else dxp[:, :cin]
         if join is not None:
             join()
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class DeconvolutionFunction(torch.autograd.Function):
@@ -406,7 +504,8 @@ class DeconvolutionFunction(torch.autograd.Function):
     out[fine] = W[o]^T x[parent(fine)]."""
 
     @staticmethod
-    def forward(ctx, x, weight, rules, n_fine):
+    def forward(ctx, x, weight, rules, n_fine, link=None):
+        """link: BnLink of the BatchNorm whose output x is (its backward sums from the backward-data's epilogue)."""
         _check_feats(x)
         K, _, cin, cout = weight.shape
         cin_p, cout_p = _pad16(cin), _pad16(cout)
@@ -418,6 +517,7 @@ class DeconvolutionFunction(torch.autograd.Function):
         out = conv_pairs(xp, wt, K, cout_p, p, p.pair_out, p.pair_in, n_fine, "deconv_fwd", 2.0 * p.total * cin * cout)
         ctx.save_for_backward(xp, wp)
         ctx.rules, ctx.dims = rules, (cin, cout)
+        ctx.link = link if (link is not None and cin_p == cin) else None
         return out if cout_p == cout else out[:, :cout].contiguous()
 
     @staticmethod
@@ -433,12 +533,19 @@ class DeconvolutionFunction(torch.autograd.Function):
             dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K, 2.0 * p.total * cin * cout, "wgrad_deconv")
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
-            dxp = conv_tile(g, wp, K, 0, cin_p, rules, xp.size(0), "deconv_bwd_data",
-                            2.0 * g.size(0) * cin * cout)
+            V = xp.size(0)
+            link, epi = ctx.link, None
+            if link is not None and link.x is not None and bn_epi_ok(rules, V, cout_p, cin_p, K):
+                epi = (BnParts(cin_p, V, g.device), link.x, link.stats, link.leak)
+            dxp = conv_tile(g, wp, K, 0, cin_p, rules, V, "deconv_bwd_data",
+                            2.0 * g.size(0) * cin * cout, epi=epi)
+            if epi is not None:
+                link.bwd = (dxp, epi[0])
             dx = dxp if cin_p == cin else dxp[:, :cin]
         if join is not None:
             join()
-        return dx, dw, None, None
+        ctx.link = None
+        return dx, dw, None, None, None
 
 
 # ------------------------------------------------------------------ network-in-network
@@ -543,37 +650,63 @@ def _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, tra
     y = torch.empty_like(x)
 
     def run(partial=partial):
-        if partial is None:
-            partial = _bn_partial_buf(V, C, x.device)
-            if train:
-                call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
-        call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train), ptr(running_mean),
-             ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
+        if isinstance(partial, BnParts):  # the producing convolution's epilogue sums (channel-major)
+            call("msp_bn_finalize_cm", ptr(partial.buf), partial.P, V, C, float(eps), float(momentum), int(train),
+                 ptr(running_mean), ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
+        else:
+            if partial is None:
+                partial = _bn_partial_buf(V, C, x.device)
+                if train:
+                    call("msp_bn_stats", ptr(x), V, C, ptr(partial), s)
+            call("msp_bn_finalize", ptr(partial), V, C, float(eps), float(momentum), int(train),
+                 ptr(running_mean), ptr(running_var), ptr(weight), ptr(bias), ptr(stats), s)
         call("msp_bn_apply", ptr(x), V, C, ptr(stats), float(leak), ptr(y), s)
     # compulsory bytes: statistics pass (read x) unless a join produced them, apply (read x, write y)
     _record(_shape("bn_fwd/hbm", C, C, V), 0, run, 4 * V * C * (3 if (partial is None and train) else 2))
     return y, stats
 
 
-def _bn_bwd(x, weight, stats, cfg, gy, addend):
-    """dx (+ addend, fused), dweight, dbias."""
+def _bn_bwd(x, weight, stats, cfg, gy, addend, link=None):
+    """dx (+ addend, fused), dweight, dbias.  link: the BnLink whose consumer's backward-data may have left this
+    BN's backward sums (used when gy is exactly the gradient that call returned)."""
     leak, train, has_w, has_b = cfg
     gy = gy.contiguous()
     V, C = x.shape
     s = _stream(x)
-    partial = _bn_partial_buf(V, C, x.device)
+    parts = None
+    if link is not None and link.bwd is not None:
+        d, p = link.bwd
+        link.bwd = None
+        if p.written and d.data_ptr() == gy.data_ptr() and tuple(d.shape) == tuple(gy.shape) and p.C == C:
+            parts = p
     dx = torch.empty_like(x)
     dw = torch.empty(C, dtype=torch.float32, device=x.device)
     db = torch.empty(C, dtype=torch.float32, device=x.device)
+    add = ptr(addend) if addend is not None else None
+    wp = ptr(weight) if has_w else None
+    if parts is not None:
+        # compulsory bytes: apply only (read x, dy [, shortcut grad], write dx); the sums came with dy
+        _record(_shape("bn_bwd/hbm", C, C, V), 0, lambda: call(
+            "msp_bn_bwd_apply_cm", ptr(x), ptr(gy), V, C, ptr(parts.buf), parts.P, ptr(stats), wp, leak, train, add,
+            ptr(dx), ptr(dw), ptr(db), s), 4 * V * C * (3 + (addend is not None)))
+        return dx, (dw if has_w else None), (db if has_b else None)
+    partial = _bn_partial_buf(V, C, x.device)
 
     def run():
         call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
-        call("msp_bn_bwd_apply_add", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats),
-             ptr(weight) if has_w else None, leak, train, ptr(addend) if addend is not None else None, ptr(dx),
+        call("msp_bn_bwd_apply_add", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats), wp, leak, train, add, ptr(dx),
              ptr(dw), ptr(db), s)
     # compulsory bytes: statistics pass (read x, dy), apply (read x, dy [, shortcut grad], write dx)
     _record(_shape("bn_bwd/hbm", C, C, V), 0, run, 4 * V * C * (5 + (addend is not None)))
     return dx, (dw if has_w else None), (db if has_b else None)
+
+
+def _link(link, x, stats, train):
+    """The BnLink of a training-mode BN forward, filled with its input and statistics (else None)."""
+    if link is None or not train:
+        return None
+    link.x, link.stats = x, stats
+    return link
 
 
 class BatchNormFunction(torch.autograd.Function):
@@ -581,19 +714,22 @@ class BatchNormFunction(torch.autograd.Function):
     `partial`: precomputed batch-statistic partials of x (ResidualJoinFunction)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial=None,
+                link=None):
         _check_feats(x)
         x = x.contiguous()
         y, stats = _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial)
         ctx.save_for_backward(x, weight, stats)
         ctx.cfg = (float(leak), int(train), weight is not None, bias is not None)
+        ctx.link = _link(link, x, stats, train)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, weight, stats = ctx.saved_tensors
-        dx, dw, db = _bn_bwd(x, weight, stats, ctx.cfg, gy, None)
-        return dx, dw, db, None, None, None, None, None, None, None
+        dx, dw, db = _bn_bwd(x, weight, stats, ctx.cfg, gy, None, ctx.link)
+        ctx.link = None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 class BatchNormForkFunction(torch.autograd.Function):
@@ -604,24 +740,27 @@ class BatchNormForkFunction(torch.autograd.Function):
     (msp_bn_bwd_apply_add) instead of autograd's separate accumulation add."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial=None,
+                link=None):
         _check_feats(x)
         x = x.contiguous()
         ctx.set_materialize_grads(False)
         y, stats = _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial)
         ctx.save_for_backward(x, weight, stats)
         ctx.cfg = (float(leak), int(train), weight is not None, bias is not None)
+        ctx.link = _link(link, x, stats, train)
         return y, x.view_as(x)
 
     @staticmethod
     def backward(ctx, gy, gx):
         x, weight, stats = ctx.saved_tensors
+        link, ctx.link = ctx.link, None
         if gy is None:
-            return gx, None, None, None, None, None, None, None, None, None
+            return gx, None, None, None, None, None, None, None, None, None, None
         if gx is not None:
             gx = gx.contiguous()
-        dx, dw, db = _bn_bwd(x, weight, stats, ctx.cfg, gy, gx)
-        return dx, dw, db, None, None, None, None, None, None, None
+        dx, dw, db = _bn_bwd(x, weight, stats, ctx.cfg, gy, gx, link)
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 class ResidualJoinFunction(torch.autograd.Function):

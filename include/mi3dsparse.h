@@ -372,6 +372,42 @@ int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* su
  * NULL). */
 int msp_join_cols(const float* a, int ca, const float* b, int cb, int64_t V, float* out, double* partial,
                   msp_stream_t stream);
+/* BatchNormalization statistics from a convolution's epilogue (round 6; the BN -> SubM -> BN -> SubM chains of
+ * models/SparseConvNet.py:63-69).  msp_conv_local_bn / msp_conv_tile_bn are msp_conv_local / msp_conv_tile plus,
+ * when epi is non-NULL, per-channel fp64 sums of the rows they write, one slot per 128-row tile, into the
+ * channel-major buffer epi->partial[2][C][P] (C = c_out, P = msp_conv_bn_parts(n_rows); the buffer holds
+ * 2 * C * (P + 1) doubles, the tail for msp_bn_bwd_apply_cm's totals):
+ *   epi->x == NULL (forward): (sum v, sum v^2) of the output rows v -- msp_bn_stats' sums of the output, for the
+ *     BatchNormalization the convolution feeds (msp_bn_finalize_cm);
+ *   epi->x != NULL (backward-data): the output is dy, the gradient of the output of the BatchNormalization whose
+ *     input rows are epi->x [n_rows][C] and statistics epi->stats [5][C] (leakiness epi->leak) -- the sums of
+ *     msp_bn_bwd_stats, (sum dz, sum dz * xhat), for msp_bn_bwd_apply_cm.
+ * Sums within a tile are taken in a fixed order and the tiles are added in tile order: deterministic.  The
+ * epilogue is available where msp_conv_tile_form(...) == 1 (per-wave tiles) and on every msp_conv_local call;
+ * msp_conv_tile_bn with epi on another form returns MSP_EINVAL. */
+typedef struct {
+  double* partial;
+  const float* x;
+  const float* stats;
+  float leak;
+} msp_bn_epilogue;
+int64_t msp_conv_bn_parts(int64_t n_rows);
+int msp_conv_local_bn(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                      const uint16_t* lidx, const int64_t* u_start, const int32_t* u_rows, const int32_t* perm,
+                      const uint8_t* wave_off, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                      const msp_bn_epilogue* epi, msp_stream_t stream);
+int msp_conv_tile_bn(const float* x, int c_in, const float* wt, int K, int flip, int c_out, int tile_rows,
+                     const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
+                     const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
+                     const msp_bn_epilogue* epi, msp_stream_t stream);
+/* msp_bn_finalize / msp_bn_bwd_apply_add over a channel-major partial buffer [2][C][P] (+ [2][C] tail) of P
+ * slots, as the epilogue above writes it. */
+int msp_bn_finalize_cm(const double* partial, int64_t P, int64_t V, int C, double eps, double momentum, int train,
+                       float* running_mean, float* running_var, const float* weight, const float* bias,
+                       float* stats, msp_stream_t stream);
+int msp_bn_bwd_apply_cm(const float* x, const float* dy, int64_t V, int C, const double* partial, int64_t P,
+                        const float* stats, const float* weight, float leak, int train, const float* addend,
+                        float* dx, float* dweight, float* dbias, msp_stream_t stream);
 int msp_split_cols(const float* in, int64_t V, int ca, int cb, float* a, float* b, msp_stream_t stream);
 
 /* ---------------- NetworkInNetwork products (replaces SCN's NetworkInNetwork

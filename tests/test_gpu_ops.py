@@ -762,6 +762,35 @@ def test_tile_local_rulebook():
     assert rules.n_rules == int((rules.nbr >= 0).sum()) == rules.pairs.total
 
 
+@pytest.mark.parametrize("n_pts,f", [(1, 3), (1, 5), (7, 3), (300, 5), (5000, 3)])
+def test_subm_map_counted_exact_workspace(n_pts, f):
+    """msp_subm_map_counted with a workspace of exactly msp_subm_map_workspace_size bytes followed by a canary:
+    the kernel's per-block counts stay inside it at every size (the size follows the launch grid; round-5 advice:
+    below ~342 rows the old formula was smaller than what the blocks wrote), and the count equals the map's."""
+    from sparseconvnet import _lib
+    rng = np.random.default_rng(n_pts)
+    coords = torch.from_numpy(rng.integers(0, 12, (n_pts, 4)).astype(np.int64))
+    coords[:, 3] = 0
+    t = scn.InputLayer(3, 16, mode=4)([coords.to(DEV), torch.ones(n_pts, 1, device=DEV)])
+    lvl = t.metadata.level(16)
+    V = lvl.n
+    table, cap = lvl.hash()
+    K = f ** 3
+    wsb = int(_lib.query("msp_subm_map_workspace_size", _lib.I64(V), f))
+    canary = 4096
+    buf = torch.full((wsb + canary,), 0xA5, dtype=torch.uint8, device=DEV)
+    nbr = torch.empty((K, V), dtype=torch.int32, device=DEV)
+    nr = torch.empty(1, dtype=torch.int64, device=DEV)
+    _lib.call("msp_subm_map_counted", _lib.ptr(lvl.keys), V, lvl.log2, lvl.size, f, _lib.ptr(table), cap,
+              _lib.ptr(nbr), _lib.ptr(nr), _lib.ptr(buf), wsb, _lib.stream())
+    torch.cuda.synchronize()
+    assert bool((buf[wsb:] == 0xA5).all()), "msp_subm_map_counted wrote past its workspace"
+    assert int(nr.item()) == int((nbr >= 0).sum())
+    with pytest.raises(RuntimeError, match="workspace too small"):
+        _lib.call("msp_subm_map_counted", _lib.ptr(lvl.keys), V, lvl.log2, lvl.size, f, _lib.ptr(table), cap,
+                  _lib.ptr(nbr), _lib.ptr(nr), _lib.ptr(buf), wsb - 1, _lib.stream())
+
+
 @pytest.mark.parametrize("mode", ["random", "dup", "distinct"])
 @pytest.mark.parametrize("T,K", [(64, 27), (128, 32), (256, 27)])
 def test_tile_local_rulebook_maps(T, K, mode):
