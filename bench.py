@@ -151,7 +151,7 @@ class KernelRecorder:
 def pmc_traffic():
     """HBM bytes per conv-family call measured with rocprofv3 PMC counters on this workload
     (scripts/pmc_traffic.sh; committed under profiles/, newest round first), or None."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         if os.path.isfile(path):
             break

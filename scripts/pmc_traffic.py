@@ -13,6 +13,7 @@ import csv, glob, json, os, sys
 root, out_path = sys.argv[1], sys.argv[2]
 conv_names = ("conv_x6s_kernel", "conv_x6l_kernel", "conv_x6d_kernel", "conv_x6p_kernel", "conv_x6r_kernel", "conv_x6g_kernel", "conv_tile7_kernel", "conv_tilep_kernel", "conv_tile4_kernel", "conv_tile_kernel")
 tot = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
+by_kernel = {}  # short kernel name -> {counter: total KB x 1024, dispatches}
 ndisp = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}
 dur = {"FETCH_SIZE": 0, "WRITE_SIZE": 0}
 for f in sorted(glob.glob(os.path.join(root, "pass*", "**", "*counter_collection.csv"), recursive=True)):
@@ -22,6 +23,10 @@ for f in sorted(glob.glob(os.path.join(root, "pass*", "**", "*counter_collection
         if ctr not in tot:
             continue
         is_conv = any(c + "<" in name or c + "(" in name for c in conv_names)
+        short = name.split("(")[0].replace("void ", "").replace("msp::", "")
+        k = by_kernel.setdefault(short, {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0, "n_FETCH_SIZE": 0, "n_WRITE_SIZE": 0})
+        k[ctr] += float(r["Counter_Value"]) * 1024.0
+        k["n_" + ctr] += 1
         if is_conv or "split_reduce_kernel" in name or "split_weights_kernel" in name or "split_weights_lane_kernel" in name:
             tot[ctr] += float(r["Counter_Value"]) * 1024.0
             if is_conv:
@@ -33,5 +38,18 @@ res = {"kernel": "msp_conv_local / msp_conv_tile / msp_conv_nbr", "calls": ndisp
        "fetch_bytes_per_call": fetch, "write_bytes_per_call": write, "traffic_bytes_per_call": fetch + write,
        "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE in separate runs of "
                "`bench.py --steps 2 --warmup 1 --no-cpu`; conv kernel + split_weights(_lane) + split_reduce dispatches per call"}
+# per kernel (every kernel of the run): bytes per dispatch and the share of the conv family's traffic
+fam = {}
+for short, k in by_kernel.items():
+    n = max(k["n_FETCH_SIZE"], k["n_WRITE_SIZE"], 1)
+    f, w = 2.0 * k["FETCH_SIZE"], k["WRITE_SIZE"]
+    fam[short] = {"dispatches": n, "fetch_bytes_per_dispatch": f / max(k["n_FETCH_SIZE"], 1),
+                  "write_bytes_per_dispatch": w / max(k["n_WRITE_SIZE"], 1),
+                  "fetch_bytes_per_conv_call": f / max(ndisp["FETCH_SIZE"], 1),
+                  "write_bytes_per_conv_call": w / max(ndisp["WRITE_SIZE"], 1)}
+res["by_kernel"] = dict(sorted(fam.items(), key=lambda kv: -(kv[1]["fetch_bytes_per_conv_call"] +
+                                                             kv[1]["write_bytes_per_conv_call"])))
 json.dump(res, open(out_path, "w"), indent=1)
-print(json.dumps(res, indent=1))
+print(json.dumps({k: v for k, v in res.items() if k != 'by_kernel'}, indent=1))
+for kk, vv in list(res['by_kernel'].items())[:25]:
+    print(f"{vv['fetch_bytes_per_conv_call'] / 1e6:9.2f} {vv['write_bytes_per_conv_call'] / 1e6:9.2f} MB per conv call  {vv['dispatches']:6d}  {kk}")
