@@ -376,8 +376,8 @@ class SubmRules:
             t = self.__dict__.setdefault("_lists", {}).get(tile_rows)
         if t is None:
             self._plan.append(("lists", self._key, tile_rows))
-            t = self._lists[tile_rows] = local_rulebook(self.nbr, self.K, self._n, self.nbr.device,
-                                                        _lib.stream(self.nbr.device), tile_rows, lists_only=True)
+            t = self._lists[tile_rows] = local_rulebook(self._map, self.K, self._n, self._map.device,
+                                                        _lib.stream(self._map.device), tile_rows, lists_only=True)
         return t
 
     def wgrad_index(self, wait=False):
@@ -426,7 +426,7 @@ class SubmRules:
                 _defer().then(decide)
                 return self._wchunk
             self._plan.append(("wchunk", self._key))
-            dev, s = self.nbr.device, _lib.stream(self.nbr.device)
+            dev, s = self._map.device, _lib.stream(self._map.device)
             lr = torch.empty(max(tiles["n_chunks"], 1) * CHUNK, dtype=torch.int32, device=dev)
             over = loc["max_u"] > int(query("msp_wgrad_chunk_cap"))
             n_far = torch.zeros(1, dtype=torch.int64, device=dev) if over else None
@@ -454,7 +454,7 @@ class SubmRules:
         """The chunk weight gradient's index from the full tile-local rulebook (msp_local_chunk_index: count, one
         host read of the chunk total -- deferred in a replay -- then fill): no 128-row tile rulebook and no
         binary searches where a tile-local convolution built that rulebook anyway."""
-        dev, s, n = self.nbr.device, _lib.stream(self.nbr.device), self._n
+        dev, s, n = self._map.device, _lib.stream(self._map.device), self._n
         n_tiles = (n + 127) // 128
         tile_start = torch.empty(n_tiles + 2, dtype=torch.int64, device=dev)
         ws = _ws(query("msp_tile_local_workspace_size", I64(n), 128), dev)
@@ -514,9 +514,16 @@ class DownRules:
         self._map, self._n = self.down, coarse.n
         # pair_in = fine row, pair_out = coarse row, grouped by child offset
         self.pairs = PairLists(self.down, K, coarse.n, dev, s, self._plan, self._key)
+        # the chunk weight gradient over the child map (round 6): 128-coarse-row tiles, each tile's distinct fine
+        # rows staged (ops.ConvolutionFunction / DeconvolutionFunction backward)
+        self._locals = {}
+        self._wchunk = None
 
     tiles_for = SubmRules.tiles_for
     note_use = SubmRules.note_use
+    lists = SubmRules.lists
+    wgrad_index = SubmRules.wgrad_index
+    _local_chunk_index = SubmRules._local_chunk_index
 
 
 class Level:

@@ -250,6 +250,14 @@ def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out, kind="pairs", flops=0):
     return out[:n_out]
 
 
+# Strided-convolution and deconvolution weight gradients on the chunk form over the child map (round 6, opt-in:
+# MI3DSPARSE_STRIDED_WGRAD_CHUNK=1).  Measured slower than the per-offset pair lists on the headline step: the kernels
+# 2.18 / 2.30 vs 1.94 / 2.01 ms per 5 steps (a 128-coarse-row tile names ~2.4 x 128 fine rows, often past the 448
+# staged, and 8 offsets leave the k-steps short), and the child maps' tile rulebooks, distinct-row lists and far-rule
+# lists add ~9 ms of prefetch host time and side-stream work: 61.0 vs 50.0-50.1 ms/step
+# (profiles/r06/ab_r06k_strided_wgrad_chunk.txt).  Kept for its tests (the far-rule path on dense children).
+STRIDED_WGRAD_CHUNK = os.environ.get("MI3DSPARSE_STRIDED_WGRAD_CHUNK", "0") == "1"
+
 _WGRAD_SIDE = {}
 # True: every weight gradient on a side stream beside the backward-data (bench.py --concurrent-wgrad).
 # Off by default: it saved 0.3 ms of 66.9 per step (round 2, eager), inside the box-to-box spread, and the
@@ -487,7 +495,18 @@ class ConvolutionFunction(torch.autograd.Function):
         dx = dw = None
         join = None
         if ctx.needs_input_grad[1]:
-            dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, 2.0 * p.total * cin * cout, "wgrad_strided")
+            flops = 2.0 * xp.size(0) * cin * cout  # one rule per fine row
+            dwp = None
+            if STRIDED_WGRAD_CHUNK:
+                # the chunk weight gradient over the child map: tiles of 128 coarse rows (dy), their children's
+                # distinct fine rows (x) staged once per tile (round 6)
+                rules.note_use("wgrad", cin_p, cout_p)
+                if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(g.size(0)), K, cin_p, cout_p)) and \
+                        rules.wgrad_index(wait=True) is not None:
+                    dwp, join = _on_side(xp, g.size(0), lambda: conv_wgrad_chunk(xp, g, rules, K, "wgrad_strided",
+                                                                                flops))
+            if dwp is None:
+                dwp, join = conv_wgrad_async(xp, g, p, p.pair_in, p.pair_out, K, flops, "wgrad_strided")
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             # dx[fine] = W[o] g[parent]: src = coarse (pair_out), dst = fine (pair_in)
@@ -530,7 +549,18 @@ class DeconvolutionFunction(torch.autograd.Function):
         dx = dw = None
         join = None
         if ctx.needs_input_grad[1]:
-            dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K, 2.0 * p.total * cin * cout, "wgrad_deconv")
+            flops = 2.0 * g.size(0) * cin * cout  # one rule per fine row
+            dwp = None
+            if STRIDED_WGRAD_CHUNK:
+                # the chunk form over the child map with the roles swapped (the coarse input rows are the tiles'
+                # own rows, the fine output gradients the gathered ones): it gives dW^T per offset (round 6)
+                rules.note_use("wgrad", cout_p, cin_p)
+                if int(_lib.query("msp_wgrad_chunk_preferred", _lib.I64(xp.size(0)), K, cout_p, cin_p)) and \
+                        rules.wgrad_index(wait=True) is not None:
+                    dwp, join = _on_side(xp, xp.size(0), lambda: conv_wgrad_chunk(g, xp, rules, K, "wgrad_deconv",
+                                                                                 flops).transpose(1, 2))
+            if dwp is None:
+                dwp, join = conv_wgrad_async(xp, g, p, p.pair_out, p.pair_in, K, flops, "wgrad_deconv")
             dw = dwp[:, :cin, :cout].reshape(K, 1, cin, cout)
         if ctx.needs_input_grad[0]:
             V = xp.size(0)

@@ -115,8 +115,11 @@ def test_subm_conv(cin, cout):
     close(conv_g.weight.grad, conv_o.weight.grad, 1e-5, "subm dW")
 
 
-@pytest.mark.parametrize("stride,cin,cout", [(2, 16, 32), (2, 32, 48), (4, 32, 64)])
+@pytest.mark.parametrize("stride,cin,cout", [(2, 16, 32), (2, 32, 48), (4, 32, 64), (2, 32, 64), (2, 64, 96)])
 def test_strided_conv_deconv_unpool(stride, cin, cout):
+    """Strided convolution, deconvolution, unpooling and max pooling against the oracle, forward and backward.
+    (2, 32, 64) and (2, 64, 96) also run with the chunk weight gradient over the child map for both the
+    convolution and the deconvolution (round 6, opt-in; channels in multiples of 32)."""
     torch.manual_seed(stride + cin)
     coords, feats = _inputs(4000, 40, n_feat=cin)
     g, o = _pair(coords, feats, size=64)
@@ -146,6 +149,74 @@ def test_strided_conv_deconv_unpool(stride, cin, cout):
     close(_to_oracle_order(type(g)(xg.grad, g.metadata, g.spatial_size), o), xo.grad, 1e-5, "dx")
     close(cg.weight.grad, co.weight.grad, 1e-5, "conv dW")
     close(dg.weight.grad, do.weight.grad, 1e-5, "deconv dW")
+    if stride == 2 and cin % 32 == 0 and cout % 32 == 0:  # the opt-in chunk form over the child map
+        from sparseconvnet import ops
+        ops.STRIDED_WGRAD_CHUNK = True
+        try:
+            for m in (cg, dg):
+                m.weight.grad = None
+            xg.grad = None
+            ug2 = dg(cg(g))
+            pg2 = scn.UnPooling(3, stride, stride)(cg(g))
+            mg2 = scn.MaxPooling(3, stride, stride)(g)
+            ((ug2.features * w1.float().to(DEV)).square().sum() + pg2.features.sum() +
+             mg2.features.square().sum()).backward()
+        finally:
+            ops.STRIDED_WGRAD_CHUNK = False
+        close(cg.weight.grad, co.weight.grad, 1e-5, "conv dW (chunk form)")
+        close(dg.weight.grad, do.weight.grad, 1e-5, "deconv dW (chunk form)")
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 64), (64, 32)])
+def test_strided_wgrad_chunk_dense_children(cin, cout):
+    """The chunk weight gradient over the child map where every coarse site has all 8 children (a solid block):
+    a 128-coarse-row tile names up to 1024 distinct fine rows, past the 448 the kernel stages, so most rules go
+    through the far-rule path (msp_wgrad_far_list + msp_conv_wgrad_far).  Convolution and deconvolution weight
+    gradients against fp64 (1e-5 of the max), and the pair-list form agrees."""
+    from sparseconvnet import ops
+    torch.manual_seed(cin + cout)
+    g0 = np.stack(np.meshgrid(*[np.arange(20)] * 3, indexing="ij"), -1).reshape(-1, 3)
+    coords = torch.from_numpy(np.concatenate([g0, np.zeros((len(g0), 1), np.int64)], 1))
+    feats = torch.randn(len(g0), cin)
+    g, o = _pair(coords, feats, size=32)
+    outs = []
+    for chunk in (True, False):
+        ops.STRIDED_WGRAD_CHUNK = chunk
+        try:
+            torch.manual_seed(5)
+            cg = scn.Convolution(3, cin, cout, 2, 2, False).to(DEV)
+            dg = scn.Deconvolution(3, cout, cin, 2, 2, False).to(DEV)
+            xg = g.features.detach().requires_grad_(True)
+            t = type(g)(xg, g.metadata, g.spatial_size)
+            u = dg(cg(t))
+            (u.features * torch.linspace(-1, 1, u.features.numel(), device=DEV).view_as(u.features)).sum().backward()
+            outs.append((cg.weight.grad.clone(), dg.weight.grad.clone()))
+            if chunk:
+                rules = g.metadata.downsample(32, 2)[1]
+                idx = rules.wgrad_index(wait=True)
+                assert idx is not None and idx["n_far"] > 0, "the dense block must exercise the far-rule path"
+        finally:
+            ops.STRIDED_WGRAD_CHUNK = False
+    co = O.Convolution(3, cin, cout, 2, 2, False).double()
+    do = O.Deconvolution(3, cout, cin, 2, 2, False).double()
+    torch.manual_seed(5)
+    co.weight.data.copy_(scn.Convolution(3, cin, cout, 2, 2, False).weight.data.double())
+    do.weight.data.copy_(scn.Deconvolution(3, cout, cin, 2, 2, False).weight.data.double())
+    xo = o.features.detach().requires_grad_(True)
+    uo = do(co(type(o)(xo, o.metadata, o.size)))
+    # the device's loss weights (a linspace over its output rows) in the oracle's row order
+    (uo.features * _device_weights_in_oracle_order(u, uo)).sum().backward()
+    close(outs[0][0], co.weight.grad, 1e-5, "conv dW (chunk form)")
+    close(outs[0][1], do.weight.grad, 1e-5, "deconv dW (chunk form)")
+    close(outs[0][0], outs[1][0], 1e-5, "conv dW chunk vs pairs")
+    close(outs[0][1], outs[1][1], 1e-5, "deconv dW chunk vs pairs")
+
+
+def _device_weights_in_oracle_order(u, uo):
+    """The per-element loss weights the device run used (linspace over its rows), permuted into the oracle's
+    row order."""
+    w = torch.linspace(-1, 1, u.features.numel(), device=DEV).view_as(u.features)
+    return _to_oracle_order(type(u)(w, u.metadata, u.spatial_size), uo).double().cpu()
 
 
 @pytest.mark.parametrize("cin,cout", [(64, 32), (96, 64), (48, 16), (160, 32)])
