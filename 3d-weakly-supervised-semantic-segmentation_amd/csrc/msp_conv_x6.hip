@@ -602,7 +602,7 @@ __global__ __launch_bounds__(kThreads) void conv_x6r_kernel(
     }
   }
   {
-    static_assert(TR == 128 && 64 % V4 == 0, "one epilogue slot per 128-row tile");
+    static_assert(!EPI || (TR == 128 && 64 % V4 == 0), "one epilogue slot per 128-row tile");
     ea.wave_reduce<V4>();
     if (lane < V4)
 #pragma unroll

@@ -1075,7 +1075,10 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
 // PW 1 (the product form): the next k-step's rule words are read from LDS at the start of the current one (within
 // an offset), so a k-step no longer opens with an LDS read -> address -> transposing-read chain: 1-6 % faster at
 // levels 0-3 (profiles/r03/kbexp_r03pw.log); PW 0 reads them at the k-step's start.
-template <int NW, int AC = 1, int PW = 1, int RS = 32>
+// ABL (experiments build only; wrong results): bit 0 keeps the first tile's LDS images for every tile (no split and
+// no image writes after the first tile; the rule words and offsets are still staged), bit 1 drops the next tile's
+// value loads -- the ablations that price the per-tile staging (round 6: -20 %, profiles/r06/kbexp_r06m_x6c_staging.log).
+template <int NW, int AC = 1, int PW = 1, int RS = 32, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -1135,12 +1138,14 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   auto issue_vals = [&](int64_t t) {  // values of tile t (rows in srow) and its rule words
 #pragma unroll
     for (int b = 0; b < XI; ++b) {
+      if ((ABL & 2) && t != t0) break;
       const int u = (tid + NTH * b) & 7;
       xv[b] = floatx4{0.f, 0.f, 0.f, 0.f};
       if (srow[b] >= 0) xv[b] = *reinterpret_cast<const floatx4*>(x + (int64_t)srow[b] * c_in + ci0 + 4 * u);
     }
 #pragma unroll
     for (int b = 0; b < DI; ++b) {
+      if ((ABL & 2) && t != t0) break;
       const int it = tid + NTH * b, u = it & 7;
       const int64_t row = t * kWTile + (it >> 3);
       dv[b] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1155,10 +1160,13 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     }
     co_v = tid < s_nch ? chunk_off[c0 + tid] : 255;
   };
+  bool first_store = true;
   auto store = [&]() {  // the staged tile into LDS (two barriers: offset table)
+    const bool images = !(ABL & 1) || first_store;
+    first_store = false;
 #pragma unroll
     for (int b = 0; b < XI; ++b) {
-      if (srow[b] >= 0) {
+      if (images && srow[b] >= 0) {
         const int it = tid + NTH * b;
         uint2 pc[3];
         split4(xv[b], pc);
@@ -1169,6 +1177,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     }
 #pragma unroll
     for (int b = 0; b < DI; ++b) {
+      if (!images) break;
       const int it = tid + NTH * b;
       uint2 pc[3];
       split4(dv[b], pc);
@@ -1699,6 +1708,12 @@ int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, 
   else if (variant == 43)  // the product form with 72-byte image rows (RS = 36)
     wgrad_x6c_kernel<8, 1, 1, 36><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr,
                                                        u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  else if (variant == 143)  // ablation: no image staging after the first tile
+    wgrad_x6c_kernel<8, 1, 1, 36, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr,
+                                                          u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  else if (variant == 343)  // ablation: no image staging and no value loads after the first tile
+    wgrad_x6c_kernel<8, 1, 1, 36, 3><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr,
+                                                          u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
 
   else {
     set_error("msp_exp_wgrad_chunk: no variant %d", variant);
