@@ -1078,7 +1078,14 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
 // ABL (experiments build only; wrong results): bit 0 keeps the first tile's LDS images for every tile (no split and
 // no image writes after the first tile; the rule words and offsets are still staged), bit 1 drops the next tile's
 // value loads -- the ablations that price the per-tile staging (round 6: -20 %, profiles/r06/kbexp_r06m_x6c_staging.log).
-template <int NW, int AC = 1, int PW = 1, int RS = 32, int ABL = 0>
+// DT 1 (direct offset table, the product since round 6): each chunk's neighbours' offsets come with its own from
+// global memory, so the table of the offsets' chunk ranges is written in the same phase as the images
+// (double-buffered, the idle buffer zeroed there): one block barrier per tile instead of two, 7-15 % faster at
+// levels 0-3 (profiles/r06/kbexp_r06o_x6c_table_balance_split.log).  DT 0: the table built through LDS after the
+// images (round 2-5).  Measured there and not kept: splitting the next tile's values in registers before the
+// barrier (38 VGPRs past the 256 two waves per SIMD allow: spills, 20-40 % slower) and dealing the offsets over the
+// waves by the range's chunk counts (no gain: -2 % to +8 %).
+template <int NW, int AC = 1, int PW = 1, int RS = 32, int ABL = 0, int DT = 0>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -1095,7 +1102,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   __shared__ __attribute__((aligned(16))) uint16_t dim[3 * kWDImg];
   __shared__ uint32_t ent[(kWMaxCh + 1) * 16];  // + one chunk: the partner read of a last odd chunk stays inside
   __shared__ uint8_t offs[kWMaxCh];
-  __shared__ int otab[2][32];
+  __shared__ int otab[2][2][32];  // [buffer][first, end][offset]; DT 0: buffer 0 only
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, p4 = i16 & 3;
@@ -1120,12 +1127,14 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     dim[(i / 32) * kWDImg + kWTile * RS + (i % 32)] = 0;
   }
   if (tid < 16) ent[kWMaxCh * 16 + tid] = (uint32_t)kWCap | ((uint32_t)kWTile << 16);
+  if (DT && tid < 128) otab[tid >> 6][(tid >> 5) & 1][tid & 31] = 0;
+  if (DT) __syncthreads();
 
   // ---- staging registers: rows of tile t + 1 (loaded at the start of t), then its values and rule words
   int32_t srow[XI];
   floatx4 xv[XI], dv[DI];
   uint32_t ev[EI];
-  int co_v = 255, s_nch = 0;
+  int co_v = 255, co_p = 255, co_n = 255, s_nch = 0;
   auto issue_rows = [&](int64_t t) {  // the tile's distinct rows (<= kWCap: checked on the host)
     const int64_t u0 = u_start[t];
     const int nu = (int)(u_start[t + 1] - u0);
@@ -1159,9 +1168,14 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       ev[b] = e < s_nch * 16 ? chunk_lr[c0 * 16 + e] : 0u;
     }
     co_v = tid < s_nch ? chunk_off[c0 + tid] : 255;
+    if (DT) {
+      co_p = tid < s_nch && tid > 0 ? chunk_off[c0 + tid - 1] : 255;
+      co_n = tid + 1 < s_nch ? chunk_off[c0 + tid + 1] : 255;
+    }
   };
+  int buf = 0;  // DT: the offset-table buffer of the staged tile
   bool first_store = true;
-  auto store = [&]() {  // the staged tile into LDS (two barriers: offset table)
+  auto store = [&]() {  // the staged tile into LDS (DT: one barrier; DT 0: two, the offset table through LDS)
     const bool images = !(ABL & 1) || first_store;
     first_store = false;
 #pragma unroll
@@ -1190,13 +1204,22 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       const int e = tid + NTH * b;
       if (e < s_nch * 16) ent[e] = ev[b];
     }
+    if constexpr (DT) {  // this tile's table into buffer buf, the other buffer (read by the last tile) zeroed
+      if (tid < 64) otab[buf ^ 1][tid >> 5][tid & 31] = 0;
+      if (tid < s_nch) {
+        if (co_p != co_v) otab[buf][0][co_v] = tid;
+        if (co_n != co_v) otab[buf][1][co_v] = tid + 1;
+      }
+      __syncthreads();
+      return;
+    }
     if (tid < s_nch) offs[tid] = (uint8_t)co_v;
-    if (tid < 64) otab[tid >> 5][tid & 31] = 0;
+    if (tid < 64) otab[0][tid >> 5][tid & 31] = 0;
     __syncthreads();
     if (tid < s_nch) {
       const int o = offs[tid];
-      if (tid == 0 || offs[tid - 1] != o) otab[0][o] = tid;
-      if (tid == s_nch - 1 || offs[tid + 1] != o) otab[1][o] = tid + 1;
+      if (tid == 0 || offs[tid - 1] != o) otab[0][0][o] = tid;
+      if (tid == s_nch - 1 || offs[tid + 1] != o) otab[0][1][o] = tid + 1;
     }
     __syncthreads();
   };
@@ -1280,8 +1303,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
 #pragma unroll
       for (int a = 0; a < NOW; ++a) {
         const int o = wave + NW * a;
-        first[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[0][o]) : 0;
-        endc[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[1][o]) : 0;
+        first[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[buf][0][o]) : 0;
+        endc[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[buf][1][o]) : 0;
         S[a + 1] = S[a] + (endc[a] - first[a] + 1) / 2;
       }
       const int n_st = S[NOW];
@@ -1305,6 +1328,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       }
       if (n_st == 0 && more) issue_vals(t + 1);
       __syncthreads();  // reads of tile t done
+      if (DT) buf ^= 1;
       if (more) store();
     }
   }
@@ -1523,7 +1547,7 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
   const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
   // 72-byte image rows (RS = 36): 9-15 % faster than the swizzled 64-byte rows at every level
   // (profiles/r05/kbexp_r05m_x6c_row_stride.log)
-  wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
+  wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS, 0, 1><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
       x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
   wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 16), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
@@ -1714,6 +1738,9 @@ int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, 
   else if (variant == 343)  // ablation: no image staging and no value loads after the first tile
     wgrad_x6c_kernel<8, 1, 1, 36, 3><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr,
                                                           u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  else if (variant == 2043)  // the round-6 product: direct offset table (DT)
+    wgrad_x6c_kernel<8, 1, 1, 36, 0, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr,
+                                                             u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
 
   else {
     set_error("msp_exp_wgrad_chunk: no variant %d", variant);

@@ -218,12 +218,19 @@ def main():
                     fs = {k: v for k, v in fs.items() if k in WFORMS.split(",")}
                 if hasattr(ops, "conv_wgrad_unit"):
                     fs["unit"] = lambda: ops.conv_wgrad_unit(x, dy, rules, 27)
-                res = []
+                res, first_x6c = [], None
                 for name, f in fs.items():
                     try:
                         ms = timeit(f)
-                        err = (f().double() - ref).abs().max().item() / scale
-                        res.append(f"{name} {ms:6.3f}ms {flops / ms / 1e9:6.1f}TF {err:.0e}")
+                        out = f()
+                        err = (out.double() - ref).abs().max().item() / scale
+                        same = ""
+                        if name.startswith("x6c_v"):  # bit-identity against the first variant listed
+                            if first_x6c is None:
+                                first_x6c = out
+                            else:
+                                same = " =" if torch.equal(out, first_x6c) else " !="
+                        res.append(f"{name} {ms:6.3f}ms {flops / ms / 1e9:6.1f}TF {err:.0e}{same}")
                     except Exception as e:
                         res.append(f"{name} n/a ({str(e)[:40]})")
                 print(f"  wgrad {cin:3d}x{cout:3d}  " + "  ".join(res), flush=True)
