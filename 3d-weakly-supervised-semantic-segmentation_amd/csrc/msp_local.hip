@@ -1085,7 +1085,12 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
 // images (round 2-5).  Measured there and not kept: splitting the next tile's values in registers before the
 // barrier (38 VGPRs past the 256 two waves per SIMD allow: spills, 20-40 % slower) and dealing the offsets over the
 // waves by the range's chunk counts (no gain: -2 % to +8 %).
-template <int NW, int AC = 1, int PW = 1, int RS = 32, int ABL = 0, int DT = 0>
+// BR > 0 (balanced ranges): the blocks' contiguous tile ranges hold equal cost, chunks + BR per tile (the staging's
+// share), instead of equal tile counts; each block finds its bounds in tile_start (a prefix sum of chunks) with two
+// rounds of block-wide counts.  Still a fixed function of the index: deterministic.  The product runs BR = 128:
+// against equal tile counts 2-4 % faster at levels 0-1, 8 % at level 2, 10-12 % at level 3, 3-6 % at level 4 (the
+// few-tile levels' ranges of 17 or 18 tiles differed by a tile; profiles/r06/kbexp_r06{q,r}_x6c_balanced_ranges.log).
+template <int NW, int AC = 1, int PW = 1, int RS = 32, int ABL = 0, int DT = 0, int BR = 0>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
@@ -1111,7 +1116,44 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   const int slice = (int)(lb % n_slices);
   const int range = (int)(lb / n_slices);
   const int ci0 = 32 * (slice / n_sl_o), co0 = 32 * (slice % n_sl_o);
-  const int64_t t0 = (int64_t)range * n_tiles / n_ranges, t1 = (int64_t)(range + 1) * n_tiles / n_ranges;
+  int64_t t0 = (int64_t)range * n_tiles / n_ranges, t1 = (int64_t)(range + 1) * n_tiles / n_ranges;
+  if constexpr (BR > 0) {
+    if (n_tiles <= (int64_t)NTH * NTH) {  // block-uniform
+      __shared__ int bcnt[2][2][NW];
+      auto cost = [&](int64_t t) { return tile_start[t] + (int64_t)BR * t; };
+      const int64_t c0 = cost(0), total = cost(n_tiles) - c0;
+      const int64_t tg[2] = {c0 + (int64_t)range * total / n_ranges, c0 + (int64_t)(range + 1) * total / n_ranges};
+      // bound(tg) = the first tile of cost >= tg (cost is increasing): round 0 counts the samples t = i st below
+      // each target, round 1 the tiles of the interval that leaves
+      const int64_t st = (n_tiles + NTH - 1) / NTH;
+      int64_t base[2] = {0, 0};
+#pragma unroll
+      for (int rd = 0; rd < 2; ++rd) {
+        int64_t c[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int64_t t = rd == 0 ? (int64_t)tid * st : base[k] + tid;
+          const bool ok = rd == 0 ? t < n_tiles : (tid < st - 1 && t < n_tiles);
+          c[k] = ok ? cost(t) : INT64_MAX;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int n = __popcll(ballot64(c[k] < tg[k]));
+          if (lane == 0) bcnt[rd][k][wave] = n;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          int n = 0;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) n += bcnt[rd][k][w];
+          base[k] = rd == 0 ? (n > 0 ? (int64_t)(n - 1) * st + 1 : 0) : base[k] + n;
+        }
+      }
+      t0 = base[0] < n_tiles ? base[0] : n_tiles;
+      t1 = base[1] < n_tiles ? base[1] : n_tiles;
+    }
+  }
 
   floatx4 acc[NOW][2][2];
 #pragma unroll
@@ -1547,7 +1589,7 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
   const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
   // 72-byte image rows (RS = 36): 9-15 % faster than the swizzled 64-byte rows at every level
   // (profiles/r05/kbexp_r05m_x6c_row_stride.log)
-  wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS, 0, 1><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
+  wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS, 0, 1, 128><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
       x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
   wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 16), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
@@ -1741,7 +1783,18 @@ int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, 
   else if (variant == 2043)  // the round-6 product: direct offset table (DT)
     wgrad_x6c_kernel<8, 1, 1, 36, 0, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr,
                                                              u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
-
+  else if (variant == 32043)  // + ranges of equal cost, 32 chunks per tile of staging
+    wgrad_x6c_kernel<8, 1, 1, 36, 0, 1, 32><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
+                                                                 chunk_lr, u_start, u_rows, n_rows, n_tiles,
+                                                                 (int)n_ranges, slab);
+  else if (variant == 64043)  // + ranges of equal cost, 64 chunks per tile of staging
+    wgrad_x6c_kernel<8, 1, 1, 36, 0, 1, 64><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
+                                                                 chunk_lr, u_start, u_rows, n_rows, n_tiles,
+                                                                 (int)n_ranges, slab);
+  else if (variant == 128043)  // + ranges of equal cost, 128 chunks per tile of staging
+    wgrad_x6c_kernel<8, 1, 1, 36, 0, 1, 128><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
+                                                                  chunk_lr, u_start, u_rows, n_rows, n_tiles,
+                                                                  (int)n_ranges, slab);
   else {
     set_error("msp_exp_wgrad_chunk: no variant %d", variant);
     return MSP_EINVAL;
