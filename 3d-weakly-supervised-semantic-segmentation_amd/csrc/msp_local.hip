@@ -1031,6 +1031,9 @@ __global__ __launch_bounds__(256) void wgrad_far_kernel(const float* __restrict_
 }
 
 constexpr int kWMaxCh = 216;                   // chunks of one 128-row tile (K <= 27 offsets x 8)
+// wgrad_x6c's offset deal (DL 1): the offsets of wave w, one per byte from the low end, 0xFF past the last
+__device__ __constant__ const uint32_t kX6cDeal[8] = {0x1a150a06u, 0x19141103u, 0x120f0502u, 0xff130c01u,
+                                                      0xff090704u, 0xffff0e0du, 0xff161000u, 0x18170b08u};
 
 // bf16 element offset of 8-byte unit v (channels 4v .. 4v+3 of the slice) of row j in a piece image
 __device__ __forceinline__ int wimg_off(int j, int v) { return j * 32 + 4 * (v ^ (((j >> 2) & 1) << 2)); }
@@ -1090,13 +1093,21 @@ __device__ __forceinline__ void split4(const floatx4& a, uint2 (&p)[3]) {
 // rounds of block-wide counts.  Still a fixed function of the index: deterministic.  The product runs BR = 128:
 // against equal tile counts 2-4 % faster at levels 0-1, 8 % at level 2, 10-12 % at level 3, 3-6 % at level 4 (the
 // few-tile levels' ranges of 17 or 18 tiles differed by a tile; profiles/r06/kbexp_r06{q,r}_x6c_balanced_ranges.log).
-template <int NW, int AC = 1, int PW = 1, int RS = 32, int ABL = 0, int DT = 0, int BR = 0>
+// DL 1 (offset deal table, NW = 8): wave w owns the offsets of kX6cDeal[w] instead of w, w + 8, ...  Every tile
+// waits at its barrier for its slowest wave, and on surfaces the round-robin deal stacks one plane's heavy offsets
+// on a few waves: the slowest wave carries 1.38 / 1.31 / 1.28 / 1.24 / 1.21 x the mean k-steps at levels 0-4 of the
+// headline batch.  The table was chosen offline by local search over those per-tile counts (scripts/kbench.py
+// X6C_DUMP; weighted by each level's share of the step): 1.18 / 1.17 / 1.16 / 1.17 / 1.17 x, and fitted on levels
+// 0-1 alone it gives the held-out levels 2-4 the same 1.17 -- it follows the scenes' axis-aligned planes, not the
+// batch.  An offset's sums are the same k-steps in the same order whichever wave runs them: bit-identical.
+template <int NW, int AC = 1, int PW = 1, int RS = 32, int ABL = 0, int DT = 0, int BR = 0, int DL = 0>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
     const float* __restrict__ x, int c_in, const float* __restrict__ dy, int c_out, int K,
     const int64_t* __restrict__ tile_start, const uint8_t* __restrict__ chunk_off,
     const uint32_t* __restrict__ chunk_lr, const int64_t* __restrict__ u_start, const int32_t* __restrict__ u_rows,
     int64_t n_rows, int64_t n_tiles, int n_ranges, float* __restrict__ slab) {
-  constexpr int NTH = 64 * NW, NOW = 32 / NW;          // offsets per wave: o = wave + NW a, a < NOW
+  constexpr int NTH = 64 * NW, NOW = 32 / NW;          // offsets per wave: o = wave + NW a, a < NOW (DL: the table)
+  static_assert(!DL || NW == 8, "the offset deal table is for 8 waves");
   constexpr int XI = (kWCap * 8 + NTH - 1) / NTH;     // x staging items (row, 4 channels) per thread
   constexpr int DI = kWTile * 8 / NTH;                // dy staging items per thread
   constexpr int EI = (kWMaxCh * 16 + NTH - 1) / NTH;  // rule words per thread
@@ -1111,6 +1122,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, p4 = i16 & 3;
+  const uint32_t deal = DL ? kX6cDeal[wave & 7] : 0u;
+  auto off_of = [&](int a) { return DL ? (int)((deal >> (8 * a)) & 0xFFu) : wave + NW * a; };  // 0xFF >= K: none
   const int n_sl_o = c_out / 32, n_slices = (c_in / 32) * n_sl_o;
   const int64_t lb = xcd_linear(blockIdx.x, gridDim.x);
   const int slice = (int)(lb % n_slices);
@@ -1344,7 +1357,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
       S[0] = 0;
 #pragma unroll
       for (int a = 0; a < NOW; ++a) {
-        const int o = wave + NW * a;
+        const int o = off_of(a);
         first[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[buf][0][o]) : 0;
         endc[a] = o < K ? __builtin_amdgcn_readfirstlane(otab[buf][1][o]) : 0;
         S[a + 1] = S[a] + (endc[a] - first[a] + 1) / 2;
@@ -1378,8 +1391,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad_x6c_kernel(
   float* sb = slab + (int64_t)range * K * c_in * c_out;
 #pragma unroll
   for (int a = 0; a < NOW; ++a) {
-    const int o = wave + NW * a;
-    if (o >= K) break;
+    const int o = off_of(a);
+    if (o >= K) continue;
 #pragma unroll
     for (int sa = 0; sa < 2; ++sa)
 #pragma unroll
@@ -1589,8 +1602,15 @@ int msp_conv_wgrad_chunk(const float* x, int c_in, const float* dy, int c_out, i
   const int64_t slices = (int64_t)(c_in / 32) * (c_out / 32);
   // 72-byte image rows (RS = 36): 9-15 % faster than the swizzled 64-byte rows at every level
   // (profiles/r05/kbexp_r05m_x6c_row_stride.log)
-  wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS, 0, 1, 128><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
-      x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges, slab);
+  // the offset deal table was fitted to the 27 offsets of a 3^3 submanifold filter; other maps deal round-robin
+  if (K == 27)
+    wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS, 0, 1, 128, 1><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
+        x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges,
+        slab);
+  else
+    wgrad_x6c_kernel<8, 1, 1, MSP_X6C_RS, 0, 1, 128, 0><<<(unsigned)(n_ranges * slices), 512, 0, s>>>(
+        x, c_in, dy, c_out, K, tile_start, chunk_off, chunk_lr, u_start, u_rows, n_rows, n_tiles, (int)n_ranges,
+        slab);
   const int64_t n4 = (int64_t)K * c_in * c_out / 4;
   wgrad_ranges_reduce_kernel<<<(unsigned)ceil_div(n4, 16), 256, 0, s>>>(reinterpret_cast<const floatx4*>(slab),
                                                                          (int)n_ranges, n4,
@@ -1791,6 +1811,10 @@ int msp_exp_wgrad_chunk(int variant, const float* x, int c_in, const float* dy, 
     wgrad_x6c_kernel<8, 1, 1, 36, 0, 1, 64><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
                                                                  chunk_lr, u_start, u_rows, n_rows, n_tiles,
                                                                  (int)n_ranges, slab);
+  else if (variant == 1128043)  // the round-6 product: + the offset deal table
+    wgrad_x6c_kernel<8, 1, 1, 36, 0, 1, 128, 1><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
+                                                                     chunk_lr, u_start, u_rows, n_rows, n_tiles,
+                                                                     (int)n_ranges, slab);
   else if (variant == 128043)  // + ranges of equal cost, 128 chunks per tile of staging
     wgrad_x6c_kernel<8, 1, 1, 36, 0, 1, 128><<<grid, 512, 0, s>>>(x, c_in, dy, c_out, K, tile_start, chunk_off,
                                                                   chunk_lr, u_start, u_rows, n_rows, n_tiles,

@@ -115,6 +115,67 @@ def conv_forms(rules, V, cin, cout):
     return forms
 
 
+def x6c_balance(tiles):
+    """wgrad_x6c's per-tile wave balance: k-steps (two chunks each) per (tile, offset), waves owning offsets
+    w, w + 8, ...; a tile takes the slowest wave's k-steps.  Prints sum over tiles of (max wave) / (mean wave) and
+    what a per-tile longest-first deal onto 8 waves (<= 4 offsets each) would give."""
+    import numpy as np
+    ts = tiles["tile_start"].cpu().numpy().astype(np.int64)
+    co = tiles["chunk_off"].cpu().numpy().astype(np.int64)
+    nt = len(ts) - 2  # tile_start carries the largest tile's chunk count after the total
+    ts = ts[:nt + 1]
+    tile_of = np.repeat(np.arange(nt), np.diff(ts))
+    ch = np.zeros((nt, 32), np.int64)
+    np.add.at(ch, (tile_of, co[:ts[-1]]), 1)
+    ks = (ch + 1) // 2
+    if os.environ.get("X6C_DUMP"):  # per-tile k-steps per offset, for choosing the offset deal offline
+        np.save(os.environ["X6C_DUMP"] + f"_n{nt}.npy", ks.astype(np.int16))
+    wave = ks.reshape(nt, 4, 8).sum(1)  # offset o = w + 8 a
+    mx, mean = wave.max(1).sum(), ks.sum() / 8
+    lpt = 0
+    for t in range(nt):
+        load = np.zeros(8, np.int64)
+        cntw = np.zeros(8, np.int64)
+        for o in np.argsort(-ks[t], kind="stable"):
+            if ks[t, o] == 0:
+                break
+            cand = np.where(cntw < 4, load, 1 << 60)
+            w = int(np.argmin(cand))
+            load[w] += ks[t, o]
+            cntw[w] += 1
+        lpt += load.max()
+    print(f"  x6c balance: k-steps {ks.sum()} mean/wave {mean:.0f}  fixed deal max {mx} ({mx / mean:.2f}x)  "
+          f"per-tile LPT max {lpt} ({lpt / mean:.2f}x)  centre offset share {ks[:, 13].sum() / ks.sum():.3f}", flush=True)
+    # per range (equal tile counts, R ranges): a range-wide deal (the rejected OB form) still waits per tile;
+    # 'no barrier' = each wave's range total (the bound if waves never waited for each other inside a range)
+    for R in sorted({max(1, 256 // s_) for s_ in (1, 4, 9, 16, 25)}):
+        if R > nt:
+            continue
+        b_ = [t_ * nt // R for t_ in range(R + 1)]
+        ob, nob, rng_mean = 0, 0, 0.0
+        for r_ in range(R):
+            blk = ks[b_[r_]:b_[r_ + 1]]
+            tot = blk.sum(0)
+            load = np.zeros(8, np.int64)
+            cntw = np.zeros(8, np.int64)
+            asg = {}
+            for o in np.argsort(-tot, kind="stable"):
+                if o >= 27:
+                    continue
+                w = int(np.argmin(np.where(cntw < 4, load, 1 << 60)))
+                asg[o] = w
+                load[w] += tot[o]
+                cntw[w] += 1
+            wv = np.zeros((len(blk), 8), np.int64)
+            for o, w in asg.items():
+                wv[:, w] += blk[:, o]
+            ob = max(ob, wv.max(1).sum())
+            nob = max(nob, blk.reshape(len(blk), 4, 8).sum(1).sum(0).max())
+            rng_mean = max(rng_mean, blk.sum() / 8)
+        print(f"    R={R}: slowest range: mean/wave {rng_mean:.0f}  range-LPT deal with per-tile waits {ob}  "
+              f"fixed deal without waits {nob}", flush=True)
+
+
 def main():
     b = make_batch(int(os.environ.get("SCENES", "8")), 50, seed=1)
     t = scn.InputLayer(3, 4096, mode=4)([torch.from_numpy(b["coords"]).to(DEV), torch.from_numpy(b["feats"]).to(DEV)])
@@ -133,6 +194,8 @@ def main():
         fill = rules.n_rules / max(tl["n_chunks"] * 16, 1)
         print(f"L{L} V={V} R={rules.n_rules} ({rules.n_rules / V:.1f}/row) tiles={loc['n_tiles']} distinct rows "
               f"per tile {cnt.mean().item() / 128:.2f}x128 (max {loc['max_u']}) chunk fill {fill:.2f}", flush=True)
+        if os.environ.get("X6C_STATS") == "1" and rules.wgrad_index() is not None:
+            x6c_balance(rules.wgrad_index()["tiles"])
         a = M * (L + 1)
         rows = torch.arange(min(NSUB, V), device=DEV)
         nb = rules.nbr[:, :len(rows)].long()
