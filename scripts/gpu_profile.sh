@@ -6,6 +6,7 @@ TAG=${TAG:-r03} STEPS=${BENCH_STEPS:-10} bash scripts/profile.sh && \
   python3 scripts/prof_summary.py $(find gpurun_out/prof_${TAG} -name "*kernel_stats.csv" | head -1) 45 > gpurun_out/kernel_stats_${TAG}_summary.txt && \
   python3 scripts/trace_gaps.py $(find gpurun_out/prof_${TAG} -name "*kernel_trace.csv" | head -1) > gpurun_out/gaps_${TAG}.txt && \
   python3 scripts/step_kernels.py $(find gpurun_out/prof_${TAG} -name "*kernel_trace.csv" | head -1) > gpurun_out/step_kernels_${TAG}.txt && \
+  python3 scripts/step_gaps.py $(find gpurun_out/prof_${TAG} -name "*kernel_trace.csv" | head -1) > gpurun_out/step_gaps_${TAG}.txt && \
   python3 scripts/kernel_by_grid.py $(find gpurun_out/prof_${TAG} -name "*kernel_trace.csv" | head -1) bn_ conv_x6 wgrad_x6 split_cols \
     > gpurun_out/kernel_by_grid_${TAG}.txt
 rc=$?

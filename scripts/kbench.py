@@ -196,6 +196,14 @@ def main():
               f"per tile {cnt.mean().item() / 128:.2f}x128 (max {loc['max_u']}) chunk fill {fill:.2f}", flush=True)
         if os.environ.get("X6C_STATS") == "1" and rules.wgrad_index() is not None:
             x6c_balance(rules.wgrad_index()["tiles"])
+        if os.environ.get("X6S_DUMP") and "lidx" in loc:  # conv_x6s's rows per (tile, 16-row group, offset)
+            import numpy as np
+            nt_ = loc["n_tiles"]
+            pres = (loc["lidx"][:, :nt_ * 128] != -1).view(27, nt_, 8, 16).sum(3)  # uint16 0xFFFF = absent
+            np.save(os.environ["X6S_DUMP"] + f"_L{L}.npy", pres.permute(1, 2, 0).to(torch.uint8).cpu().numpy())
+            bits = (loc["lidx"][:, :nt_ * 128] != -1).to(torch.int64)
+            mask = (bits << torch.arange(27, device=DEV).view(27, 1)).sum(0)  # offset mask per tile row position
+            np.save(os.environ["X6S_DUMP"] + f"_mask_L{L}.npy", mask.to(torch.int32).cpu().numpy())
         a = M * (L + 1)
         rows = torch.arange(min(NSUB, V), device=DEV)
         nb = rules.nbr[:, :len(rows)].long()
