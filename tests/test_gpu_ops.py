@@ -1012,6 +1012,52 @@ def test_conv_wgrad_chunk_from_local_index(cin, cout):
     assert (dw - dw_t).abs().max().item() / scale < 2e-6
 
 
+@pytest.mark.parametrize("cin,cout", [(32, 32), (64, 96)])
+def test_conv_wgrad_chunk_any_range_count(cin, cout):
+    """msp_conv_wgrad_chunk's persistent blocks take contiguous tile ranges of equal cost (chunks + 128 per tile,
+    bounds found in-kernel from tile_start) and deal the 27 offsets to their waves by a fitted table (round 6).
+    Every range count -- one range, a few, one tile per range, the library's own choice -- gives dW within 1e-5 of
+    fp64 (one range keeps every offset's sum in one block's fp32 registers over all tiles: 2.9e-6 measured; the
+    library's own count is held to 1e-6 by test_conv_wgrad_chunk_accuracy), each run-to-run bit-identical; and a
+    tile count that is not a multiple of the range count is covered."""
+    from sparseconvnet import _lib
+    from sparseconvnet._lib import ptr
+    torch.manual_seed(3 * cin + cout)
+    coords, feats = _inputs(20000, 40, n_batch=2)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    rules = t.metadata.level(64).subm_rules(3)
+    V = t.metadata.level(64).n
+    idx = rules.wgrad_index(wait=True)
+    assert idx["n_far"] == 0
+    tiles = idx["tiles"]
+    n_tiles = (V + 127) // 128
+    x = torch.randn(V, cin, device=DEV)
+    dy = torch.randn(V, cout, device=DEV)
+    nb = rules.nbr.long()
+    ref = torch.empty(27, cin, cout, dtype=torch.float64, device=DEV)
+    for o in range(27):
+        m = nb[o] >= 0
+        ref[o] = x[nb[o][m]].double().t() @ dy[m].double()
+    scale = ref.abs().max().item()
+    own = int(_lib.query("msp_wgrad_chunk_ranges", _lib.I64(V), cin, cout))
+    counts = sorted({1, 3, 7, max(1, n_tiles // 2 + 1), n_tiles, own})
+    assert any(n_tiles % c for c in counts)
+
+    def run(n_ranges):
+        dw = torch.empty(27, cin, cout, device=DEV)
+        slab = torch.empty(n_ranges, 27, cin, cout, device=DEV)
+        _lib.call("msp_conv_wgrad_chunk", ptr(x), cin, ptr(dy), cout, 27, tiles["tile_rows"],
+                  ptr(tiles["tile_start"]), ptr(tiles["chunk_off"]), ptr(idx["chunk_lr"]), ptr(idx["u_start"]),
+                  ptr(idx["u_rows"]), V, n_ranges, ptr(slab), ptr(dw), _lib.stream())
+        return dw
+    for c in counts:
+        a, b = run(c), run(c)
+        err = (a.double() - ref).abs().max().item() / scale
+        print(f"wgrad_chunk {cin}x{cout} n_tiles={n_tiles} ranges={c}: max err {err:.2e}")
+        assert err < (1e-6 if c == own else 1e-5)
+        assert torch.equal(a, b)
+
+
 def test_conv_wgrad_chunk_over_cap_far_rules():
     """A map whose 128-row tiles name more distinct input rows than the chunk weight gradient stages
     (msp_wgrad_chunk_cap, 448): msp_wgrad_chunk_index counts the rules whose row lies past the cap (n_far, ADVICE
