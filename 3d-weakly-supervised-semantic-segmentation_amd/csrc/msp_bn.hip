@@ -421,15 +421,28 @@ __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const double* __res
   if (dweight) dweight[c] = (float)s2[1];
 }
 
+// SPLIT (msp_bn_bwd_apply_split, round 6): dx's columns [0, ca) go to dx as [V][ca] and [ca, C) to dxb as
+// [V][C - ca] -- the two gradients of a JoinTable that produced x, written here instead of by a split pass.
+template <bool SPLIT = false>
 __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ dy, int64_t n, int C,
                                                           int64_t V, const double* __restrict__ sums,
                                                           const float* __restrict__ stats,
                                                           const float* __restrict__ weight, float leak, int train,
-                                                          const float* __restrict__ addend, float* __restrict__ dx) {
+                                                          const float* __restrict__ addend, float* __restrict__ dx,
+                                                          int ca = 0, float* __restrict__ dxb = nullptr) {
   const int64_t stride = (int64_t)gridDim.x * kT;
   const double invV = V > 0 ? 1.0 / (double)V : 0.0;
   const BnStats st(stats, C);
+  auto store = [&](int64_t i, int c, float d) {
+    if constexpr (SPLIT) {
+      const int64_t v = i / C;
+      if (c < ca) dx[v * ca + c] = d;
+      else dxb[v * (C - ca) + (c - ca)] = d;
+    } else {
+      dx[i] = d;
+    }
+  };
   for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += stride) {
     const int c = (int)(i % C);
     const float xv = x[i], g = dy[i];
@@ -439,21 +452,24 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply_kernel(const float* __restric
       const float xh = st.centred(xv, c) * st.is[c];
       const float mdz = (float)(sums[c] * invV), mdzx = (float)(sums[C + c] * invV);
       const float d = w * st.is[c] * (dz - mdz - xh * mdzx);
-      dx[i] = addend ? d + addend[i] : d;
+      store(i, c, addend ? d + addend[i] : d);
     } else {
       const float d = w * st.is[c] * dz;
-      dx[i] = addend ? d + addend[i] : d;
+      store(i, c, addend ? d + addend[i] : d);
     }
   }
 }
 
-// Vector form of the above (same column ownership as bn_apply4_kernel).
+// Vector form of the above (same column ownership as bn_apply4_kernel).  SPLIT: quad stores when ca % 4 == 0, else
+// element stores (a quad may straddle the split); the arithmetic is the same either way.
+template <bool SPLIT = false>
 __global__ __launch_bounds__(kT) void bn_bwd_apply4_kernel(const float* __restrict__ x,
                                                            const float* __restrict__ dy, int64_t V, int C,
                                                            const double* __restrict__ sums,
                                                            const float* __restrict__ stats,
                                                            const float* __restrict__ weight, float leak, int train,
-                                                           const float* __restrict__ addend, float* __restrict__ dx) {
+                                                           const float* __restrict__ addend, float* __restrict__ dx,
+                                                           int ca = 0, float* __restrict__ dxb = nullptr) {
   const int C4 = C >> 2, R = kT / C4;
   const int t = threadIdx.x, c4 = t % C4, ro = t / C4;
   if (ro >= R) return;
@@ -474,7 +490,12 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply4_kernel(const float* __restri
   }
   const float4* x4 = reinterpret_cast<const float4*>(x);
   const float4* g4 = reinterpret_cast<const float4*>(dy);
-  float4* d4 = reinterpret_cast<float4*>(dx);
+  // the thread's column quad is fixed: SPLIT writes it to the first or the second output, row stride C4o
+  const int ca4 = ca >> 2;
+  const bool quad = !SPLIT || (ca & 3) == 0;  // block-uniform
+  const bool to_b = SPLIT && c4 >= ca4;
+  float4* d4 = reinterpret_cast<float4*>(to_b ? dxb : dx);
+  const int C4o = SPLIT ? (to_b ? C4 - ca4 : ca4) : C4, c4o = to_b ? c4 - ca4 : c4;
   const int64_t step = (int64_t)gridDim.x * R;
   auto f = [&](float xv, float g, int k) {
     const float xc = (xv - mh[k]) - ml[k];
@@ -489,7 +510,17 @@ __global__ __launch_bounds__(kT) void bn_bwd_apply4_kernel(const float* __restri
       const float4 e = reinterpret_cast<const float4*>(addend)[v * C4 + c4];
       d = make_float4(d.x + e.x, d.y + e.y, d.z + e.z, d.w + e.w);
     }
-    d4[v * C4 + c4] = d;
+    if (quad) {
+      d4[v * C4o + c4o] = d;
+    } else {  // SPLIT with ca % 4 != 0
+      const float e[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = 4 * c4 + k;
+        if (c < ca) dx[v * ca + c] = e[k];
+        else dxb[v * (C - ca) + (c - ca)] = e[k];
+      }
+    }
   }
 }
 
@@ -622,7 +653,7 @@ int msp_bn_bwd_stats(const float* x, const float* dy, int64_t V, int C, const fl
 // dx from the per-channel totals `sums` [2][C] (the finalize before it wrote them)
 static int bn_bwd_apply_sums(const float* x, const float* dy, int64_t V, int C, const double* sums,
                              const float* stats, const float* weight, float leak, int train, const float* addend,
-                             float* dx, hipStream_t s);
+                             float* dx, hipStream_t s, int ca = 0, float* dxb = nullptr);
 
 int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, const double* partial,
                          const float* stats, const float* weight, float leak, int train, const float* addend,
@@ -649,17 +680,40 @@ int msp_bn_bwd_apply_cm(const float* x, const float* dy, int64_t V, int C, const
 
 static int bn_bwd_apply_sums(const float* x, const float* dy, int64_t V, int C, const double* sums,
                              const float* stats, const float* weight, float leak, int train, const float* addend,
-                             float* dx, hipStream_t s) {
+                             float* dx, hipStream_t s, int ca, float* dxb) {
   const int64_t n = V * C;
   if (n > 0) {
-    if (C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx) &&
-        (addend == nullptr || aligned16(addend)))
+    const bool vec = C % 4 == 0 && C <= 4 * kT && aligned16(x) && aligned16(dy) && aligned16(dx) &&
+                     (addend == nullptr || aligned16(addend));
+    if (dxb != nullptr) {  // split output (msp_bn_bwd_apply_split); the vector form whenever the unsplit one runs
+      if (vec && (ca % 4 != 0 || aligned16(dxb)))
+        bn_bwd_apply4_kernel<true><<<rows_grid(V, C), kT, 0, s>>>(x, dy, V, C, sums, stats, weight, leak, train,
+                                                                  addend, dx, ca, dxb);
+      else
+        bn_bwd_apply_kernel<true><<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train,
+                                                             addend, dx, ca, dxb);
+    } else if (vec) {
       bn_bwd_apply4_kernel<<<rows_grid(V, C), kT, 0, s>>>(x, dy, V, C, sums, stats, weight, leak, train, addend,
                                                           dx);
-    else
+    } else {
       bn_bwd_apply_kernel<<<ew_grid(n), kT, 0, s>>>(x, dy, n, C, V, sums, stats, weight, leak, train, addend, dx);
+    }
   }
   return check_launch("msp_bn_bwd_apply");
+}
+
+int msp_bn_bwd_apply_split(const float* x, const float* dy, int64_t V, int C, const double* partial,
+                           const float* stats, const float* weight, float leak, int train, const float* addend,
+                           int ca, float* dxa, float* dxb, float* dweight, float* dbias, msp_stream_t stream) {
+  MSP_REQUIRE(C > 0 && ca > 0 && ca < C && V >= 0, "msp_bn_bwd_apply_split: bad split (C=%d ca=%d)", C, ca);
+  MSP_REQUIRE((dxa && dxb) || V == 0, "msp_bn_bwd_apply_split: NULL output");
+  MSP_REQUIRE(V == 0 || (dxa != dxb && (const float*)dxa != addend && (const float*)dxb != addend &&
+                         (const float*)dxa != x && (const float*)dxb != x),
+              "msp_bn_bwd_apply_split: outputs must not alias each other or an input");
+  hipStream_t s = as_stream(stream);
+  double* sums = const_cast<double*>(partial) + bn_parts(V, C) * 2 * C;
+  bn_bwd_finalize_kernel<<<(unsigned)C, kT, 0, s>>>(partial, bn_parts(V, C), C, dweight, dbias, sums);
+  return bn_bwd_apply_sums(x, dy, V, C, sums, stats, weight, leak, train, addend, dxa, s, ca, dxb);
 }
 
 int msp_bn_bwd_apply(const float* x, const float* dy, int64_t V, int C, const double* partial, const float* stats,

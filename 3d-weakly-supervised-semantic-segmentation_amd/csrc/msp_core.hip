@@ -196,7 +196,7 @@ int scan_small_inplace(int64_t* data, int64_t n, int64_t* total, hipStream_t s) 
 
 extern "C" {
 
-int msp_abi_version(void) { return 9; }
+int msp_abi_version(void) { return 10; }
 
 const char* msp_last_error(void) { return msp::g_err; }
 

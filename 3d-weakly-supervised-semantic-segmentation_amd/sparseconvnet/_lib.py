@@ -88,6 +88,7 @@ PROTOTYPES = {
     "msp_bn_bwd_stats": (I, [P, P, I64, I, P, F, P, P]),
     "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
+    "msp_bn_bwd_apply_split": (I, [P, P, I64, I, P, P, P, F, I, P, I, P, P, P, P, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),
     "msp_conv_bn_parts": (I64, [I64]),
     "msp_conv_local_bn": (I, [P, I, P, I, I, I, I, P, P, P, P, P, I64, P, P, SZ, P, P]),

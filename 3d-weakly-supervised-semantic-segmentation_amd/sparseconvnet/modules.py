@@ -262,7 +262,15 @@ class BatchNormalization(nn.Module):
             else None
         args = (self.weight, self.bias, self.running_mean, self.running_var, self.eps, self.momentum,
                 float(self.leakiness), self.training, self._joined_partial(input), link)
-        if self.__dict__.pop("_fork", False):
+        fork = self.__dict__.pop("_fork", False)
+        js = self._join_sources(input)
+        if js is not None:
+            # x is a JoinTable's [a | b]: the backward writes a's and b's gradients itself, no split pass
+            # (ops.BatchNormJoinFunction; with fork, also the shortcut's gradient of x added inside it)
+            f, xs = ops.BatchNormJoinFunction.apply(input.features.detach(), js[0], js[1], fork, *args)
+            if fork:
+                self._fork_shortcut = SparseConvNetTensor(xs, input.metadata, input.spatial_size)
+        elif fork:
             # residual fork requested by ConcatTable: x is handed on to the shortcut through the Function so
             # the shortcut's gradient of x is added inside the BN backward (ops.BatchNormForkFunction)
             f, xs = ops.BatchNormForkFunction.apply(input.features, *args)
@@ -273,6 +281,15 @@ class BatchNormalization(nn.Module):
         if link is not None:
             out._bn_link = (f, link)
         return out
+
+    def _join_sources(self, input):
+        """(a, b) when input is exactly a two-way JoinTable's output (JoinTable leaves them) and the fused split
+        applies (ops.FUSE_JOIN_SPLIT, device tensors, a gradient to propagate)."""
+        js = getattr(input, "_join_src", None)
+        if js is None or not ops.FUSE_JOIN_SPLIT or js[0] is not input.features or not input.features.is_cuda:
+            return None
+        a, b = js[1], js[2]
+        return (a, b) if (a.requires_grad or b.requires_grad) and torch.is_grad_enabled() else None
 
     def _joined_partial(self, input):
         """Batch-statistic partials a residual join left on its output (AddTable), if they are for exactly
@@ -408,6 +425,8 @@ class JoinTable(nn.Module):
         out = SparseConvNetTensor(f, input[0].metadata, input[0].spatial_size)
         if partial is not None:
             out._bn_partial = (f, partial)
+        if len(input) == 2:  # the BatchNormalization this join feeds may write the inputs' gradients itself
+            out._join_src = (f, input[0].features, input[1].features)
         return out
 
 

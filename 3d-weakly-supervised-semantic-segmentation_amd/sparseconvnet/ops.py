@@ -793,6 +793,83 @@ class BatchNormForkFunction(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None, None, None, None
 
 
+def _bn_bwd_split(x, weight, stats, cfg, gy, addend, ca, need_a, need_b):
+    """_bn_bwd with dx written as its two column blocks [V][ca], [V][C - ca] (msp_bn_bwd_apply_split): the
+    gradients of the JoinTable inputs that x joined, with no split pass.  Returns (ga, gb, dweight, dbias)."""
+    leak, train, has_w, has_b = cfg
+    gy = gy.contiguous()
+    V, C = x.shape
+    s = _stream(x)
+    ga = torch.empty((V, ca), dtype=torch.float32, device=x.device)
+    gb = torch.empty((V, C - ca), dtype=torch.float32, device=x.device)
+    dw = torch.empty(C, dtype=torch.float32, device=x.device)
+    db = torch.empty(C, dtype=torch.float32, device=x.device)
+    partial = _bn_partial_buf(V, C, x.device)
+    add = ptr(addend) if addend is not None else None
+
+    def run():
+        call("msp_bn_bwd_stats", ptr(x), ptr(gy), V, C, ptr(stats), leak, ptr(partial), s)
+        call("msp_bn_bwd_apply_split", ptr(x), ptr(gy), V, C, ptr(partial), ptr(stats),
+             ptr(weight) if has_w else None, leak, train, add, ca, ptr(ga), ptr(gb), ptr(dw), ptr(db), s)
+    # compulsory bytes: statistics pass (read x, dy), apply (read x, dy [, shortcut grad], write dx's two blocks)
+    _record(_shape("bn_bwd/hbm", C, C, V), 0, run, 4 * V * C * (5 + (addend is not None)))
+    return (ga if need_a else None), (gb if need_b else None), (dw if has_w else None), (db if has_b else None)
+
+
+# The UNet decoder's JoinTable -> BatchNormalization: the BN's backward writes the join inputs' gradients itself
+# (BatchNormJoinFunction) instead of a [V][C] dx that JoinFunction's backward then splits (msp_split_cols: one read
+# and one write of V x C floats per join, 0.26 ms/step at C3).  False: JoinFunction's split, as before.
+FUSE_JOIN_SPLIT = True
+
+
+class BatchNormJoinFunction(torch.autograd.Function):
+    """BatchNormFunction / BatchNormForkFunction (fork = True: the second output is x for the shortcut, whose
+    gradient is added inside the backward) over the output x = [a | b] of a JoinTable.  x comes in detached (the
+    join's forward already ran and left its statistics partials); a and b carry the gradient: the backward
+    writes d[a | b] as its two column blocks (msp_bn_bwd_apply_split), so the join's split pass is not needed.
+    The join's own autograd node receives no gradient from here; any other consumer of the joined tensor still
+    back-propagates through it (JoinFunction's split), and autograd adds the two contributions to a and b."""
+
+    @staticmethod
+    def forward(ctx, x, a, b, fork, weight, bias, running_mean, running_var, eps, momentum, leak, train,
+                partial=None, link=None):
+        _check_feats(x)
+        if x.size(1) != a.size(1) + b.size(1) or x.size(0) != a.size(0):
+            raise ValueError(f"BatchNormJoinFunction: x {tuple(x.shape)} is not the join of {tuple(a.shape)} and "
+                             f"{tuple(b.shape)}")
+        x = x.contiguous()
+        ctx.set_materialize_grads(False)
+        y, stats = _bn_fwd(x, weight, bias, running_mean, running_var, eps, momentum, leak, train, partial)
+        ctx.save_for_backward(x, weight, stats)
+        ctx.cfg = (float(leak), int(train), weight is not None, bias is not None)
+        ctx.ca = a.size(1)
+        ctx.link = _link(link, x, stats, train)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gx):
+        x, weight, stats = ctx.saved_tensors
+        link, ctx.link = ctx.link, None
+        if link is not None:
+            link.bwd = None  # a consumer's epilogue sums are not used on this path
+        need_a, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        none = (None,) * 10
+        if gy is None:
+            if gx is None:
+                return (None, None, None) + none + (None,)
+            gx = gx.contiguous()
+            V, C = gx.shape
+            ga = torch.empty((V, ctx.ca), dtype=torch.float32, device=gx.device) if need_a else None
+            gb = torch.empty((V, C - ctx.ca), dtype=torch.float32, device=gx.device) if need_b else None
+            if ga is not None or gb is not None:
+                call("msp_split_cols", ptr(gx), V, ctx.ca, C - ctx.ca, ptr(ga), ptr(gb), _stream(gx))
+            return (None, ga, gb) + none + (None,)
+        if gx is not None:
+            gx = gx.contiguous()
+        ga, gb, dw, db = _bn_bwd_split(x, weight, stats, ctx.cfg, gy, gx, ctx.ca, need_a, need_b)
+        return (None, ga, gb, None, dw, db) + (None,) * 8
+
+
 class ResidualJoinFunction(torch.autograd.Function):
     """a + b (SCN AddTable of a residual block) fused with the batch-statistic
     partials of the sum (msp_add_bn_stats): the next BatchNormalization, which

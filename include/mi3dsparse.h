@@ -365,6 +365,13 @@ int msp_bn_bwd_apply_add(const float* x, const float* dy, int64_t V, int C, cons
                          float* dx, float* dweight, float* dbias, msp_stream_t stream);
 int msp_add_bn_stats(const float* a, const float* b, int64_t V, int C, float* sum, double* partial,
                      msp_stream_t stream);
+/* msp_bn_bwd_apply_split (ABI 10): msp_bn_bwd_apply_add with dx written as two tensors, columns [0, ca) to dxa
+ * [V][ca] and [ca, C) to dxb [V][C - ca] -- where x was a JoinTable's output ([a | b], msp_join_cols), these are
+ * the gradients of a and b, and no msp_split_cols pass follows (the UNet decoder's join -> BN fork).  Same
+ * arithmetic per element as msp_bn_bwd_apply_add; 0 < ca < C; dxa, dxb non-NULL and aliasing nothing. */
+int msp_bn_bwd_apply_split(const float* x, const float* dy, int64_t V, int C, const double* partial,
+                           const float* stats, const float* weight, float leak, int train, const float* addend,
+                           int ca, float* dxa, float* dxb, float* dweight, float* dbias, msp_stream_t stream);
 /* Channel join (SCN JoinTable, the UNet / FCN skip joins: identity branch first, then the upsampled deeper
  * level): out[v] = [a[v] | b[v]], a [V][ca], b [V][cb], out [V][ca + cb].  With partial
  * non-NULL also the msp_bn_stats partials of out (identical to msp_bn_stats on it), for the BatchNormalization

@@ -73,7 +73,7 @@ def test_prototypes_match_header():
 
 def test_queries_and_validation_without_gpu():
     lib = _lib.load()
-    assert lib.msp_abi_version() == 9
+    assert lib.msp_abi_version() == 10
     assert _lib.query("msp_hash_capacity", 1000) == 2048
     assert _lib.query("msp_hash_capacity", 10) == 1024
     assert _lib.query("msp_scan_workspace_size", 5000) > 0

@@ -681,6 +681,74 @@ def test_residual_block_fused_matches_unfused(C, leak, nin, monkeypatch):
         assert torch.equal(b1, b2), n1
 
 
+@pytest.mark.parametrize("ca,cb,residual", [(32, 32, True), (64, 32, True), (16, 16, False), (6, 10, False)])
+def test_join_bn_split_backward_matches_split_pass(ca, cb, residual, monkeypatch):
+    """The UNet decoder's JoinTable -> BatchNormalization (residual: the BN fork of ConcatTable(NIN shortcut,
+    BN-SubM-BN-SubM) + AddTable; else BN -> SubM): with ops.FUSE_JOIN_SPLIT the BN's backward writes the join
+    inputs' gradients as two blocks (msp_bn_bwd_apply_split, ops.BatchNormJoinFunction) instead of a [V][C] dx
+    that msp_split_cols then splits.  Outputs, both inputs' gradients, every parameter gradient and the running
+    statistics are bit-identical to the split pass (the same arithmetic per element); 6 + 10 channels take the
+    scalar kernel.  A second consumer of the joined tensor still gets its gradient through the join."""
+    from sparseconvnet import ops
+    monkeypatch.setattr(ops, "FUSE_BN_STATS", False)
+    torch.manual_seed(ca + 7 * cb)
+    coords, feats = _inputs(4000, 24, n_feat=ca)
+    t = scn.InputLayer(3, 64, mode=4)([coords.to(DEV), feats.to(DEV)])
+    C = ca + cb
+    b0 = torch.randn(t.features.size(0), cb, device=DEV)
+
+    def make():
+        torch.manual_seed(2)
+        if residual:
+            blk = scn.Sequential().add(scn.JoinTable()).add(
+                scn.ConcatTable().add(scn.NetworkInNetwork(C, ca, False)).add(
+                    scn.Sequential().add(scn.BatchNormLeakyReLU(C, leakiness=0.333))
+                    .add(scn.SubmanifoldConvolution(3, C, ca, 3, False))
+                    .add(scn.BatchNormLeakyReLU(ca, leakiness=0.333))
+                    .add(scn.SubmanifoldConvolution(3, ca, ca, 3, False)))).add(scn.AddTable())
+        else:
+            blk = scn.Sequential().add(scn.JoinTable()).add(scn.BatchNormReLU(C)).add(
+                scn.SubmanifoldConvolution(3, C, ca, 3, False))
+        return blk.to(DEV).train()
+
+    outs = []
+    for fuse in (True, False):
+        monkeypatch.setattr(ops, "FUSE_JOIN_SPLIT", fuse)
+        net = make()
+        a = t.features.detach().clone().requires_grad_(True)
+        b = b0.clone().requires_grad_(True)
+        ta = scn.SparseConvNetTensor(a, t.metadata, t.spatial_size)
+        tb = scn.SparseConvNetTensor(b, t.metadata, t.spatial_size)
+        y = net([ta, tb]).features
+        w = torch.linspace(-1, 1, y.numel(), device=DEV).view_as(y)
+        (y * w).square().sum().backward()
+        outs.append((y.detach(), a.grad, b.grad, [p.grad for p in net.parameters()],
+                     [bf.clone() for bf in net.buffers()]))
+    for u, v in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(u, v)
+    for u, v in zip(outs[0][3] + outs[0][4], outs[1][3] + outs[1][4]):
+        assert torch.equal(u, v)
+    # a second consumer of the joined tensor: its gradient comes back through the join's split, added to a and b
+    monkeypatch.setattr(ops, "FUSE_JOIN_SPLIT", True)
+    a = t.features.detach().clone().requires_grad_(True)
+    b = b0.clone().requires_grad_(True)
+    j = scn.JoinTable().train()([scn.SparseConvNetTensor(a, t.metadata, t.spatial_size),
+                                 scn.SparseConvNetTensor(b, t.metadata, t.spatial_size)])
+    bn = scn.BatchNormReLU(C).to(DEV).train()
+    g1 = torch.randn(a.size(0), C, device=DEV)
+    g2 = torch.randn(a.size(0), C, device=DEV)
+    ((bn(j).features * g1).sum() + (j.features * g2).sum()).backward()
+    ga1, gb1 = a.grad.clone(), b.grad.clone()
+    monkeypatch.setattr(ops, "FUSE_JOIN_SPLIT", False)
+    a.grad = b.grad = None
+    bn2 = scn.BatchNormReLU(C).to(DEV).train()
+    j = scn.JoinTable().train()([scn.SparseConvNetTensor(a, t.metadata, t.spatial_size),
+                                 scn.SparseConvNetTensor(b, t.metadata, t.spatial_size)])
+    ((bn2(j).features * g1).sum() + (j.features * g2).sum()).backward()
+    torch.testing.assert_close(ga1, a.grad, rtol=0, atol=1e-6)
+    torch.testing.assert_close(gb1, b.grad, rtol=0, atol=1e-6)
+
+
 @pytest.mark.parametrize("M,K,N", [(300007, 64, 32), (40000, 128, 64), (9001, 192, 96), (5000, 320, 160),
                                    (777, 48, 48), (130, 448, 224), (1, 32, 16), (0, 64, 32), (270001, 32, 64),
                                    (30000, 64, 128), (20000, 96, 192)])
