@@ -288,6 +288,9 @@ def main():
                     help="untimed steps after the timed region with every family recorded (per-family rooflines "
                          "and the step-level compulsory bytes); 0 = none")
     ap.add_argument("--foreach-adam", action="store_true", help="torch's foreach Adam instead of the fused one")
+    ap.add_argument("--adam", choices=["library", "torch"], default="library",
+                    help="library: the reference's Adam update in one launch over every parameter (wsss3d.optim.Adam, "
+                         "msp_adam_step); torch: torch.optim.Adam (fused multi-tensor, or --foreach-adam)")
     ap.add_argument("--concurrent-wgrad", action="store_true",
                     help="every weight gradient on a side stream beside the backward-data (sparseconvnet.ops)")
     ap.add_argument("--compute-priority", type=int, choices=[0, 1], default=0,
@@ -436,16 +439,21 @@ def main():
         cls, _ = MODEL_REGISTRY.get("MultiLabel")
         model = wrap(cls(pc).to(dev))
     n_params = sum(p.numel() for p in model.parameters())
-    # the reference's optimizer (train.py:39, Adam lr 1e-3); one fused multi-tensor kernel per step
-    # (--foreach-adam: torch's default foreach form, ~21 launches per step)
+    # the reference's optimizer (train.py:39, Adam lr 1e-3): by default its update in one library launch over
+    # every parameter (wsss3d.optim.Adam); --adam torch: torch's fused multi-tensor kernels (12 launches per step),
+    # --foreach-adam: torch's default foreach form (~21)
     # N ranks over RCCL: the bucket all-reduces are captured into the step's graph, issued as each bucket's
     # gradients become final, so they run beside the rest of the backward (dp.GradSync overlap);
     # BENCH_GRAD_OVERLAP=0 restores one all-reduce over the whole buffer after each replay
     overlap = graph_dp and dist.is_initialized() and dist.get_backend() == "nccl" and \
         os.environ.get("BENCH_GRAD_OVERLAP", "1") != "0"
     gsync = dp.GradSync(model, dev, overlap=overlap) if graph_dp else None
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
-                                                           {"fused": True, "capturable": use_graph}))
+    if args.adam == "library" and not args.foreach_adam:
+        from wsss3d.optim import Adam as LibAdam
+        opt = LibAdam(model.parameters(), lr=1e-3)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, **({"foreach": True} if args.foreach_adam else
+                                                               {"fused": True, "capturable": use_graph}))
     # every convolution's split-bf16 weight image of a step in one launch at its start (sparseconvnet.weight_images;
     # the optimizer's steps invalidate them)
     wimg = scn.weight_images.enable(model, dev, optimizer=opt) if args.weight_images else None
@@ -847,6 +855,10 @@ def main():
             "config": {
                 "workload": workload,
                 "preset": preset,
+                "optimizer": ("Adam lr 1e-3 (train.py:39), the update in one library launch over every parameter "
+                              "(wsss3d.optim.Adam, msp_adam_step)" if args.adam == "library" and not args.foreach_adam
+                              else "torch.optim.Adam lr 1e-3 (train.py:39), " +
+                              ("foreach" if args.foreach_adam else "fused multi-tensor")),
                 "timed_step": "zero_grad -> forward (metadata from raw device coordinates) -> loss -> backward -> "
                               "Adam step; BASELINE.md's metric excludes the optimizer step, so including it is "
                               "conservative.  ms_per_step = wall time over the timed steps / steps (max over "

@@ -509,6 +509,27 @@ int msp_merge(const float* xyz, const float* rgb, const int64_t* labels, const i
               int64_t* coords, float* feats, int64_t* labels_out, int64_t* point_ids, int64_t point_id_base,
               int64_t* batch_offsets, float* scene_labels, void* ws, size_t ws_bytes, msp_stream_t stream);
 
+/* The training step's optimizer (round 6, ABI 10): torch.optim.Adam (the reference's train.py:39, Adam(lr=1e-3);
+ * amsgrad off) over up to MSP_ADAM_MAX_TENSORS parameter tensors in one launch.  table: device array of n
+ * msp_adam_tensor (param, exp_avg, exp_avg_sq: fp32, n floats each, contiguous); chunk_start: device exclusive
+ * prefix sums [n + 1] of msp_adam_chunks(table[i].n) (n_chunks = chunk_start[n]); grads: HOST array of n device
+ * gradient pointers (NULL: that tensor is skipped this step), passed to the kernel by value, so a captured graph
+ * keeps the step's own; step: device float step count, incremented first when bump != 0 (the first call of an
+ * optimizer step), then read as t.  Per element (fp32; 1 - b1, 1 - b2 and the bias corrections formed in double,
+ * as torch's fused Adam takes its scalars): g += wd * p; m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g^2;
+ * p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps). */
+#define MSP_ADAM_MAX_TENSORS 256
+typedef struct {
+  float* param;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;
+} msp_adam_tensor;
+int64_t msp_adam_chunks(int64_t n);
+int msp_adam_step(const msp_adam_tensor* table, const int64_t* chunk_start, const float* const* grads, int n,
+                  int64_t n_chunks, float* step, int bump, double lr, double beta1, double beta2, double eps,
+                  double weight_decay, msp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

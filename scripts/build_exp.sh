@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../3d-weakly-supervised-semantic-segmentation_amd/csrc"
 mkdir -p ../build/exp
 OBJS=""
 PIDS=""
-for f in msp_core msp_meta msp_conv msp_bn msp_layers msp_tail msp_merge msp_conv_x6 msp_nin msp_local msp_sort; do
+for f in msp_core msp_meta msp_conv msp_bn msp_layers msp_tail msp_merge msp_conv_x6 msp_nin msp_local msp_sort msp_optim; do
   extra=""
   case $f in msp_conv_x6|msp_local) extra="-mllvm -amdgpu-mfma-vgpr-form" ;; esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -I/opt/rocm/include \
