@@ -28,6 +28,7 @@ class Adam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._built = None
+        self._key = None
         self.step_count = None
 
     def _build(self):
@@ -36,7 +37,7 @@ class Adam(torch.optim.Optimizer):
                                "step allocates the moments and uploads the tensor table)")
         params = [p for g in self.param_groups for p in g["params"]]
         if not params:
-            self._built = []
+            self._built, self._key = [], ()
             return
         dev = params[0].device
         for p in params:
@@ -64,6 +65,14 @@ class Adam(torch.optim.Optimizer):
                 dstart = torch.tensor(starts, dtype=torch.int64, device=dev)
                 built.append((g, part, dtab, dstart, starts[-1]))
         self._built = built
+        # what the table points at: a parameter moved or re-allocated (model.to(...), load_state_dict into new
+        # storage, a group added) means a rebuild, never a write through a stale pointer
+        self._key = self._table_key()
+
+    def _table_key(self):
+        return tuple((id(p), p.data_ptr(), self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr())
+                     if p in self.state and "exp_avg" in self.state[p] else (id(p), p.data_ptr(), 0, 0)
+                     for g in self.param_groups for p in g["params"])
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -71,7 +80,7 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        if self._built is None:
+        if self._built is None or self._table_key() != self._key:
             self._build()
         stream = _lib.stream(self.step_count.device) if self.step_count is not None else None
         first = True

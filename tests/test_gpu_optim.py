@@ -93,3 +93,24 @@ def test_adam_captured_step_replays_like_eager():
     for a, b in zip(ps_g, ps_e):
         assert torch.equal(a, b)
     assert float(opt_g.step_count) == float(opt_e.step_count) == 4.0
+
+
+def test_adam_follows_moved_parameters():
+    """A parameter re-homed between steps (new storage, as after load_state_dict into fresh tensors or .to()):
+    the tensor table is rebuilt instead of written through a stale pointer, and the update stays torch's."""
+    init = _params([(64, 48), (48,)], 4)
+    grads = [[torch.randn_like(t) for t in init] for _ in range(3)]
+    res = []
+    for cls, kw in ((Adam, {}), (torch.optim.Adam, {"fused": True})):
+        ps = [torch.nn.Parameter(t.clone()) for t in init]
+        opt = cls(ps, lr=1e-3, **kw)
+        for k, sg in enumerate(grads):
+            if k == 1:
+                ps[0].data = ps[0].data.clone()  # new storage
+            for p, gr in zip(ps, sg):
+                p.grad = gr.clone()
+            opt.step()
+        torch.cuda.synchronize()
+        res.append([p.detach() for p in ps])
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, rtol=2e-6, atol=2e-7)
