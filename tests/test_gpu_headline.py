@@ -251,8 +251,8 @@ def test_fused_eval_head_matches_oracle_eval_mode():
 
 @pytest.mark.timeout(900)
 def test_timed_configuration_matches_eager_headline():
-    """The configuration bench.py times -- the C3 step (SparseConvUNet m=32, reps 2, residual, MultiLabel, fused
-    capturable Adam) on the 8-scene batches, metadata prefetched on the side stream, every split-bf16 weight image
+    """The configuration bench.py times -- the C3 step (SparseConvUNet m=32, reps 2, residual, MultiLabel, the
+    library's one-launch Adam, wsss3d.optim.Adam) on the 8-scene batches, metadata prefetched on the side stream, every split-bf16 weight image
     prepared in one launch, the whole step captured into a HIP graph (sparseconvnet.graphs.capture) and replayed --
     against the same steps launched eagerly with inline metadata and per-call weight splits (the path the oracle
     tests above pin): parameters, gradients and Adam moments bit-identical after two captured steps on two
@@ -267,7 +267,8 @@ def test_timed_configuration_matches_eager_headline():
     xs = [EasyDict(coords=torch.from_numpy(b["coords"]).to(DEV), feature=torch.from_numpy(b["feats"]).to(DEV),
                    batch_offsets=b["batch_offsets"]) for b in bs]
     ys = [torch.from_numpy(b["scene_labels"]).to(DEV) for b in bs]
-    opts = [torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=True) for m in (model, twin)]
+    from wsss3d.optim import Adam
+    opts = [Adam(m.parameters(), lr=1e-3) for m in (model, twin)]
     images = scn.weight_images.enable(twin, DEV, optimizer=opts[1])
 
     def body(m, opt, k, wi=None):
