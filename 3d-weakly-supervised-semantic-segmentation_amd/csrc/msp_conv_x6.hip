@@ -697,6 +697,65 @@ int launch_x6r_exp(int variant, const float* x, int c_in, const float* wt, int K
 }
 #endif
 
+// ---------------------------------------------------------------- one contribution per output row, split-bf16
+// msp_conv_pairs_x6 (round 6): the deconvolution forward and the strided convolution's backward-data -- every
+// output row has exactly one (source row, offset) pair -- on the x6 MFMAs instead of conv_pairs_kernel's exact
+// fp32 16x16x4 ones.  A wave takes one 16-pair chunk of one offset: lane (r, q) gathers pair r's source row at k
+// 8q .. +7 per 32-deep slice and splits it into three bf16 pieces, the offset's weight fragments come from the
+// per-call image (split_weights_kernel, NC = 16 NT, KS = 32: x6r's layout), and each 16 x 16 output tile is six
+// MFMAs per slice summed in a zeroed accumulator (the gather forms' order); lane (r, q) then holds output channels
+// 16 t + 4 q .. +3 of pair r and stores them as one float4.  conv_pairs_kernel's fp32 MFMA chain is 8 dependent
+// 32-cycle MFMAs per 32 input channels; here it is 6 of 16 cycles.
+template <int NT>
+__global__ __launch_bounds__(kThreads) void conv_pairs_x6_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int c_out,
+    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
+    const int64_t* __restrict__ chunk_start, int64_t n_chunks, int n_y, float* __restrict__ out) {
+  constexpr int NC = 16 * NT, WU = 3 * 4 * NC;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t chunk = (int64_t)blockIdx.x * kWaves + wave;
+  if (chunk >= n_chunks) return;  // wave-uniform; no block barrier
+  int lo = 0, hi = K;             // chunk_start[lo] <= chunk < chunk_start[hi]: the chunk's offset
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (chunk_start[mid] <= chunk) lo = mid;
+    else hi = mid;
+  }
+  const int o = lo, cy = blockIdx.y;
+  const int64_t p0 = off_start[o] + (chunk - chunk_start[o]) * MSP_CHUNK, p1 = off_start[o + 1];
+  const int r = lane & 15, q = lane >> 4;
+  const int src = p0 + r < p1 ? pin[p0 + r] : -1;
+  const int nkk = (c_in + 31) / 32;
+  const u32x4* wo = wimg + ((int64_t)o * n_y + cy) * nkk * WU + q * NC + r;
+  const float* xs = x + (int64_t)(src < 0 ? 0 : src) * c_in;
+  floatx4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int kk = 0; kk < nkk; ++kk) {
+    const int k = min(32 * kk + 8 * q, c_in - 8);  // past c_in: finite data times zero weights
+    floatx4 a = *reinterpret_cast<const floatx4*>(xs + k), b = *reinterpret_cast<const floatx4*>(xs + k + 4);
+    if (src < 0) a = b = floatx4{0.f, 0.f, 0.f, 0.f};
+    u32x4 xp[3];
+    split8(a, b, xp);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const u32x4 w0 = wo[kk * WU + 0 * 4 * NC + 16 * t], w1 = wo[kk * WU + 1 * 4 * NC + 16 * t],
+                  w2 = wo[kk * WU + 2 * 4 * NC + 16 * t];
+      floatx4 c = mfma_bf16(w2, xp[0], floatx4{0.f, 0.f, 0.f, 0.f});
+      c = mfma_bf16(w1, xp[1], c);
+      c = mfma_bf16(w0, xp[2], c);
+      c = mfma_bf16(w1, xp[0], c);
+      c = mfma_bf16(w0, xp[1], c);
+      acc[t] += mfma_bf16(w0, xp[0], c);
+    }
+  }
+  if (p0 + r < p1) {
+    float* dst = out + (int64_t)pout[p0 + r] * c_out + cy * NC + 4 * q;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(dst + 16 * t) = acc[t];
+  }
+}
+
 // ---------------------------------------------------------------- dense row groups
 // Submanifold convolutions on large levels, straight from the neighbour map
 // nbr[K][n] (int32, -1 absent): no tile rulebook and no LDS accumulation.
@@ -1233,6 +1292,33 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
 using namespace msp;
 
 extern "C" {
+
+size_t msp_conv_pairs_x6_workspace_size(int K, int c_in, int c_out) {
+  return (size_t)K * (size_t)c_out * (size_t)(ceil_div(c_in, 32) * 32) * 6;
+}
+
+int msp_conv_pairs_x6(const float* x, int c_in, const float* wt, int K, int c_out, const int32_t* pair_in,
+                      const int32_t* pair_out, const int64_t* off_start, const int64_t* chunk_start, int64_t n_chunks,
+                      float* out, void* ws, size_t ws_bytes, msp_stream_t stream) {
+  MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0 && K >= 1,
+              "msp_conv_pairs_x6: channels must be positive multiples of 16 (c_in=%d c_out=%d)", c_in, c_out);
+  MSP_REQUIRE(ws && ws_bytes >= msp_conv_pairs_x6_workspace_size(K, c_in, c_out),
+              "msp_conv_pairs_x6: workspace too small");
+  if (n_chunks == 0) return MSP_OK;
+  hipStream_t s = as_stream(stream);
+  const int NT = (c_out / 16) % 2 == 0 ? 2 : 1, NC = 16 * NT, n_y = c_out / NC;
+  u32x4* img = static_cast<u32x4*>(ws);
+  const int64_t units = (int64_t)msp_conv_pairs_x6_workspace_size(K, c_in, c_out) / 16;
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, NC, 32, img, 0);
+  dim3 grid((unsigned)ceil_div(n_chunks, kWaves), (unsigned)n_y);
+  if (NT == 2)
+    conv_pairs_x6_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, img, K, c_out, pair_in, pair_out, off_start,
+                                                      chunk_start, n_chunks, n_y, out);
+  else
+    conv_pairs_x6_kernel<1><<<grid, kThreads, 0, s>>>(x, c_in, img, K, c_out, pair_in, pair_out, off_start,
+                                                      chunk_start, n_chunks, n_y, out);
+  return check_launch("msp_conv_pairs_x6");
+}
 
 // Dense row-group form on the large levels with c_out >= 64 (measured against msp_conv_tile on the headline
 // batch, profiles/r01/kbench_nbr_r01v.log: L0 32->64 -13 %, L1 64->64 -3 %, L2 96->96 -9 %, 192->96 -6 %; the

@@ -89,6 +89,8 @@ PROTOTYPES = {
     "msp_bn_bwd_apply": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P]),
     "msp_bn_bwd_apply_add": (I, [P, P, I64, I, P, P, P, F, I, P, P, P, P, P]),
     "msp_bn_bwd_apply_split": (I, [P, P, I64, I, P, P, P, F, I, P, I, P, P, P, P, P]),
+    "msp_conv_pairs_x6_workspace_size": (SZ, [I, I, I]),
+    "msp_conv_pairs_x6": (I, [P, I, P, I, I, P, P, P, P, I64, P, P, SZ, P]),
     "msp_adam_chunks": (I64, [I64]),
     "msp_adam_step": (I, [P, P, P, I, I64, P, I, D, D, D, D, D, P]),
     "msp_add_bn_stats": (I, [P, P, I64, I, P, P, P]),

@@ -238,15 +238,29 @@ def conv_local(x, wt, K, flip, c_out, rules, n_rows, kind="conv_local", flops=0,
     return out[:n_rows]
 
 
+# One contribution per output row (deconvolution forward, strided backward-data) on the split-bf16 MFMAs
+# (msp_conv_pairs_x6, round 6) instead of the exact fp32 16x16x4 MFMA chains of msp_conv_pairs.
+PAIRS_X6 = os.environ.get("MI3DSPARSE_PAIRS_X6", "1") == "1"
+PAIRS_FORM = "x6" if PAIRS_X6 else "f32"
+
+
 def conv_pairs(x, wt, K, c_out, pairs, pin, pout, n_out, kind="pairs", flops=0):
+    """out[pout[p]] = wt[o]^T x[pin[p]] (wt [K][c_out][c_in]), one pair per output row."""
     out = torch.empty((max(n_out, 1), c_out), dtype=torch.float32, device=x.device)
     if pairs.n_chunks:
         c_in = x.size(1)
         # compulsory bytes: source rows, output rows, weights, the pair lists
         nbytes = 4 * (x.size(0) * c_in + n_out * c_out + K * c_in * c_out) + 8 * pairs.total
-        _record(kind + "/f32", flops, lambda: call(
-            "msp_conv_pairs", ptr(x), c_in, ptr(wt), K, c_out, ptr(pin), ptr(pout), ptr(pairs.off_start),
-            ptr(pairs.chunk_start), pairs.n_chunks, ptr(out), _stream(x)), nbytes)
+        if PAIRS_X6 and c_in % 16 == 0 and c_out % 16 == 0:
+            wsb = int(_lib.query("msp_conv_pairs_x6_workspace_size", K, c_in, c_out))
+            ws = torch.empty(max(wsb, 16) // 4 + 4, dtype=torch.float32, device=x.device)
+            _record(kind + "/x6", flops, lambda: call(
+                "msp_conv_pairs_x6", ptr(x), c_in, ptr(wt), K, c_out, ptr(pin), ptr(pout), ptr(pairs.off_start),
+                ptr(pairs.chunk_start), pairs.n_chunks, ptr(out), ptr(ws), wsb, _stream(x)), nbytes)
+        else:
+            _record(kind + "/f32", flops, lambda: call(
+                "msp_conv_pairs", ptr(x), c_in, ptr(wt), K, c_out, ptr(pin), ptr(pout), ptr(pairs.off_start),
+                ptr(pairs.chunk_start), pairs.n_chunks, ptr(out), _stream(x)), nbytes)
     return out[:n_out]
 
 

@@ -307,6 +307,12 @@ int msp_dense_order(const int32_t* nbr, int K, int64_t n, int log2_window, int32
 int msp_conv_pairs(const float* x, int c_in, const float* wt, int K, int c_out, const int32_t* pair_in,
                    const int32_t* pair_out, const int64_t* off_start, const int64_t* chunk_start,
                    int64_t n_chunks, float* out, msp_stream_t stream);
+/* msp_conv_pairs_x6 (round 6, ABI 10): the same on the split-bf16 MFMAs (fp32-class, as the other x6 forms) with
+ * wt given as [K][c_out][c_in]; ws (>= msp_conv_pairs_x6_workspace_size bytes) receives the call's weight image. */
+size_t msp_conv_pairs_x6_workspace_size(int K, int c_in, int c_out);
+int msp_conv_pairs_x6(const float* x, int c_in, const float* wt, int K, int c_out, const int32_t* pair_in,
+                      const int32_t* pair_out, const int64_t* off_start, const int64_t* chunk_start, int64_t n_chunks,
+                      float* out, void* ws, size_t ws_bytes, msp_stream_t stream);
 /* Weight gradient dW[o] (c_in x c_out) = sum over pairs of offset o of
  * x[pair_in]^T dy[pair_out].  Each offset's pair list (sorted by one side's
  * row) is cut into n_pieces equal pieces; piece j of every offset covers

@@ -18,7 +18,7 @@ import pytest
 import torch
 
 import sparseconvnet as scn  # noqa: F401
-from sparseconvnet import _lib
+from sparseconvnet import _lib, ops
 from oracle.encoders import OracleEncoder
 from oracle.parity import run_shared_masks
 from wsss3d import EasyDict, MODEL_REGISTRY
@@ -98,7 +98,7 @@ def test_headline_unet_full_size_parity():
     kinds = _run("SparseConvUNet", 32, 2, True, 2,
                  need=["subm_fwd/x6r", "subm_fwd/x6s", "subm_bwd_data/x6s", "subm_fwd/x6d",
                        "nin_fwd/f32", "nin_bwd_data/f32", "nin_fwd/x6", "nin_bwd_data/x6", "wgrad_strided/x6", "wgrad_deconv/x6", "wgrad/x6c", "nin_wgrad/x6", "conv_fwd/x6d",
-                       "deconv_fwd/f32", "subm_fwd/f32n", "wgrad/f32n"])
+                       "deconv_fwd/" + ops.PAIRS_FORM, "subm_fwd/f32n", "wgrad/f32n"])
     assert kinds["subm_fwd/x6s"] >= 4
 
 

@@ -28,7 +28,7 @@ import torch
 import torch.nn.functional as F
 
 import sparseconvnet as scn  # noqa: F401
-from sparseconvnet import _lib
+from sparseconvnet import _lib, ops
 from oracle import scn_oracle as O
 from oracle.encoders import OracleEncoder
 from oracle.parity import raster_perm, run_shared_masks
@@ -131,7 +131,7 @@ def test_headline_batch_logits_parity():
           f"max |logit| {logits_o.abs().max().item():.3e}); worst per-layer relative error {worst_layer:.2e}")
     assert err <= LOGIT_BAR, f"C3 per-point logits: {err:.3e} > {LOGIT_BAR}"
     need = ["subm_fwd/x6r", "subm_fwd/x6s", "subm_fwd/x6d", "subm_fwd/f32n", "nin_fwd/f32", "nin_fwd/x6",
-            "conv_fwd/x6d", "deconv_fwd/f32", "logits_fwd"]
+            "conv_fwd/x6d", "deconv_fwd/" + ops.PAIRS_FORM, "logits_fwd"]
     got = {k.split("/")[0] if k.startswith("logits_fwd") else k for k in rec.kinds}
     missing = [k for k in need if k not in got]
     assert not missing, f"production forms that did not run: {missing} (ran: {sorted(rec.kinds)})"
@@ -212,7 +212,7 @@ def test_headline_batch_backward_parity():
         assert e <= 1e-3 * scale + 1e-9, f"grad {key}: {e:.3e} vs scale {scale:.3e}"
     print(f"C3 backward: {n} parameter gradients, worst max err / tensor max {worst:.3e} (bar 1e-3)")
     need = ["subm_bwd_data/x6r", "subm_bwd_data/x6s", "wgrad/x6c", "wgrad_strided/x6", "wgrad_deconv/x6", "nin_wgrad/x6",
-            "wgrad/f32n", "conv_bwd_data/f32", "deconv_bwd_data/x6d", "bn_bwd/hbm"]
+            "wgrad/f32n", "conv_bwd_data/" + ops.PAIRS_FORM, "deconv_bwd_data/x6d", "bn_bwd/hbm"]
     missing = [k for k in need if k not in rec.kinds]
     assert not missing, f"production forms that did not run: {missing} (ran: {sorted(rec.kinds)})"
 

@@ -224,7 +224,8 @@ def test_conv_pairs_runs_cross_offsets(cin, cout):
     """msp_conv_pairs at a size where a wave takes a run of chunks with the weights in registers (c_in <= 64),
     runs crossing from one offset into the next and over an empty offset, against fp64: every output row has one
     contribution, W[o]^T x[pin], as the deconvolution forward and the strided backward-data have.  c_in = 96 and
-    160 take the one-chunk form.  The library's f32 MFMA products are exact, so 1e-5 is the fp32 accumulation."""
+    160 take the one-chunk form.  The library's f32 MFMA products are exact, so 1e-5 is the fp32 accumulation; the
+    split-bf16 form (msp_conv_pairs_x6, the production path since round 6) is held to the same bar."""
     from sparseconvnet import _lib
     g = torch.Generator().manual_seed(cin + cout)
     K, n_out, n_in = 8, 300_000, 50_000
@@ -254,6 +255,14 @@ def test_conv_pairs_runs_cross_offsets(cin, cout):
         a, b = int(starts[o]), int(starts[o + 1])
         ref[pout[a:b].long()] = x[pin[a:b].long()].double() @ wt[o].double().t()
     close(out, ref, 1e-5, f"conv_pairs {cin}->{cout}")
+    # the split-bf16 form (msp_conv_pairs_x6): three-piece products, one zeroed accumulator per 32-deep slice
+    wsb = int(_lib.query("msp_conv_pairs_x6_workspace_size", K, cin, cout))
+    ws = torch.empty(wsb // 4 + 4, dtype=torch.float32, device=DEV)
+    out6 = torch.full((n_out, cout), float("nan"), device=DEV)
+    _lib.call("msp_conv_pairs_x6", dx.data_ptr(), cin, dwt.data_ptr(), K, cout, dpin.data_ptr(), dpout.data_ptr(),
+              dst.data_ptr(), dcs.data_ptr(), n_chunks, out6.data_ptr(), ws.data_ptr(), wsb, _lib.stream())
+    torch.cuda.synchronize()
+    close(out6, ref, 1e-5, f"conv_pairs_x6 {cin}->{cout}")
 
 
 @pytest.mark.parametrize("C,leak,train,mu,sd", [(32, 0.0, True, 1.5, 3.0), (48, 0.333, True, 1.5, 3.0),
