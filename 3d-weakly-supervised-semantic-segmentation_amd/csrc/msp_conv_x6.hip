@@ -756,6 +756,130 @@ __global__ __launch_bounds__(kThreads) void conv_pairs_x6_kernel(
   }
 }
 
+// The same over a run of consecutive chunks per wave (c_in <= 32 KK): the next chunk's x rows are loaded and the
+// indices two chunks ahead read while the current chunk's MFMAs and stores run (the latency chain index -> row
+// gather -> MFMA -> scattered store is what bounds the one-chunk form: 2.5 TB/s and 43 TF/s at level 0).  WREG
+// keeps the offset's weight fragments in registers across the run (reloaded when the run crosses an offset).
+template <int NT, int KK, bool WREG>
+__global__ __launch_bounds__(kThreads) void conv_pairs_x6_pipe_kernel(
+    const float* __restrict__ x, int c_in, const u32x4* __restrict__ wimg, int K, int c_out,
+    const int32_t* __restrict__ pin, const int32_t* __restrict__ pout, const int64_t* __restrict__ off_start,
+    const int64_t* __restrict__ chunk_start, int64_t n_chunks, int run, int n_y, float* __restrict__ out) {
+  constexpr int NC = 16 * NT, WU = 3 * 4 * NC;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t ch0 = ((int64_t)blockIdx.x * kWaves + wave) * run;
+  if (ch0 >= n_chunks) return;  // wave-uniform; no block barrier
+  const int64_t ch1 = ch0 + run < n_chunks ? ch0 + run : n_chunks;
+  const int cy = blockIdx.y, r = lane & 15, q = lane >> 4;
+  const int nkk = (c_in + 31) / 32;
+  int oi = 0, hi = K;  // chunk_start[oi] <= ch0 < chunk_start[hi]
+  while (hi - oi > 1) {
+    const int mid = (oi + hi) >> 1;
+    if (chunk_start[mid] <= ch0) oi = mid;
+    else hi = mid;
+  }
+  int64_t oi_first = chunk_start[oi], oi_end = chunk_start[oi + 1], pb = off_start[oi], pe = off_start[oi + 1];
+  auto indices = [&](int64_t ch, int& src, int& dst, int& o_of) {
+    if (ch >= oi_end) {
+      do {
+        ++oi;
+        oi_end = chunk_start[oi + 1];
+      } while (ch >= oi_end);
+      oi_first = chunk_start[oi];
+      pb = off_start[oi];
+      pe = off_start[oi + 1];
+    }
+    const int64_t p = pb + (ch - oi_first) * MSP_CHUNK + r;
+    src = p < pe ? pin[p] : -1;
+    dst = p < pe ? pout[p] : -1;
+    o_of = oi;
+  };
+  auto load_x = [&](int src, floatx4 (&a)[KK][2]) {
+    const float* xs = x + (int64_t)(src < 0 ? 0 : src) * c_in;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      if (kk < nkk) {
+        const int k = min(32 * kk + 8 * q, c_in - 8);  // past c_in: finite data times zero weights
+        a[kk][0] = *reinterpret_cast<const floatx4*>(xs + k);
+        a[kk][1] = *reinterpret_cast<const floatx4*>(xs + k + 4);
+      }
+  };
+  u32x4 w[WREG ? KK : 1][NT][3];
+  int ow = -1;
+  int s_c, d_c, o_c, s_n = -1, d_n = -1, o_n = 0;
+  floatx4 a[KK][2];
+  indices(ch0, s_c, d_c, o_c);
+  load_x(s_c, a);
+  if (ch0 + 1 < ch1) indices(ch0 + 1, s_n, d_n, o_n);
+  for (int64_t ch = ch0; ch < ch1; ++ch) {
+    const u32x4* wo = wimg + ((int64_t)o_c * n_y + cy) * nkk * WU + q * NC + r;
+    if (WREG && o_c != ow) {
+      ow = o_c;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        if (kk < nkk) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) w[WREG ? kk : 0][t][j] = wo[kk * WU + j * 4 * NC + 16 * t];
+        }
+    }
+    const bool more = ch + 1 < ch1;
+    floatx4 an[KK][2];
+    if (more) load_x(s_n, an);
+    int s2 = -1, d2 = -1, o2 = o_n;
+    if (ch + 2 < ch1) indices(ch + 2, s2, d2, o2);
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      if (kk < nkk) {
+        floatx4 lo = a[kk][0], hi4 = a[kk][1];
+        if (s_c < 0) lo = hi4 = floatx4{0.f, 0.f, 0.f, 0.f};
+        u32x4 xp[3];
+        split8(lo, hi4, xp);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          u32x4 w0, w1, w2;
+          if (WREG) {
+            w0 = w[WREG ? kk : 0][t][0];
+            w1 = w[WREG ? kk : 0][t][1];
+            w2 = w[WREG ? kk : 0][t][2];
+          } else {
+            w0 = wo[kk * WU + 0 * 4 * NC + 16 * t];
+            w1 = wo[kk * WU + 1 * 4 * NC + 16 * t];
+            w2 = wo[kk * WU + 2 * 4 * NC + 16 * t];
+          }
+          floatx4 c = mfma_bf16(w2, xp[0], floatx4{0.f, 0.f, 0.f, 0.f});
+          c = mfma_bf16(w1, xp[1], c);
+          c = mfma_bf16(w0, xp[2], c);
+          c = mfma_bf16(w1, xp[0], c);
+          c = mfma_bf16(w0, xp[1], c);
+          acc[t] += mfma_bf16(w0, xp[0], c);
+        }
+      }
+    if (d_c >= 0) {
+      float* dst = out + (int64_t)d_c * c_out + cy * NC + 4 * q;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) *reinterpret_cast<floatx4*>(dst + 16 * t) = acc[t];
+    }
+    if (more) {
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        a[kk][0] = an[kk][0];
+        a[kk][1] = an[kk][1];
+      }
+      s_c = s_n;
+      d_c = d_n;
+      o_c = o_n;
+      s_n = s2;
+      d_n = d2;
+      o_n = o2;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- dense row groups
 // Submanifold convolutions on large levels, straight from the neighbour map
 // nbr[K][n] (int32, -1 absent): no tile rulebook and no LDS accumulation.
@@ -1287,6 +1411,46 @@ int launch_x6(const PlanX6& p, const float* x, int c_in, const float* wt, int K,
   return MSP_OK;
 }
 
+#ifndef MSP_PAIRS_X6_FORM
+#define MSP_PAIRS_X6_FORM 2  // runs with the weights in registers: profiles/r06/pairs_bench_r06pb.log
+#endif
+
+// form % 10: 0 one chunk per wave, 1 runs of chunks (c_in <= 128), 2 runs with the weights in registers; form / 10:
+// the waves the runs are sized for (x 1024; 0 = 8192)
+void launch_pairs_x6(int form, const float* x, int c_in, const u32x4* img, int K, int c_out, const int32_t* pair_in,
+                     const int32_t* pair_out, const int64_t* off_start, const int64_t* chunk_start, int64_t n_chunks,
+                     float* out, hipStream_t s) {
+  const int NT = (c_out / 16) % 2 == 0 ? 2 : 1, n_y = c_out / (16 * NT);
+  const int kind = form % 10;
+  if (kind != 0 && c_in <= 128) {
+    const int64_t waves = form / 10 ? (int64_t)(form / 10) * 1024 : 8192;
+    int64_t run = n_chunks * n_y / waves;
+    run = run < 1 ? 1 : run > 16 ? 16 : run;
+    dim3 grid((unsigned)ceil_div(ceil_div(n_chunks, run), kWaves), (unsigned)n_y);
+#define PIPE(N, KK, WR)                                                                                          \
+  conv_pairs_x6_pipe_kernel<N, KK, WR><<<grid, kThreads, 0, s>>>(x, c_in, img, K, c_out, pair_in, pair_out,     \
+                                                                off_start, chunk_start, n_chunks, (int)run, n_y, \
+                                                                out)
+    const bool wr = kind == 2;
+    if (c_in <= 64) {
+      if (NT == 2) { if (wr) PIPE(2, 2, true); else PIPE(2, 2, false); }
+      else { if (wr) PIPE(1, 2, true); else PIPE(1, 2, false); }
+    } else {
+      if (NT == 2) { if (wr) PIPE(2, 4, true); else PIPE(2, 4, false); }
+      else { if (wr) PIPE(1, 4, true); else PIPE(1, 4, false); }
+    }
+#undef PIPE
+    return;
+  }
+  dim3 grid((unsigned)ceil_div(n_chunks, kWaves), (unsigned)n_y);
+  if (NT == 2)
+    conv_pairs_x6_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, img, K, c_out, pair_in, pair_out, off_start,
+                                                      chunk_start, n_chunks, n_y, out);
+  else
+    conv_pairs_x6_kernel<1><<<grid, kThreads, 0, s>>>(x, c_in, img, K, c_out, pair_in, pair_out, off_start,
+                                                      chunk_start, n_chunks, n_y, out);
+}
+
 }  // namespace msp
 
 using namespace msp;
@@ -1306,17 +1470,12 @@ int msp_conv_pairs_x6(const float* x, int c_in, const float* wt, int K, int c_ou
               "msp_conv_pairs_x6: workspace too small");
   if (n_chunks == 0) return MSP_OK;
   hipStream_t s = as_stream(stream);
-  const int NT = (c_out / 16) % 2 == 0 ? 2 : 1, NC = 16 * NT, n_y = c_out / NC;
+  const int NT = (c_out / 16) % 2 == 0 ? 2 : 1, NC = 16 * NT;
   u32x4* img = static_cast<u32x4*>(ws);
   const int64_t units = (int64_t)msp_conv_pairs_x6_workspace_size(K, c_in, c_out) / 16;
   split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, NC, 32, img, 0);
-  dim3 grid((unsigned)ceil_div(n_chunks, kWaves), (unsigned)n_y);
-  if (NT == 2)
-    conv_pairs_x6_kernel<2><<<grid, kThreads, 0, s>>>(x, c_in, img, K, c_out, pair_in, pair_out, off_start,
-                                                      chunk_start, n_chunks, n_y, out);
-  else
-    conv_pairs_x6_kernel<1><<<grid, kThreads, 0, s>>>(x, c_in, img, K, c_out, pair_in, pair_out, off_start,
-                                                      chunk_start, n_chunks, n_y, out);
+  launch_pairs_x6(MSP_PAIRS_X6_FORM, x, c_in, img, K, c_out, pair_in, pair_out, off_start, chunk_start, n_chunks,
+                  out, s);
   return check_launch("msp_conv_pairs_x6");
 }
 
@@ -1356,6 +1515,22 @@ int msp_conv_nbr(const float* x, int c_in, const float* wt, int K, int flip, int
 }
 
 #ifdef MSP_EXPERIMENTS
+int msp_exp_conv_pairs_x6(int variant, const float* x, int c_in, const float* wt, int K, int c_out,
+                          const int32_t* pair_in, const int32_t* pair_out, const int64_t* off_start,
+                          const int64_t* chunk_start, int64_t n_chunks, float* out, void* ws, size_t ws_bytes,
+                          msp_stream_t stream) {
+  MSP_REQUIRE(c_in > 0 && c_in % 16 == 0 && c_out > 0 && c_out % 16 == 0 && K >= 1, "msp_exp_conv_pairs_x6: shape");
+  MSP_REQUIRE(ws && ws_bytes >= msp_conv_pairs_x6_workspace_size(K, c_in, c_out), "msp_exp_conv_pairs_x6: ws");
+  if (n_chunks == 0) return MSP_OK;
+  hipStream_t s = as_stream(stream);
+  const int NT = (c_out / 16) % 2 == 0 ? 2 : 1;
+  u32x4* img = static_cast<u32x4*>(ws);
+  const int64_t units = (int64_t)msp_conv_pairs_x6_workspace_size(K, c_in, c_out) / 16;
+  split_weights_kernel<<<(unsigned)ceil_div(units, 256), 256, 0, s>>>(wt, K, c_out, c_in, 16 * NT, 32, img, 0);
+  launch_pairs_x6(variant, x, c_in, img, K, c_out, pair_in, pair_out, off_start, chunk_start, n_chunks, out, s);
+  return check_launch("msp_exp_conv_pairs_x6");
+}
+
 int msp_exp_conv_x6r(int variant, const float* x, int c_in, const float* wt, int K, int flip, int c_out,
                      int tile_rows, const int64_t* tile_start, const uint8_t* chunk_off, const int32_t* chunk_src,
                      const uint16_t* chunk_row, int64_t n_rows, float* out, void* ws, size_t ws_bytes,
