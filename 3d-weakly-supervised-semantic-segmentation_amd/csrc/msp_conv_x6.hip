@@ -34,6 +34,8 @@
 #include "msp_x6.h"
 #include "msp_bn_epi.h"
 
+#include <cstdlib>
+
 namespace msp {
 
 // wt [K][c_out][c_in] fp32 -> the per-step LDS images of conv_x6d_kernel:
@@ -1354,7 +1356,15 @@ PlanX6 plan_x6(int64_t n_rows, int c_out) {
   }
   p.n_y = n16 / p.nt;
   const int64_t blocks = n_tiles * p.n_y;
-  const int64_t target = n_tiles <= 8 ? 2048 : 1024, cap = n_tiles <= 8 ? 16 : 8;
+  int64_t target = n_tiles <= 8 ? 2048 : 1024, cap = n_tiles <= 8 ? 16 : 8;
+#ifdef MSP_EXPERIMENTS  // split sweeps (scripts/kbench.py): MSP_X6D_SPLIT="target_small,cap_small,target,cap"
+  if (const char* e = getenv("MSP_X6D_SPLIT")) {
+    long v[4] = {2048, 16, 1024, 8};
+    sscanf(e, "%ld,%ld,%ld,%ld", &v[0], &v[1], &v[2], &v[3]);
+    target = n_tiles <= 8 ? v[0] : v[2];
+    cap = n_tiles <= 8 ? v[1] : v[3];
+  }
+#endif
   if (blocks < target) {
     const int64_t sp = (target + blocks - 1) / blocks;
     p.split = (int)(sp > cap ? cap : sp);
