@@ -265,6 +265,51 @@ def test_conv_pairs_runs_cross_offsets(cin, cout):
     close(out6, ref, 1e-5, f"conv_pairs_x6 {cin}->{cout}")
 
 
+@pytest.mark.parametrize("cin,cout,K,counts", [
+    (16, 16, 1, [1]),                       # one pair, one offset
+    (32, 48, 8, [0, 17, 0, 0, 33, 1, 0, 16]),  # empty offsets first and between, partial chunks (NT = 1 of 3 tiles)
+    (144, 48, 8, [5, 0, 40, 3, 0, 0, 70, 2]),  # c_in > 128: one chunk per wave; 144 = 4.5 slices (zero-padded k)
+    (128, 80, 27, None),                      # c_in = 128 (four slices in registers), c_out 80 (NT = 1, 5 column tiles)
+])
+def test_conv_pairs_x6_edges(cin, cout, K, counts):
+    """msp_conv_pairs_x6 at the edges of its forms against fp64 (1e-5 of the max): a single pair, empty offsets at
+    the start and between (a wave's run crosses them), partial last chunks, c_in past the register-run form's 128,
+    and column tiles of 16 (odd c_out / 16).  Output rows no pair names stay untouched (NaN sentinel)."""
+    from sparseconvnet import _lib
+    g = torch.Generator().manual_seed(cin * 7 + cout + K)
+    if counts is None:
+        counts = torch.randint(0, 400, (K,), generator=g).tolist()
+    counts = torch.tensor(counts, dtype=torch.int64)
+    n_pairs = int(counts.sum())
+    n_out, n_in = n_pairs + 37, max(n_pairs // 2, 1) + 5
+    starts = torch.zeros(K + 1, dtype=torch.int64)
+    starts[1:] = counts.cumsum(0)
+    pout = torch.randperm(n_out, generator=g)[:n_pairs].int()
+    pin = torch.randint(0, n_in, (n_pairs,), generator=g).int()
+    chunk_start = torch.zeros(K + 1, dtype=torch.int64)
+    chunk_start[1:] = ((counts + 15) // 16).cumsum(0)
+    n_chunks = int(chunk_start[-1])
+    x = torch.randn(n_in, cin, generator=g)
+    wt = torch.randn(K, cout, cin, generator=g)
+    wsb = int(_lib.query("msp_conv_pairs_x6_workspace_size", K, cin, cout))
+    ws = torch.empty(wsb // 4 + 4, dtype=torch.float32, device=DEV)
+    out = torch.full((n_out, cout), float("nan"), device=DEV)
+    dx, dwt, dpin, dpout = x.to(DEV), wt.to(DEV), pin.to(DEV), pout.to(DEV)
+    dst, dcs = starts.to(DEV), chunk_start.to(DEV)
+    _lib.call("msp_conv_pairs_x6", dx.data_ptr(), cin, dwt.data_ptr(), K, cout, dpin.data_ptr(), dpout.data_ptr(),
+              dst.data_ptr(), dcs.data_ptr(), n_chunks, out.data_ptr(), ws.data_ptr(), wsb, _lib.stream())
+    torch.cuda.synchronize()
+    ref = torch.full((n_out, cout), float("nan"), dtype=torch.float64)
+    for o in range(K):
+        a, b = int(starts[o]), int(starts[o + 1])
+        ref[pout[a:b].long()] = x[pin[a:b].long()].double() @ wt[o].double().t()
+    named = torch.zeros(n_out, dtype=torch.bool)
+    named[pout.long()] = True
+    o_cpu = out.double().cpu()
+    assert torch.isnan(o_cpu[~named]).all(), "rows no pair names were written"
+    close(o_cpu[named], ref[named], 1e-5, f"conv_pairs_x6 edges {cin}->{cout} K={K}")
+
+
 @pytest.mark.parametrize("C,leak,train,mu,sd", [(32, 0.0, True, 1.5, 3.0), (48, 0.333, True, 1.5, 3.0),
                                                 (896, 0.0, True, 1.5, 3.0), (16, 0.0, False, 1.5, 3.0),
                                                 (32, 0.0, True, 10.0, 0.01)])
