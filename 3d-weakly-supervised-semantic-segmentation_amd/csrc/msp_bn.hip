@@ -24,7 +24,10 @@
 namespace msp {
 
 constexpr int kT = 256;
-constexpr int64_t kMaxParts = 1024;
+#ifndef MSP_BN_MAX_PARTS
+#define MSP_BN_MAX_PARTS 1024
+#endif
+constexpr int64_t kMaxParts = MSP_BN_MAX_PARTS;
 
 // Partial-sum blocks: two 4-deep passes of the vector form per block (R = 1024 / C rows per pass, so
 // 8 R rows per block, 16..256), at most kMaxParts.  Sized by C so the small levels (C up to 448, a few
