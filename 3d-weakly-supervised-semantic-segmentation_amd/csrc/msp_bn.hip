@@ -28,6 +28,9 @@ constexpr int kT = 256;
 #define MSP_BN_MAX_PARTS 1024
 #endif
 constexpr int64_t kMaxParts = MSP_BN_MAX_PARTS;
+#ifndef MSP_BN_UNROLL  // bn_reduce4's rows in flight per thread (experiments: 8)
+#define MSP_BN_UNROLL 4
+#endif
 
 // Partial-sum blocks: two 4-deep passes of the vector form per block (R = 1024 / C rows per pass, so
 // 8 R rows per block, 16..256), at most kMaxParts.  Sized by C so the small levels (C up to 448, a few
@@ -121,13 +124,14 @@ __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict_
       return e;
     };
     int64_t v = v0 + ro;
+    constexpr int U = MSP_BN_UNROLL;  // rows in flight per thread and tensor
     if (MODE == 3) {
-      for (; v + 3 * R < v1; v += 4 * R) {
-        float4 e[4];
+      for (; v + (U - 1) * R < v1; v += U * R) {
+        float4 e[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) e[u] = src4[(v + u * R) * sc4 + soff];
+        for (int u = 0; u < U; ++u) e[u] = src4[(v + u * R) * sc4 + soff];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           s4[(v + u * R) * C4 + c4] = e[u];
           term(e[u], e[u]);
         }
@@ -138,15 +142,15 @@ __global__ __launch_bounds__(kT) void bn_reduce4_kernel(const float* __restrict_
       }
     }
     if (MODE != 3) {
-    for (; v + 3 * R < v1; v += 4 * R) {
-      float4 xa[4], ga[4];
+    for (; v + (U - 1) * R < v1; v += U * R) {
+      float4 xa[U], ga[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         xa[u] = x4[(v + u * R) * C4 + c4];
         if (MODE != 0) ga[u] = g4[(v + u * R) * C4 + c4];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         if (MODE == 2) {
           const float4 sm = join((v + u * R) * C4 + c4, xa[u], ga[u]);
           term(sm, sm);
